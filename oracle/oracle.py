@@ -1,0 +1,287 @@
+"""Python face of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this, and only
+as the checker / CPU baseline. The product package (0xfec_amd/) never imports it.
+
+Two layers:
+  1. ctypes bindings to oracle/_build/liboracle.so (fec_oracle.c): klauspost-v1.12.4
+     Encode / ReconstructData and the XOR byte loops over whole batches of equal-length shards.
+  2. A restatement of the reference's scheme layer (the Go code above the codec) over plain
+     Python dicts, with the same error ordering and output framing:
+       reedSolomonScheme.repairSymbols          internal/fec/reed_solomon.go:26-68
+       addLengthToSourceSymbolPayload           internal/fec/reed_solomon.go:70-89
+       reedSolomonScheme.recoverSymbolPayloads  internal/fec/reed_solomon.go:92-136
+       xorScheme.repairSymbols / xor            internal/fec/xor.go:14-56
+       xorScheme.recoverSymbolPayloads          internal/fec/xor.go:66-104
+       block.isRecoverable / isComplete         internal/fec/block.go:88-95
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+
+MAX_PACKET_BUFFER_SIZE = 1452      # internal/protocol/protocol.go:111
+MAX_FEC_PACKET_BUFFER_SIZE = 1434  # internal/protocol/protocol.go:136-138
+REPAIR_PAYLOAD_METADATA_LEN = 2    # internal/protocol/protocol.go:140
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u8p = ctypes.c_void_p
+        sz = ctypes.c_size_t
+        L.fo_gf_mul.restype = ctypes.c_uint8
+        L.fo_gf_mul.argtypes = [ctypes.c_uint8, ctypes.c_uint8]
+        L.fo_gf_div.restype = ctypes.c_uint8
+        L.fo_gf_div.argtypes = [ctypes.c_uint8, ctypes.c_uint8]
+        L.fo_build_matrix.argtypes = [ctypes.c_int, ctypes.c_int, u8p]
+        L.fo_invert.argtypes = [ctypes.c_int, u8p]
+        L.fo_rs_encode_batch.argtypes = [ctypes.c_int, ctypes.c_int, sz, sz, u8p, sz, u8p, sz, sz, ctypes.c_int]
+        L.fo_rs_reconstruct_batch.argtypes = [ctypes.c_int, ctypes.c_int, sz, sz, u8p, sz, sz, u8p, u8p, ctypes.c_int]
+        L.fo_xor_encode_batch.argtypes = [ctypes.c_int, sz, sz, u8p, sz, u8p, sz, sz, ctypes.c_int]
+        L.fo_xor_reconstruct_batch.argtypes = [ctypes.c_int, sz, sz, u8p, sz, sz, u8p, u8p, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def gf_mul(a, b):
+    return lib().fo_gf_mul(a, b)
+
+
+def build_matrix(k, n):
+    out = np.zeros((n, k), dtype=np.uint8)
+    if lib().fo_build_matrix(k, n, _ptr(out)) != 0:
+        raise ValueError("bad shape")
+    return out
+
+
+def invert(m):
+    m = np.ascontiguousarray(m, dtype=np.uint8).copy()
+    if lib().fo_invert(m.shape[0], _ptr(m)) != 0:
+        raise ValueError("singular")
+    return m
+
+
+# ---------------------------------------------------------------- batched codec (layer 1)
+
+def rs_encode(k, m, shards, threads=0):
+    """shards: uint8 [B, n, S] (S >= shard length). Fills shards[:, k:, :] in place from
+    shards[:, :k, :] over the full S bytes. Returns shards."""
+    B, n, S = shards.shape
+    assert n == k + m and shards.flags.c_contiguous
+    base = shards.ctypes.data
+    rc = lib().fo_rs_encode_batch(k, m, S, B, ctypes.c_void_p(base), n * S,
+                                  ctypes.c_void_p(base + k * S), n * S, S, threads)
+    assert rc == 0
+    return shards
+
+
+def rs_reconstruct(k, m, shards, masks, threads=0, length=None):
+    """In place klauspost ReconstructData on uint8 [B, n, S] with uint32 present masks [B].
+    Returns per-block status (0 ok, -1 too few shards)."""
+    B, n, S = shards.shape
+    assert n == k + m and shards.flags.c_contiguous
+    masks = np.ascontiguousarray(masks, dtype=np.uint32)
+    status = np.zeros(B, dtype=np.int32)
+    lib().fo_rs_reconstruct_batch(k, m, S if length is None else length, B, _ptr(shards), n * S, S,
+                                  _ptr(masks), _ptr(status), threads)
+    return status
+
+
+def xor_encode(k, shards, threads=0):
+    B, n, S = shards.shape
+    assert n == k + 1 and shards.flags.c_contiguous
+    base = shards.ctypes.data
+    assert lib().fo_xor_encode_batch(k, S, B, ctypes.c_void_p(base), n * S,
+                                     ctypes.c_void_p(base + k * S), n * S, S, threads) == 0
+    return shards
+
+
+def xor_reconstruct(k, shards, masks, threads=0):
+    B, n, S = shards.shape
+    assert n == k + 1 and shards.flags.c_contiguous
+    masks = np.ascontiguousarray(masks, dtype=np.uint32)
+    status = np.zeros(B, dtype=np.int32)
+    lib().fo_xor_reconstruct_batch(k, S, B, _ptr(shards), n * S, S, _ptr(masks), _ptr(status), threads)
+    return status
+
+
+# ---------------------------------------------------------------- scheme layer (layer 2)
+
+class Payload:
+    """A Go []byte as the scheme sees it: its bytes (len) and its capacity (cap)."""
+
+    def __init__(self, data, cap=None):
+        self.data = bytes(data)
+        self.cap = len(self.data) if cap is None else cap
+
+    def __len__(self):
+        return len(self.data)
+
+
+class Block:
+    """internal/fec/block.go:23-34 fields, as the reference's table tests fill them."""
+
+    def __init__(self, id=0, tot_src=0, tot_rep=0, biggest=0, smallest=0, largest=0,
+                 sources=None, repairs=None):
+        self.id = id
+        self.tot_src = tot_src
+        self.tot_rep = tot_rep
+        self.biggest = biggest
+        self.smallest = smallest
+        self.largest = largest
+        self.sources = dict(sources or {})   # ssid -> Payload
+        self.repairs = dict(repairs or {})   # parity id -> Payload
+
+    def is_recoverable(self):   # block.go:88-90
+        return len(self.sources) + len(self.repairs) >= self.tot_src
+
+    def is_complete(self):      # block.go:93-95
+        return len(self.sources) == self.tot_src
+
+
+def _shard_from_payload(b, ssid):
+    """addLengthToSourceSymbolPayload (reed_solomon.go:70-89): payload[:biggest+2] resliced into
+    its (zeroed) capacity, big-endian uint16(len) at [biggest]."""
+    p = b.sources.get(ssid)
+    if p is None:
+        return None, "block [%d, %d] is complete but SID %d does not exist" % (b.smallest, b.largest, ssid)
+    L = REPAIR_PAYLOAD_METADATA_LEN + b.biggest
+    if L > p.cap:
+        return None, "shard len (%d) is greater than capacity of payload (%d)" % (L, p.cap)
+    buf = bytearray(L)
+    n = min(len(p), b.biggest)
+    buf[:n] = p.data[:n]
+    ln = len(p) & 0xFFFF
+    buf[b.biggest] = ln >> 8
+    buf[b.biggest + 1] = ln & 0xFF
+    return bytes(buf), None
+
+
+def rs_repair_symbols(b, k, m):
+    """reedSolomonScheme.repairSymbols -> ([(block_id, parity_id, payload)], err)."""
+    if not b.is_complete():
+        return None, "block does not have enough source symbols to generate repair symbols"
+    if b.biggest > MAX_FEC_PACKET_BUFFER_SIZE:
+        return None, ("source symbol payload len is greater is too big for FEC headers. Max %d and got %d"
+                      % (MAX_FEC_PACKET_BUFFER_SIZE, b.biggest))
+    L = REPAIR_PAYLOAD_METADATA_LEN + b.biggest
+    shards = np.zeros((1, b.tot_src + b.tot_rep, L), dtype=np.uint8)
+    for i in range(b.tot_src):
+        s, err = _shard_from_payload(b, b.smallest + i)
+        if err:
+            return None, err
+        shards[0, i] = np.frombuffer(s, dtype=np.uint8)
+    assert (k, m) == (b.tot_src, b.tot_rep)
+    rs_encode(k, m, shards)
+    return [(b.id, i, bytes(shards[0, k + i])) for i in range(m)], None
+
+
+def rs_recover_symbol_payloads(b, k, m):
+    """reedSolomonScheme.recoverSymbolPayloads -> (bytes | None, err)."""
+    if not b.is_recoverable():
+        return None, "not enough present symbols to repair the missing ones"
+    if b.is_complete():
+        return None, None
+    L = REPAIR_PAYLOAD_METADATA_LEN + b.biggest
+    n = b.tot_src + b.tot_rep
+    shards = np.zeros((1, n, L), dtype=np.uint8)
+    mask = 0
+    missing = []
+    for i in range(b.tot_src):
+        ssid = b.smallest + i
+        if ssid not in b.sources:
+            missing.append(i)
+            continue
+        s, err = _shard_from_payload(b, ssid)
+        if err:
+            return None, err
+        shards[0, i] = np.frombuffer(s, dtype=np.uint8)
+        mask |= 1 << i
+    for pid, p in b.repairs.items():
+        if len(p) != L:
+            return None, "shard sizes do not match"   # klauspost ErrShardSize
+        shards[0, k + pid] = np.frombuffer(p.data, dtype=np.uint8)
+        mask |= 1 << (k + pid)
+    st = rs_reconstruct(k, m, shards, np.array([mask], dtype=np.uint32))
+    if st[0] != 0:
+        return None, "too few shards given"             # klauspost ErrTooFewShards
+    out = bytearray()
+    for i in missing:
+        sh = shards[0, i]
+        ln = (int(sh[b.biggest]) << 8) | int(sh[b.biggest + 1])
+        out += bytes(sh[:ln])
+    return bytes(out), None
+
+
+def _xor_into(acc, payload, biggest):
+    """xorScheme.xor (xor.go:44-56)."""
+    for i, v in enumerate(payload.data):
+        acc[i] ^= v
+    ln = len(payload) & 0xFFFF
+    acc[biggest] ^= ln >> 8
+    acc[biggest + 1] ^= ln & 0xFF
+
+
+def xor_repair_symbols(b):
+    """xorScheme.repairSymbols -> ([(block_id, 0, payload)], err)."""
+    if not b.is_complete():
+        return None, "block does not have enough source symbols to generate repair symbols"
+    if b.tot_rep != 1:
+        return None, "xor only supports 1 repair symbol. Expected 1, received %d" % b.tot_rep
+    if b.biggest > MAX_FEC_PACKET_BUFFER_SIZE:
+        return None, ("source symbol payload len is greater is too big for FEC headers. Max %d and got %d"
+                      % (MAX_FEC_PACKET_BUFFER_SIZE, b.biggest))
+    acc = bytearray(REPAIR_PAYLOAD_METADATA_LEN + b.biggest)
+    for p in b.sources.values():
+        _xor_into(acc, p, b.biggest)
+    return [(b.id, 0, bytes(acc))], None
+
+
+def xor_recover_symbol_payloads(b):
+    """xorScheme.recoverSymbolPayloads -> (bytes | None, err); also fills the block map."""
+    if not b.is_recoverable():
+        return None, "not enough present symbols to repair the missing ones"
+    if b.is_complete():
+        return None, None
+    acc = bytearray(MAX_PACKET_BUFFER_SIZE)
+    for p in b.repairs.values():
+        for i, v in enumerate(p.data):
+            acc[i] ^= v
+    for p in b.sources.values():
+        _xor_into(acc, p, b.biggest)
+    ln = (acc[b.biggest] << 8) | acc[b.biggest + 1]
+    rec = bytes(acc[:ln])
+    for ssid in range(b.smallest, b.largest + 1):
+        if ssid not in b.sources:
+            b.sources[ssid] = Payload(rec, MAX_PACKET_BUFFER_SIZE)
+    if not b.is_complete():
+        return None, "block is not complete after recovery"
+    return rec, None
+
+
+def block_from_fixture(blk):
+    """Build a Block from a tests/golden/reference_cases.json block entry."""
+    def pl(d):
+        return {int(k): Payload(bytes.fromhex(v["hex"]), v["cap"]) for k, v in d.items()}
+    return Block(id=blk["id"], tot_src=blk["totNumSourceSymbols"], tot_rep=blk["totNumRepairSymbols"],
+                 biggest=blk["biggestSourceSymbolLenSoFar"], smallest=blk["smallestSSID"],
+                 largest=blk["largestSSID"], sources=pl(blk["ssidToSourcePayload"]),
+                 repairs=pl(blk["pidToRepairPayload"]))
