@@ -1,0 +1,207 @@
+"""0xfec_amd — MI355X-native block FEC engine (the hot path of ddritzenhoff/0xFEC internal/fec).
+
+The compute lives in lib0xfec_hip.so (hand-written gfx950 HIP kernels behind the C ABI of
+include/fec_hip.h). This module is a thin ctypes face of that ABI, plus the host-side mirror
+of the reference's scheme/manager layer (see `scheme`). There is no CPU fallback: if the
+library is missing the import fails, and without a HIP device every compute call raises.
+
+Import by name (the directory starts with a digit):
+    fec = importlib.import_module("0xfec_amd")
+"""
+import ctypes
+import os
+
+from ._build import LIB as _LIB_PATH
+
+if not os.path.exists(_LIB_PATH):
+    raise ImportError("lib0xfec_hip.so not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                      "(or python 0xfec_amd/_build.py)")
+
+lib = ctypes.CDLL(_LIB_PATH)
+
+# --- return codes / flags (include/fec_hip.h)
+FEC_OK = 0
+FEC_ERR_INVALID_ARG = -1
+FEC_ERR_INV_SHARD_NUM = -2
+FEC_ERR_MAX_SHARD_NUM = -3
+FEC_ERR_TOO_FEW_SHARDS = -4
+FEC_ERR_SHARD_SIZE = -5
+FEC_ERR_SHARD_NO_DATA = -6
+FEC_ERR_ALIGNMENT = -7
+FEC_ERR_HIP = -8
+FEC_ERR_NOMEM = -9
+FEC_ERR_NO_DEVICE = -10
+FEC_DEVICE = 0
+FEC_HOST = 1
+FEC_MAX_DECODE_SHARDS = 32
+
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+_i = ctypes.c_int
+
+lib.fec_version.restype = ctypes.c_char_p
+lib.fec_strerror.restype = ctypes.c_char_p
+lib.fec_strerror.argtypes = [_i]
+lib.fec_device_count.argtypes = [ctypes.POINTER(_i)]
+lib.fec_ctx_create.argtypes = [_i, ctypes.POINTER(_vp)]
+lib.fec_ctx_destroy.argtypes = [_vp]
+lib.fec_ctx_destroy.restype = None
+lib.fec_ctx_set_stream.argtypes = [_vp, _vp]
+lib.fec_ctx_stream.argtypes = [_vp]
+lib.fec_ctx_stream.restype = _vp
+lib.fec_sync.argtypes = [_vp]
+lib.fec_rs_matrix.argtypes = [_i, _i, _vp]
+lib.fec_rs_prepare.argtypes = [_vp, _i, _i]
+lib.fec_rs_encode_batch.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _i]
+lib.fec_rs_reconstruct_batch.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _sz, _vp, _vp, _i]
+lib.fec_xor_encode_batch.argtypes = [_vp, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _i]
+lib.fec_xor_reconstruct_batch.argtypes = [_vp, _i, _sz, _sz, _vp, _sz, _sz, _vp, _vp, _i]
+
+
+class FecError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        msg = lib.fec_strerror(code).decode()
+        super().__init__("%s%s (code %d)" % (what + ": " if what else "", msg, code))
+
+
+def _check(rc, what=""):
+    if rc != FEC_OK:
+        raise FecError(rc, what)
+    return rc
+
+
+def version():
+    return lib.fec_version().decode()
+
+
+def device_count():
+    n = _i(0)
+    lib.fec_device_count(ctypes.byref(n))
+    return n.value
+
+
+def rs_matrix(k, m):
+    """n x k systematic matrix of RS(k, m) (klauspost reedsolomon.New default); no device."""
+    import numpy as np
+    out = np.zeros((k + m, k), dtype=np.uint8)
+    _check(lib.fec_rs_matrix(k, m, out.ctypes.data), "fec_rs_matrix")
+    return out
+
+
+def _addr(x):
+    """(address, memory kind) for a numpy array, a torch tensor, or a raw device address."""
+    if isinstance(x, int):
+        return x, FEC_DEVICE
+    mod = type(x).__module__
+    if mod.startswith("numpy"):
+        return x.ctypes.data, FEC_HOST
+    if mod.startswith("torch"):
+        return x.data_ptr(), (FEC_DEVICE if x.is_cuda else FEC_HOST)
+    raise TypeError("unsupported buffer type %r" % type(x))
+
+
+def _shape3(shards):
+    B, n, S = shards.shape
+    if hasattr(shards, "is_contiguous"):
+        assert shards.is_contiguous()
+    else:
+        assert shards.flags.c_contiguous
+    return B, n, S
+
+
+class Codec:
+    """One device context (one HIP stream). Batch entry points over [B, n, S] uint8 arrays:
+    numpy arrays run the FEC_HOST path (staged through pinned memory), CUDA tensors the
+    FEC_DEVICE path (asynchronous on the ctx stream; call sync())."""
+
+    def __init__(self, device=0):
+        h = _vp()
+        _check(lib.fec_ctx_create(device, ctypes.byref(h)), "fec_ctx_create")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if self._h:
+            lib.fec_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def stream(self):
+        return lib.fec_ctx_stream(self._h)
+
+    def set_stream(self, stream_ptr):
+        _check(lib.fec_ctx_set_stream(self._h, stream_ptr or None))
+
+    def use_torch_stream(self):
+        """Enqueue on torch's current stream of this device, so codec calls order naturally
+        with torch ops on the same tensors."""
+        import torch
+        self.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+        return self
+
+    def sync(self):
+        return _check(lib.fec_sync(self._h), "fec_sync")
+
+    def prepare(self, k, m):
+        return _check(lib.fec_rs_prepare(self._h, k, m), "fec_rs_prepare")
+
+    # ---- raw C-ABI mirrors (addresses + strides)
+    def rs_encode_raw(self, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss, flags):
+        return _check(lib.fec_rs_encode_batch(self._h, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss, flags),
+                      "fec_rs_encode_batch")
+
+    def rs_reconstruct_raw(self, k, m, shard_len, nblocks, shards, bs, ss, masks, status, flags):
+        return lib.fec_rs_reconstruct_batch(self._h, k, m, shard_len, nblocks, shards, bs, ss, masks, status, flags)
+
+    # ---- array conveniences: shards is [B, n, S]; shard_len defaults to S
+    def rs_encode(self, k, m, shards, shard_len=None):
+        B, n, S = _shape3(shards)
+        assert n == k + m
+        a, kind = _addr(shards)
+        L = S if shard_len is None else shard_len
+        return self.rs_encode_raw(k, m, L, B, a, n * S, a + k * S, n * S, S, kind)
+
+    def rs_reconstruct(self, k, m, shards, masks, status=None, shard_len=None):
+        """Returns the C return code (FEC_OK or FEC_ERR_TOO_FEW_SHARDS for FEC_HOST)."""
+        B, n, S = _shape3(shards)
+        assert n == k + m
+        a, kind = _addr(shards)
+        ma, mkind = _addr(masks)
+        assert mkind == kind, "masks must live where the shards live"
+        sa = _addr(status)[0] if status is not None else None
+        L = S if shard_len is None else shard_len
+        rc = self.rs_reconstruct_raw(k, m, L, B, a, n * S, S, ma, sa, kind)
+        if rc not in (FEC_OK, FEC_ERR_TOO_FEW_SHARDS):
+            _check(rc, "fec_rs_reconstruct_batch")
+        return rc
+
+    def xor_encode(self, k, shards, shard_len=None):
+        B, n, S = _shape3(shards)
+        assert n == k + 1
+        a, kind = _addr(shards)
+        L = S if shard_len is None else shard_len
+        return _check(lib.fec_xor_encode_batch(self._h, k, L, B, a, n * S, a + k * S, n * S, S, kind),
+                      "fec_xor_encode_batch")
+
+    def xor_reconstruct(self, k, shards, masks, status=None, shard_len=None):
+        B, n, S = _shape3(shards)
+        assert n == k + 1
+        a, kind = _addr(shards)
+        ma, _ = _addr(masks)
+        sa = _addr(status)[0] if status is not None else None
+        L = S if shard_len is None else shard_len
+        rc = lib.fec_xor_reconstruct_batch(self._h, k, L, B, a, n * S, S, ma, sa, kind)
+        if rc not in (FEC_OK, FEC_ERR_TOO_FEW_SHARDS):
+            _check(rc, "fec_xor_reconstruct_batch")
+        return rc

@@ -1,0 +1,625 @@
+// fec_capi.cpp — C ABI of the MI355X FEC codec (include/fec_hip.h).
+//
+// Owns the per-device context: HIP stream, per-(k, m) code cache (systematic matrix,
+// device parity rows, encode PermTabs), decode plan workspace, pinned staging for the
+// FEC_HOST path. No CPU compute fallback exists: without a HIP device every compute
+// entry point fails with FEC_ERR_NO_DEVICE / FEC_ERR_HIP.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <utility>
+#include <vector>
+
+#include "../../include/fec_hip.h"
+#include "fec_kernels.hpp"
+#include "gf256.h"
+#include "rs_matrix.hpp"
+
+namespace {
+
+struct Code {
+    int k = 0, m = 0;
+    std::vector<uint8_t> matrix;   // n x k
+    uint8_t* d_prows = nullptr;    // m x k
+    uint32_t* d_tabs = nullptr;    // m x k PermTabs
+};
+
+// Bytes of staged shards per FEC_HOST chunk (x2 buffers, in and out).
+constexpr size_t kStageBytes = size_t(128) << 20;
+// Upper bound on decode plan workspace.
+constexpr size_t kPlanBytes = size_t(256) << 20;
+// nblocks * chunks-per-shard must stay below 2^31 per launch (32-bit item ids).
+constexpr uint64_t kMaxItems = uint64_t(1) << 31;
+
+}  // namespace
+
+struct fec_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    std::map<std::pair<int, int>, Code> codes;
+    uint8_t* d_plans = nullptr;
+    size_t plans_cap = 0;
+    int* d_err = nullptr;    // [0] sticky device-path error, [1] host-path error
+    uint8_t* h_stage = nullptr;
+    uint8_t* d_stage = nullptr;
+    size_t stage_cap = 0;
+    uint32_t* d_masks = nullptr;
+    int32_t* d_status = nullptr;
+    size_t masks_cap = 0;
+    int grid_cache[3][6] = {};
+};
+
+#define HIP_TRY(expr)                      \
+    do {                                   \
+        if ((expr) != hipSuccess) {        \
+            (void)hipGetLastError();       \
+            return FEC_ERR_HIP;            \
+        }                                  \
+    } while (0)
+
+static int select_device(fec_ctx* ctx) {
+    if (!ctx) return FEC_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    return FEC_OK;
+}
+
+static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+static int get_code(fec_ctx* ctx, int k, int m, Code** out) {
+    if (k <= 0 || m < 0) return FEC_ERR_INV_SHARD_NUM;
+    if (k + m > 256) return FEC_ERR_MAX_SHARD_NUM;
+    auto key = std::make_pair(k, m);
+    auto it = ctx->codes.find(key);
+    if (it != ctx->codes.end()) {
+        *out = &it->second;
+        return FEC_OK;
+    }
+    Code c;
+    c.k = k;
+    c.m = m;
+    c.matrix = rs::build_matrix(k, k + m);
+    if (c.matrix.empty()) return FEC_ERR_INV_SHARD_NUM;
+    if (m > 0) {
+        std::vector<uint32_t> tabs((size_t)m * k * 8);
+        for (int r = 0; r < m; ++r)
+            for (int j = 0; j < k; ++j) {
+                gf::PermTab t = gf::make_permtab(c.matrix[(size_t)(k + r) * k + j]);
+                memcpy(&tabs[((size_t)r * k + j) * 8], &t, sizeof(t));
+            }
+        HIP_TRY(hipMalloc(&c.d_prows, (size_t)m * k));
+        HIP_TRY(hipMalloc(&c.d_tabs, tabs.size() * 4));
+        HIP_TRY(hipMemcpy(c.d_prows, c.matrix.data() + (size_t)k * k, (size_t)m * k, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(c.d_tabs, tabs.data(), tabs.size() * 4, hipMemcpyHostToDevice));
+    }
+    auto res = ctx->codes.emplace(key, std::move(c));
+    *out = &res.first->second;
+    return FEC_OK;
+}
+
+static int grow_plans(fec_ctx* ctx, size_t bytes) {
+    if (bytes <= ctx->plans_cap) return FEC_OK;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (ctx->d_plans) HIP_TRY(hipFree(ctx->d_plans));
+    ctx->d_plans = nullptr;
+    ctx->plans_cap = 0;
+    HIP_TRY(hipMalloc(&ctx->d_plans, bytes));
+    ctx->plans_cap = bytes;
+    return FEC_OK;
+}
+
+static int grow_stage(fec_ctx* ctx, size_t bytes) {
+    if (bytes <= ctx->stage_cap) return FEC_OK;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (ctx->h_stage) HIP_TRY(hipHostFree(ctx->h_stage));
+    if (ctx->d_stage) HIP_TRY(hipFree(ctx->d_stage));
+    ctx->h_stage = nullptr;
+    ctx->d_stage = nullptr;
+    ctx->stage_cap = 0;
+    HIP_TRY(hipHostMalloc(&ctx->h_stage, bytes, hipHostMallocDefault));
+    HIP_TRY(hipMalloc(&ctx->d_stage, bytes));
+    ctx->stage_cap = bytes;
+    return FEC_OK;
+}
+
+static int grow_masks(fec_ctx* ctx, size_t n) {
+    if (n <= ctx->masks_cap) return FEC_OK;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (ctx->d_masks) HIP_TRY(hipFree(ctx->d_masks));
+    if (ctx->d_status) HIP_TRY(hipFree(ctx->d_status));
+    ctx->d_masks = nullptr;
+    ctx->d_status = nullptr;
+    ctx->masks_cap = 0;
+    HIP_TRY(hipMalloc(&ctx->d_masks, n * 4));
+    HIP_TRY(hipMalloc(&ctx->d_status, n * 4));
+    ctx->masks_cap = n;
+    return FEC_OK;
+}
+
+static int slot_of(uint32_t sel) { return sel <= 1 ? 0 : sel <= 2 ? 1 : sel <= 4 ? 2 : sel <= 8 ? 3 : 4; }
+
+static int grid_for(fec_ctx* ctx, int which, uint32_t sel, size_t lds) {
+    int& g = ctx->grid_cache[which][slot_of(sel)];
+    if (g == 0) g = fk::occupancy_grid(ctx->device, which, sel, lds);
+    return g;
+}
+
+static size_t round16(size_t x) { return (x + 15) & ~size_t(15); }
+
+// ---------------------------------------------------------------- device-memory cores
+
+static int rs_encode_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks, const uint8_t* data,
+                            size_t dbs, uint8_t* parity, size_t pbs, size_t ss) {
+    const uint32_t cps = (uint32_t)((len + fk::kChunk - 1) / fk::kChunk);
+    const size_t per_launch = std::max<size_t>(1, (size_t)(kMaxItems / cps));
+    const int k = code->k;
+    for (size_t b0 = 0; b0 < nblocks; b0 += per_launch) {
+        const size_t nb = std::min(per_launch, nblocks - b0);
+        for (int r0 = 0; r0 < code->m; r0 += 16) {
+            const int mr = std::min(16, code->m - r0);
+            fk::EncodeArgs a{};
+            a.in = data + b0 * dbs;
+            a.out = parity + b0 * pbs + (size_t)r0 * ss;
+            a.in_bs = dbs;
+            a.out_bs = pbs;
+            a.ss = ss;
+            a.k = (uint32_t)k;
+            a.m = (uint32_t)mr;
+            a.len = (uint32_t)len;
+            a.cps = cps;
+            a.total = (uint32_t)(nb * cps);
+            a.div_cps = fk::make_fastdiv(cps);
+            a.tabs = code->d_tabs + (size_t)r0 * k * 8;
+            const size_t lds = (size_t)mr * k * sizeof(gf::PermTab);
+            int grid = grid_for(ctx, 0, (uint32_t)mr, lds <= 65536 ? lds : 0);
+            grid = (int)std::min<uint64_t>((uint64_t)grid, (a.total + fk::kThreads - 1) / fk::kThreads);
+            if (grid < 1) grid = 1;
+            HIP_TRY(fk::launch_rs_encode(a, grid, ctx->stream));
+        }
+    }
+    return FEC_OK;
+}
+
+static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks, uint8_t* shards,
+                                 size_t bs, size_t ss, const uint32_t* masks, int32_t* status, int* err) {
+    const uint32_t k = (uint32_t)code->k, m = (uint32_t)code->m;
+    const uint32_t maxe = std::max<uint32_t>(1, std::min(k, m));
+    const uint32_t cps = (uint32_t)((len + fk::kChunk - 1) / fk::kChunk);
+    const uint32_t ps = fk::plan_stride_bytes(k, maxe);
+    size_t per_launch = std::min<size_t>(kPlanBytes / ps, (size_t)(kMaxItems / cps));
+    per_launch = std::max<size_t>(1, std::min(per_launch, nblocks));
+    int rc = grow_plans(ctx, per_launch * ps);
+    if (rc) return rc;
+    const uint32_t G = fk::pick_tile_blocks(cps, k, maxe);
+    for (size_t b0 = 0; b0 < nblocks; b0 += per_launch) {
+        const size_t nb = std::min(per_launch, nblocks - b0);
+        fk::PlanArgs p{};
+        p.masks = masks + b0;
+        p.plans = ctx->d_plans;
+        p.status = status ? status + b0 : nullptr;
+        p.err = err;
+        p.prows = code->d_prows;
+        p.k = k;
+        p.m = m;
+        p.nblocks = (uint32_t)nb;
+        p.plan_stride = ps;
+        p.maxe = maxe;
+        HIP_TRY(fk::launch_rs_plan(p, ctx->stream));
+        fk::ReconArgs a{};
+        a.shards = shards + b0 * bs;
+        a.bs = bs;
+        a.ss = ss;
+        a.plans = ctx->d_plans;
+        a.k = k;
+        a.len = (uint32_t)len;
+        a.cps = cps;
+        a.nblocks = (uint32_t)nb;
+        a.plan_stride = ps;
+        a.maxe = maxe;
+        a.g = G;
+        a.ntiles = (uint32_t)((nb + G - 1) / G);
+        a.div_cps = fk::make_fastdiv(cps);
+        const size_t lds = (size_t)G * maxe * k * sizeof(gf::PermTab) + (size_t)G * ps;
+        int grid = grid_for(ctx, 1, maxe, lds);
+        grid = std::min<int>(grid, (int)a.ntiles);
+        if (grid < 1) grid = 1;
+        HIP_TRY(fk::launch_rs_reconstruct(a, grid, ctx->stream));
+    }
+    return FEC_OK;
+}
+
+static int xor_encode_device(fec_ctx* ctx, int k, size_t len, size_t nblocks, const uint8_t* data, size_t dbs,
+                             uint8_t* parity, size_t pbs, size_t ss) {
+    const uint32_t cps = (uint32_t)((len + fk::kChunk - 1) / fk::kChunk);
+    const size_t per_launch = std::max<size_t>(1, (size_t)(kMaxItems / cps));
+    for (size_t b0 = 0; b0 < nblocks; b0 += per_launch) {
+        const size_t nb = std::min(per_launch, nblocks - b0);
+        fk::XorArgs a{};
+        a.in = data + b0 * dbs;
+        a.out = parity + b0 * pbs;
+        a.in_bs = dbs;
+        a.out_bs = pbs;
+        a.ss = ss;
+        a.k = (uint32_t)k;
+        a.len = (uint32_t)len;
+        a.cps = cps;
+        a.total = (uint32_t)(nb * cps);
+        a.div_cps = fk::make_fastdiv(cps);
+        int grid = grid_for(ctx, 2, 1, 0);
+        grid = (int)std::min<uint64_t>((uint64_t)grid, (a.total + fk::kThreads - 1) / fk::kThreads);
+        if (grid < 1) grid = 1;
+        HIP_TRY(fk::launch_xor_encode(a, grid, ctx->stream));
+    }
+    return FEC_OK;
+}
+
+static int xor_reconstruct_device(fec_ctx* ctx, int k, size_t len, size_t nblocks, uint8_t* shards, size_t bs,
+                                  size_t ss, const uint32_t* masks, int32_t* status, int* err) {
+    const uint32_t cps = (uint32_t)((len + fk::kChunk - 1) / fk::kChunk);
+    const size_t per_launch = std::max<size_t>(1, (size_t)(kMaxItems / cps));
+    for (size_t b0 = 0; b0 < nblocks; b0 += per_launch) {
+        const size_t nb = std::min(per_launch, nblocks - b0);
+        fk::XorArgs a{};
+        a.in = shards + b0 * bs;
+        a.out = shards + b0 * bs;
+        a.in_bs = bs;
+        a.out_bs = bs;
+        a.ss = ss;
+        a.masks = masks + b0;
+        a.status = status ? status + b0 : nullptr;
+        a.err = err;
+        a.k = (uint32_t)k;
+        a.len = (uint32_t)len;
+        a.cps = cps;
+        a.total = (uint32_t)(nb * cps);
+        a.div_cps = fk::make_fastdiv(cps);
+        int grid = grid_for(ctx, 2, 1, 0);
+        grid = (int)std::min<uint64_t>((uint64_t)grid, (a.total + fk::kThreads - 1) / fk::kThreads);
+        if (grid < 1) grid = 1;
+        HIP_TRY(fk::launch_xor_reconstruct(a, grid, ctx->stream));
+    }
+    return FEC_OK;
+}
+
+// ---------------------------------------------------------------- validation helpers
+
+static int check_device_layout(const void* p, size_t bs, size_t ss, size_t len) {
+    if (!p) return FEC_ERR_INVALID_ARG;
+    if (!aligned16(p) || (bs & 15) || (ss & 15)) return FEC_ERR_ALIGNMENT;
+    if (ss < len) return FEC_ERR_INVALID_ARG;
+    return FEC_OK;
+}
+
+// Blocks per FEC_HOST chunk for `slots` staged shard slots per block of `ssd` bytes.
+static size_t host_chunk_blocks(size_t slots, size_t ssd) {
+    const size_t per_block = slots * ssd;
+    return std::max<size_t>(1, kStageBytes / per_block);
+}
+
+// ---------------------------------------------------------------- C ABI
+
+extern "C" {
+
+const char* fec_version(void) { return "0xfec-mi355x 0.1.0 (gfx950)"; }
+
+const char* fec_strerror(int code) {
+    switch (code) {
+        case FEC_OK: return "ok";
+        case FEC_ERR_INVALID_ARG: return "invalid argument";
+        case FEC_ERR_INV_SHARD_NUM: return "cannot create Encoder with less than one data shard or less than zero parity shards";
+        case FEC_ERR_MAX_SHARD_NUM: return "cannot create Encoder with more than 256 data+parity shards";
+        case FEC_ERR_TOO_FEW_SHARDS: return "too few shards given";
+        case FEC_ERR_SHARD_SIZE: return "shard sizes do not match";
+        case FEC_ERR_SHARD_NO_DATA: return "no shard data";
+        case FEC_ERR_ALIGNMENT: return "device shard layout must be 16-byte aligned";
+        case FEC_ERR_HIP: return "HIP runtime error";
+        case FEC_ERR_NOMEM: return "out of memory";
+        case FEC_ERR_NO_DEVICE: return "no HIP device";
+        default: return "unknown error";
+    }
+}
+
+int fec_device_count(int* count) {
+    if (!count) return FEC_ERR_INVALID_ARG;
+    *count = 0;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return FEC_ERR_NO_DEVICE;
+    }
+    *count = n;
+    return n > 0 ? FEC_OK : FEC_ERR_NO_DEVICE;
+}
+
+int fec_ctx_create(int device, fec_ctx** out) {
+    if (!out) return FEC_ERR_INVALID_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        return FEC_ERR_NO_DEVICE;
+    }
+    if (device < 0 || device >= n) return FEC_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(device));
+    fec_ctx* ctx = new fec_ctx();
+    ctx->device = device;
+    if (hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&ctx->d_err, 2 * sizeof(int)) != hipSuccess ||
+        hipMemset(ctx->d_err, 0, 2 * sizeof(int)) != hipSuccess) {
+        (void)hipGetLastError();
+        fec_ctx_destroy(ctx);
+        return FEC_ERR_HIP;
+    }
+    ctx->stream = ctx->own;
+    *out = ctx;
+    return FEC_OK;
+}
+
+void fec_ctx_destroy(fec_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto& kv : ctx->codes) {
+        if (kv.second.d_prows) (void)hipFree(kv.second.d_prows);
+        if (kv.second.d_tabs) (void)hipFree(kv.second.d_tabs);
+    }
+    if (ctx->d_plans) (void)hipFree(ctx->d_plans);
+    if (ctx->d_err) (void)hipFree(ctx->d_err);
+    if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+    if (ctx->d_stage) (void)hipFree(ctx->d_stage);
+    if (ctx->d_masks) (void)hipFree(ctx->d_masks);
+    if (ctx->d_status) (void)hipFree(ctx->d_status);
+    if (ctx->own) (void)hipStreamDestroy(ctx->own);
+    (void)hipGetLastError();
+    delete ctx;
+}
+
+int fec_ctx_set_stream(fec_ctx* ctx, void* hip_stream) {
+    if (!ctx) return FEC_ERR_INVALID_ARG;
+    ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own;
+    return FEC_OK;
+}
+
+void* fec_ctx_stream(fec_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int fec_sync(fec_ctx* ctx) {
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    int err = 0;
+    HIP_TRY(hipMemcpy(&err, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (err) {
+        HIP_TRY(hipMemset(ctx->d_err, 0, sizeof(int)));
+        return FEC_ERR_TOO_FEW_SHARDS;
+    }
+    return FEC_OK;
+}
+
+int fec_rs_matrix(int k, int m, uint8_t* out) {
+    if (!out) return FEC_ERR_INVALID_ARG;
+    if (k <= 0 || m < 0) return FEC_ERR_INV_SHARD_NUM;
+    if (k + m > 256) return FEC_ERR_MAX_SHARD_NUM;
+    std::vector<uint8_t> mat = rs::build_matrix(k, k + m);
+    if (mat.empty()) return FEC_ERR_INV_SHARD_NUM;
+    memcpy(out, mat.data(), mat.size());
+    return FEC_OK;
+}
+
+int fec_rs_prepare(fec_ctx* ctx, int k, int m) {
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    Code* code = nullptr;
+    return get_code(ctx, k, m, &code);
+}
+
+int fec_rs_encode_batch(fec_ctx* ctx, int k, int m, size_t shard_len, size_t nblocks, const uint8_t* data,
+                        size_t data_block_stride, uint8_t* parity, size_t parity_block_stride,
+                        size_t shard_stride, int flags) {
+    if (k <= 0 || m < 0) return FEC_ERR_INV_SHARD_NUM;
+    if (k + m > 256) return FEC_ERR_MAX_SHARD_NUM;
+    if (flags != FEC_DEVICE && flags != FEC_HOST) return FEC_ERR_INVALID_ARG;
+    if (shard_len == 0) return FEC_ERR_SHARD_NO_DATA;
+    if (shard_len > (size_t(1) << 30)) return FEC_ERR_INVALID_ARG;
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    Code* code = nullptr;
+    if ((rc = get_code(ctx, k, m, &code))) return rc;
+    if (nblocks == 0 || m == 0) return FEC_OK;
+    if (!data || !parity) return FEC_ERR_INVALID_ARG;
+    if (flags == FEC_DEVICE) {
+        if ((rc = check_device_layout(data, data_block_stride, shard_stride, shard_len))) return rc;
+        if ((rc = check_device_layout(parity, parity_block_stride, shard_stride, shard_len))) return rc;
+        return rs_encode_device(ctx, code, shard_len, nblocks, data, data_block_stride, parity,
+                                parity_block_stride, shard_stride);
+    }
+    // FEC_HOST: stage [chunk][n][ssd] through pinned memory.
+    const size_t ssd = round16(shard_len);
+    const size_t n = (size_t)k + m;
+    const size_t chunk = host_chunk_blocks(n, ssd);
+    if ((rc = grow_stage(ctx, std::min(chunk, nblocks) * n * ssd))) return rc;
+    for (size_t b0 = 0; b0 < nblocks; b0 += chunk) {
+        const size_t nb = std::min(chunk, nblocks - b0);
+        for (size_t b = 0; b < nb; ++b)
+            for (int j = 0; j < k; ++j)
+                memcpy(ctx->h_stage + (b * n + j) * ssd, data + (b0 + b) * data_block_stride + j * shard_stride,
+                       shard_len);
+        HIP_TRY(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, nb * n * ssd, hipMemcpyHostToDevice, ctx->stream));
+        if ((rc = rs_encode_device(ctx, code, shard_len, nb, ctx->d_stage, n * ssd, ctx->d_stage + k * ssd,
+                                   n * ssd, ssd)))
+            return rc;
+        HIP_TRY(hipMemcpyAsync(ctx->h_stage, ctx->d_stage, nb * n * ssd, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        for (size_t b = 0; b < nb; ++b)
+            for (int i = 0; i < m; ++i)
+                memcpy(parity + (b0 + b) * parity_block_stride + i * shard_stride,
+                       ctx->h_stage + (b * n + k + i) * ssd, shard_len);
+    }
+    return FEC_OK;
+}
+
+int fec_rs_reconstruct_batch(fec_ctx* ctx, int k, int m, size_t shard_len, size_t nblocks, uint8_t* shards,
+                             size_t block_stride, size_t shard_stride, const uint32_t* present_mask,
+                             int32_t* block_status, int flags) {
+    if (k <= 0 || m < 0) return FEC_ERR_INV_SHARD_NUM;
+    if (k + m > FEC_MAX_DECODE_SHARDS) return FEC_ERR_MAX_SHARD_NUM;
+    if (flags != FEC_DEVICE && flags != FEC_HOST) return FEC_ERR_INVALID_ARG;
+    if (shard_len == 0) return FEC_ERR_SHARD_NO_DATA;
+    if (shard_len > (size_t(1) << 30)) return FEC_ERR_INVALID_ARG;
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    Code* code = nullptr;
+    if ((rc = get_code(ctx, k, m, &code))) return rc;
+    if (nblocks == 0) return FEC_OK;
+    if (!shards || !present_mask) return FEC_ERR_INVALID_ARG;
+    if (flags == FEC_DEVICE) {
+        if ((rc = check_device_layout(shards, block_stride, shard_stride, shard_len))) return rc;
+        return rs_reconstruct_device(ctx, code, shard_len, nblocks, shards, block_stride, shard_stride,
+                                     present_mask, block_status, ctx->d_err);
+    }
+    const size_t ssd = round16(shard_len);
+    const size_t n = (size_t)k + m;
+    const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
+    const uint32_t kmask = (1u << k) - 1u;
+    const size_t chunk = host_chunk_blocks(n, ssd);
+    if ((rc = grow_stage(ctx, std::min(chunk, nblocks) * n * ssd))) return rc;
+    if ((rc = grow_masks(ctx, std::min(chunk, nblocks)))) return rc;
+    HIP_TRY(hipMemsetAsync(ctx->d_err + 1, 0, sizeof(int), ctx->stream));
+    std::vector<int32_t> st;
+    for (size_t b0 = 0; b0 < nblocks; b0 += chunk) {
+        const size_t nb = std::min(chunk, nblocks - b0);
+        for (size_t b = 0; b < nb; ++b) {
+            const uint32_t mask = present_mask[b0 + b] & all;
+            if ((mask & kmask) == kmask) continue;   // nothing to rebuild: skip the copy
+            for (size_t i = 0; i < n; ++i)
+                if ((mask >> i) & 1u)
+                    memcpy(ctx->h_stage + (b * n + i) * ssd, shards + (b0 + b) * block_stride + i * shard_stride,
+                           shard_len);
+        }
+        HIP_TRY(hipMemcpyAsync(ctx->d_masks, present_mask + b0, nb * 4, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, nb * n * ssd, hipMemcpyHostToDevice, ctx->stream));
+        if ((rc = rs_reconstruct_device(ctx, code, shard_len, nb, ctx->d_stage, n * ssd, ssd, ctx->d_masks,
+                                        ctx->d_status, ctx->d_err + 1)))
+            return rc;
+        st.resize(nb);
+        HIP_TRY(hipMemcpyAsync(st.data(), ctx->d_status, nb * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(ctx->h_stage, ctx->d_stage, nb * n * ssd, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        for (size_t b = 0; b < nb; ++b) {
+            if (block_status) block_status[b0 + b] = st[b];
+            if (st[b] != 0) continue;
+            const uint32_t mask = present_mask[b0 + b] & all;
+            for (int i = 0; i < k; ++i)
+                if (!((mask >> i) & 1u))
+                    memcpy(shards + (b0 + b) * block_stride + i * shard_stride, ctx->h_stage + (b * n + i) * ssd,
+                           shard_len);
+        }
+    }
+    int err = 0;
+    HIP_TRY(hipMemcpy(&err, ctx->d_err + 1, sizeof(int), hipMemcpyDeviceToHost));
+    return err ? FEC_ERR_TOO_FEW_SHARDS : FEC_OK;
+}
+
+int fec_xor_encode_batch(fec_ctx* ctx, int k, size_t shard_len, size_t nblocks, const uint8_t* data,
+                         size_t data_block_stride, uint8_t* parity, size_t parity_block_stride, size_t shard_stride,
+                         int flags) {
+    if (k <= 0) return FEC_ERR_INV_SHARD_NUM;
+    if (k + 1 > 256) return FEC_ERR_MAX_SHARD_NUM;
+    if (flags != FEC_DEVICE && flags != FEC_HOST) return FEC_ERR_INVALID_ARG;
+    if (shard_len == 0) return FEC_ERR_SHARD_NO_DATA;
+    if (shard_len > (size_t(1) << 30)) return FEC_ERR_INVALID_ARG;
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    if (nblocks == 0) return FEC_OK;
+    if (!data || !parity) return FEC_ERR_INVALID_ARG;
+    if (flags == FEC_DEVICE) {
+        if ((rc = check_device_layout(data, data_block_stride, shard_stride, shard_len))) return rc;
+        if ((rc = check_device_layout(parity, parity_block_stride, shard_stride, shard_len))) return rc;
+        return xor_encode_device(ctx, k, shard_len, nblocks, data, data_block_stride, parity, parity_block_stride,
+                                 shard_stride);
+    }
+    const size_t ssd = round16(shard_len);
+    const size_t n = (size_t)k + 1;
+    const size_t chunk = host_chunk_blocks(n, ssd);
+    if ((rc = grow_stage(ctx, std::min(chunk, nblocks) * n * ssd))) return rc;
+    for (size_t b0 = 0; b0 < nblocks; b0 += chunk) {
+        const size_t nb = std::min(chunk, nblocks - b0);
+        for (size_t b = 0; b < nb; ++b)
+            for (int j = 0; j < k; ++j)
+                memcpy(ctx->h_stage + (b * n + j) * ssd, data + (b0 + b) * data_block_stride + j * shard_stride,
+                       shard_len);
+        HIP_TRY(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, nb * n * ssd, hipMemcpyHostToDevice, ctx->stream));
+        if ((rc = xor_encode_device(ctx, k, shard_len, nb, ctx->d_stage, n * ssd, ctx->d_stage + k * ssd, n * ssd,
+                                    ssd)))
+            return rc;
+        HIP_TRY(hipMemcpyAsync(ctx->h_stage, ctx->d_stage, nb * n * ssd, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        for (size_t b = 0; b < nb; ++b)
+            memcpy(parity + (b0 + b) * parity_block_stride, ctx->h_stage + (b * n + k) * ssd, shard_len);
+    }
+    return FEC_OK;
+}
+
+int fec_xor_reconstruct_batch(fec_ctx* ctx, int k, size_t shard_len, size_t nblocks, uint8_t* shards,
+                              size_t block_stride, size_t shard_stride, const uint32_t* present_mask,
+                              int32_t* block_status, int flags) {
+    if (k <= 0) return FEC_ERR_INV_SHARD_NUM;
+    if (k + 1 > FEC_MAX_DECODE_SHARDS) return FEC_ERR_MAX_SHARD_NUM;
+    if (flags != FEC_DEVICE && flags != FEC_HOST) return FEC_ERR_INVALID_ARG;
+    if (shard_len == 0) return FEC_ERR_SHARD_NO_DATA;
+    if (shard_len > (size_t(1) << 30)) return FEC_ERR_INVALID_ARG;
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    if (nblocks == 0) return FEC_OK;
+    if (!shards || !present_mask) return FEC_ERR_INVALID_ARG;
+    if (flags == FEC_DEVICE) {
+        if ((rc = check_device_layout(shards, block_stride, shard_stride, shard_len))) return rc;
+        return xor_reconstruct_device(ctx, k, shard_len, nblocks, shards, block_stride, shard_stride, present_mask,
+                                      block_status, ctx->d_err);
+    }
+    const size_t ssd = round16(shard_len);
+    const size_t n = (size_t)k + 1;
+    const uint32_t all = (1u << n) - 1u;
+    const uint32_t kmask = (1u << k) - 1u;
+    const size_t chunk = host_chunk_blocks(n, ssd);
+    if ((rc = grow_stage(ctx, std::min(chunk, nblocks) * n * ssd))) return rc;
+    if ((rc = grow_masks(ctx, std::min(chunk, nblocks)))) return rc;
+    HIP_TRY(hipMemsetAsync(ctx->d_err + 1, 0, sizeof(int), ctx->stream));
+    std::vector<int32_t> st;
+    for (size_t b0 = 0; b0 < nblocks; b0 += chunk) {
+        const size_t nb = std::min(chunk, nblocks - b0);
+        for (size_t b = 0; b < nb; ++b) {
+            const uint32_t mask = present_mask[b0 + b] & all;
+            if ((mask & kmask) == kmask) continue;
+            for (size_t i = 0; i < n; ++i)
+                if ((mask >> i) & 1u)
+                    memcpy(ctx->h_stage + (b * n + i) * ssd, shards + (b0 + b) * block_stride + i * shard_stride,
+                           shard_len);
+        }
+        HIP_TRY(hipMemcpyAsync(ctx->d_masks, present_mask + b0, nb * 4, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, nb * n * ssd, hipMemcpyHostToDevice, ctx->stream));
+        if ((rc = xor_reconstruct_device(ctx, k, shard_len, nb, ctx->d_stage, n * ssd, ssd, ctx->d_masks,
+                                         ctx->d_status, ctx->d_err + 1)))
+            return rc;
+        st.resize(nb);
+        HIP_TRY(hipMemcpyAsync(st.data(), ctx->d_status, nb * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(ctx->h_stage, ctx->d_stage, nb * n * ssd, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        for (size_t b = 0; b < nb; ++b) {
+            if (block_status) block_status[b0 + b] = st[b];
+            if (st[b] != 0) continue;
+            const uint32_t mask = present_mask[b0 + b] & all;
+            for (int i = 0; i < k; ++i)
+                if (!((mask >> i) & 1u))
+                    memcpy(shards + (b0 + b) * block_stride + i * shard_stride, ctx->h_stage + (b * n + i) * ssd,
+                           shard_len);
+        }
+    }
+    int err = 0;
+    HIP_TRY(hipMemcpy(&err, ctx->d_err + 1, sizeof(int), hipMemcpyDeviceToHost));
+    return err ? FEC_ERR_TOO_FEW_SHARDS : FEC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,476 @@
+// fec_kernels.hip — gfx950 (MI355X, CDNA4) kernels for block FEC.
+//
+// Hot path of ddritzenhoff/0xFEC internal/fec (reed_solomon.go:51 Encode, :124
+// ReconstructData; xor.go:28-33, :80-86), rebuilt for CDNA4:
+//   * byte-wise GF(2^8) work on packed dwords with v_perm_b32 product tables
+//     (three lookups per dword per coefficient; no MFMA — this is not a contraction)
+//   * every lane owns one 16-byte column chunk of a block and streams the k input
+//     shards of that chunk with global_load_dwordx4 (a wave covers 1 KiB contiguous
+//     per input shard), accumulating all outputs in VGPRs, so each input byte is read
+//     from HBM exactly once and each output byte written once
+//   * coefficient tables sit in LDS and are read wave-uniform (broadcast)
+//   * decode solves only the e x e system of the erased data shards per block
+//     (rs_plan_kernel), which is the same linear solution klauspost computes from the
+//     full k x k inverse of the first k present rows.
+#include <hip/hip_runtime.h>
+
+#include "fec_kernels.hpp"
+#include "gf256.h"
+
+namespace fk {
+
+FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f{d, 0, 0};
+    uint32_t l = 0;
+    while ((1ull << l) < d) ++l;
+    f.shift = l;
+    f.magic = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+    return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+    const uint32_t t = __umulhi(n, f.magic);
+    return (uint32_t)(((uint64_t)t + n) >> f.shift);
+}
+
+struct Idx {
+    uint32_t a, b, c;
+};
+
+__device__ __forceinline__ Idx split(uint32_t x) {
+    return {x & 0x07070707u, (x >> 3) & 0x07070707u, (x >> 6) & 0x03030303u};
+}
+
+// c * x for four packed bytes, c given by its PermTab.
+__device__ __forceinline__ uint32_t gmul(const Idx& i, uint32_t t0lo, uint32_t t0hi, uint32_t t1lo,
+                                         uint32_t t1hi, uint32_t t2) {
+    return __builtin_amdgcn_perm(t0hi, t0lo, i.a) ^ __builtin_amdgcn_perm(t1hi, t1lo, i.b) ^
+           __builtin_amdgcn_perm(t2, t2, i.c);
+}
+
+__device__ __forceinline__ uint4 ld16(const uint8_t* p) {
+    return *reinterpret_cast<const uint4*>(p);
+}
+
+__device__ __forceinline__ void st16(uint8_t* p, uint4 v) {
+    *reinterpret_cast<uint4*>(p) = v;
+}
+
+__device__ __forceinline__ uint32_t lane_of(const uint4& v, int d) {
+    return d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
+}
+
+// Store the first nb (< 16) bytes of v.
+__device__ __forceinline__ void st_partial(uint8_t* p, const uint4& v, uint32_t nb) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t w = lane_of(v, d);
+        if (4u * d + 4u <= nb) {
+            *reinterpret_cast<uint32_t*>(p + 4 * d) = w;
+        } else if (4u * d < nb) {
+            const uint32_t rem = nb - 4u * d;
+            if (rem >= 2) *reinterpret_cast<uint16_t*>(p + 4 * d) = (uint16_t)w;
+            if (rem & 1) p[4 * d + (rem & 2)] = (uint8_t)(w >> (8 * (rem & 2)));
+        }
+    }
+}
+
+__device__ __forceinline__ void store_chunk(uint8_t* p, const uint4& v, uint32_t nb) {
+    if (nb >= 16)
+        st16(p, v);
+    else
+        st_partial(p, v, nb);
+}
+
+// acc ^= tab * x, for one 16-byte chunk.
+__device__ __forceinline__ void mac(uint4& acc, const Idx (&ix)[4], const gf::PermTab* t) {
+    const uint4 lo = *reinterpret_cast<const uint4*>(t);   // t0lo t0hi t1lo t1hi
+    const uint32_t t2 = t->t2;
+    acc.x ^= gmul(ix[0], lo.x, lo.y, lo.z, lo.w, t2);
+    acc.y ^= gmul(ix[1], lo.x, lo.y, lo.z, lo.w, t2);
+    acc.z ^= gmul(ix[2], lo.x, lo.y, lo.z, lo.w, t2);
+    acc.w ^= gmul(ix[3], lo.x, lo.y, lo.z, lo.w, t2);
+}
+
+// ------------------------------------------------------------------ RS encode
+// One lane = one 16-byte column chunk of one block; all m parities accumulate in VGPRs.
+template <int MAXM, bool LDS_TABS>
+__global__ __launch_bounds__(kThreads) void rs_encode_kernel(EncodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const gf::PermTab* tabs;
+    if constexpr (LDS_TABS) {
+        uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
+        const uint32_t nw = a.m * a.k * 8;
+        for (uint32_t i = threadIdx.x; i < nw; i += kThreads) dst[i] = a.tabs[i];
+        __syncthreads();
+        tabs = reinterpret_cast<const gf::PermTab*>(smem);
+    } else {
+        tabs = reinterpret_cast<const gf::PermTab*>(a.tabs);
+    }
+    const uint32_t k = a.k, m = a.m;
+    const uint32_t stride = gridDim.x * kThreads;
+    for (uint32_t item = blockIdx.x * kThreads + threadIdx.x; item < a.total; item += stride) {
+        const uint32_t b = fdiv(item, a.div_cps);
+        const uint32_t c = item - b * a.cps;
+        const uint8_t* src = a.in + (uint64_t)b * a.in_bs + (uint64_t)c * kChunk;
+        uint4 acc[MAXM];
+#pragma unroll
+        for (int r = 0; r < MAXM; ++r) acc[r] = make_uint4(0, 0, 0, 0);
+        for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
+            uint4 x[kInGroup];
+#pragma unroll
+            for (int jj = 0; jj < kInGroup; ++jj) {
+                const uint32_t j = min(j0 + jj, k - 1);   // clamp: loads stay unconditional
+                x[jj] = ld16(src + (uint64_t)j * a.ss);
+            }
+#pragma unroll
+            for (int jj = 0; jj < kInGroup; ++jj) {
+                if (j0 + jj < k) {
+                    const Idx ix[4] = {split(x[jj].x), split(x[jj].y), split(x[jj].z), split(x[jj].w)};
+#pragma unroll
+                    for (int r = 0; r < MAXM; ++r)
+                        if (r < (int)m) mac(acc[r], ix, tabs + r * k + j0 + jj);
+                }
+            }
+        }
+        uint8_t* dst = a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk;
+        const uint32_t nb = a.len - c * kChunk;
+#pragma unroll
+        for (int r = 0; r < MAXM; ++r)
+            if (r < (int)m) store_chunk(dst + (uint64_t)r * a.ss, acc[r], nb);
+    }
+}
+
+// ------------------------------------------------------------------ RS reconstruct plan
+// One thread per block. From the present mask: E = erased data shards (e of them),
+// R = first e present parity shards; the first k present shards are then exactly
+// {present data} + R. Solve A[R][E] (e x e) and express each erased shard over those k
+// inputs. Writes the plan (see plan_stride_bytes).
+template <int MAXE>
+__global__ __launch_bounds__(kThreads) void rs_plan_kernel(PlanArgs a) {
+    __shared__ uint8_t s_exp[512];
+    __shared__ uint8_t s_log[256];
+    for (int i = threadIdx.x; i < 512; i += kThreads) s_exp[i] = gf::kTables.exp[i];
+    for (int i = threadIdx.x; i < 256; i += kThreads) s_log[i] = gf::kTables.log[i];
+    __syncthreads();
+    const uint32_t b = blockIdx.x * kThreads + threadIdx.x;
+    if (b >= a.nblocks) return;
+    auto mul = [&](uint32_t x, uint32_t y) -> uint32_t {
+        return (x && y) ? s_exp[s_log[x] + s_log[y]] : 0u;
+    };
+    const uint32_t k = a.k, m = a.m, n = k + m;
+    const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
+    const uint32_t mask = a.masks[b] & all;
+    const uint32_t kmask = k >= 32 ? 0xFFFFFFFFu : ((1u << k) - 1u);
+    uint8_t* P = a.plans + (uint64_t)b * a.plan_stride;
+    const uint32_t e = k - __popc(mask & kmask);
+    int32_t st = 0;
+    if (e == 0) {
+        P[0] = 0;
+    } else if ((uint32_t)__popc(mask) < k) {
+        P[0] = 0;
+        st = -4;  // FEC_ERR_TOO_FEW_SHARDS
+        atomicOr(a.err, 1);
+    } else {
+        uint8_t E[MAXE], R[MAXE];
+        uint32_t ne = 0, nr = 0;
+        for (uint32_t i = 0; i < k; ++i)
+            if (!((mask >> i) & 1u)) E[ne++] = (uint8_t)i;
+        for (uint32_t p = 0; p < m && nr < e; ++p)
+            if ((mask >> (k + p)) & 1u) R[nr++] = (uint8_t)p;
+        // Gauss-Jordan on [A | I], A[t][i] = prows[R[t]][E[i]]
+        uint8_t A[MAXE][2 * MAXE];
+        for (uint32_t t = 0; t < e; ++t)
+            for (uint32_t i = 0; i < 2 * e; ++i)
+                A[t][i] = i < e ? a.prows[R[t] * k + E[i]] : (uint8_t)(i - e == t);
+        for (uint32_t col = 0; col < e; ++col) {
+            uint32_t piv = col;
+            while (piv < e && A[piv][col] == 0) ++piv;
+            if (piv != col)
+                for (uint32_t i = 0; i < 2 * e; ++i) {
+                    const uint8_t tmp = A[piv][i];
+                    A[piv][i] = A[col][i];
+                    A[col][i] = tmp;
+                }
+            const uint32_t inv = s_exp[255 - s_log[A[col][col]]];
+            for (uint32_t i = 0; i < 2 * e; ++i) A[col][i] = (uint8_t)mul(inv, A[col][i]);
+            for (uint32_t r = 0; r < e; ++r) {
+                if (r == col) continue;
+                const uint32_t f = A[r][col];
+                if (!f) continue;
+                for (uint32_t i = 0; i < 2 * e; ++i) A[r][i] ^= (uint8_t)mul(f, A[col][i]);
+            }
+        }
+        // inputs: present data ascending, then parities R
+        uint8_t* out_idx = P + 4;
+        uint8_t* in_idx = P + 4 + a.maxe;
+        uint8_t* coef = P + 4 + a.maxe + k;
+        uint32_t pos = 0;
+        for (uint32_t j = 0; j < k; ++j) {
+            if (!((mask >> j) & 1u)) continue;
+            in_idx[pos] = (uint8_t)j;
+            for (uint32_t i = 0; i < e; ++i) {
+                uint32_t c = 0;
+                for (uint32_t t = 0; t < e; ++t) c ^= mul(A[i][e + t], a.prows[R[t] * k + j]);
+                coef[i * k + pos] = (uint8_t)c;
+            }
+            ++pos;
+        }
+        for (uint32_t t = 0; t < e; ++t, ++pos) {
+            in_idx[pos] = (uint8_t)(k + R[t]);
+            for (uint32_t i = 0; i < e; ++i) coef[i * k + pos] = A[i][e + t];
+        }
+        for (uint32_t i = 0; i < e; ++i) out_idx[i] = E[i];
+        P[0] = (uint8_t)e;
+    }
+    if (a.status) a.status[b] = st;
+}
+
+// ------------------------------------------------------------------ RS reconstruct
+// A workgroup takes tiles of G consecutive blocks: it stages their plans in LDS, expands
+// every coefficient to its PermTab once, then lanes sweep the G*cps (block, chunk) items.
+// Rows beyond a block's own erasure count carry zero tables, and each item loops only to
+// the wave's largest erasure count (ballot), so one-erasure batches do one row of work.
+template <int MAXE>
+__global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t k = a.k, G = a.g, maxe = a.maxe;
+    gf::PermTab* tabs = reinterpret_cast<gf::PermTab*>(smem);                // G*maxe*k
+    uint8_t* plans = smem + (size_t)G * maxe * k * sizeof(gf::PermTab);      // G*plan_stride
+    for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+        const uint32_t b0 = tile * G;
+        const uint32_t gt = min(G, a.nblocks - b0);
+        __syncthreads();   // previous tile fully consumed
+        {
+            const uint32_t nw = gt * a.plan_stride / 4;
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(a.plans + (uint64_t)b0 * a.plan_stride);
+            uint32_t* dst = reinterpret_cast<uint32_t*>(plans);
+            for (uint32_t i = threadIdx.x; i < nw; i += kThreads) dst[i] = src[i];
+        }
+        __syncthreads();
+        {
+            const uint32_t ne = gt * maxe * k;
+            for (uint32_t i = threadIdx.x; i < ne; i += kThreads) {
+                const uint32_t g = i / (maxe * k);
+                const uint32_t rem = i - g * maxe * k;
+                const uint32_t r = rem / k, j = rem - r * k;
+                const uint8_t* P = plans + g * a.plan_stride;
+                const uint8_t c = r < P[0] ? P[4 + maxe + k + r * k + j] : 0;
+                tabs[i] = gf::make_permtab(c);
+            }
+        }
+        __syncthreads();
+        const uint32_t nitems = gt * a.cps;
+        for (uint32_t base = 0; base < nitems; base += kThreads) {
+            const uint32_t t = base + threadIdx.x;
+            const bool inr = t < nitems;
+            const uint32_t g = inr ? fdiv(t, a.div_cps) : 0;
+            const uint32_t c = t - g * a.cps;
+            const uint8_t* P = plans + g * a.plan_stride;
+            const uint32_t nout = inr ? P[0] : 0;
+            uint32_t rows = 0;
+#pragma unroll
+            for (int r = 0; r < MAXE; ++r)
+                if (__any((int)nout > r)) rows = r + 1;
+            if (nout == 0) continue;
+            const uint8_t* in_idx = P + 4 + maxe;
+            const gf::PermTab* T = tabs + g * maxe * k;
+            uint8_t* blk = a.shards + (uint64_t)(b0 + g) * a.bs + (uint64_t)c * kChunk;
+            uint4 acc[MAXE];
+#pragma unroll
+            for (int r = 0; r < MAXE; ++r) acc[r] = make_uint4(0, 0, 0, 0);
+            for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
+                uint4 x[kInGroup];
+#pragma unroll
+                for (int jj = 0; jj < kInGroup; ++jj) {
+                    const uint32_t j = min(j0 + jj, k - 1);
+                    x[jj] = ld16(blk + (uint64_t)in_idx[j] * a.ss);
+                }
+#pragma unroll
+                for (int jj = 0; jj < kInGroup; ++jj) {
+                    if (j0 + jj < k) {
+                        const Idx ix[4] = {split(x[jj].x), split(x[jj].y), split(x[jj].z), split(x[jj].w)};
+#pragma unroll
+                        for (int r = 0; r < MAXE; ++r)
+                            if (r < (int)rows) mac(acc[r], ix, T + r * k + j0 + jj);
+                    }
+                }
+            }
+            const uint32_t nb = a.len - c * kChunk;
+            const uint8_t* out_idx = P + 4;
+#pragma unroll
+            for (int r = 0; r < MAXE; ++r)
+                if (r < (int)nout) store_chunk(blk + (uint64_t)out_idx[r] * a.ss, acc[r], nb);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ XOR
+__global__ __launch_bounds__(kThreads) void xor_encode_kernel(XorArgs a) {
+    const uint32_t k = a.k;
+    const uint32_t stride = gridDim.x * kThreads;
+    for (uint32_t item = blockIdx.x * kThreads + threadIdx.x; item < a.total; item += stride) {
+        const uint32_t b = fdiv(item, a.div_cps);
+        const uint32_t c = item - b * a.cps;
+        const uint8_t* src = a.in + (uint64_t)b * a.in_bs + (uint64_t)c * kChunk;
+        uint4 acc = make_uint4(0, 0, 0, 0);
+        for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
+            uint4 x[kInGroup];
+#pragma unroll
+            for (int jj = 0; jj < kInGroup; ++jj) x[jj] = ld16(src + (uint64_t)min(j0 + jj, k - 1) * a.ss);
+#pragma unroll
+            for (int jj = 0; jj < kInGroup; ++jj)
+                if (j0 + jj < k) {
+                    acc.x ^= x[jj].x;
+                    acc.y ^= x[jj].y;
+                    acc.z ^= x[jj].z;
+                    acc.w ^= x[jj].w;
+                }
+        }
+        store_chunk(a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk, acc, a.len - c * kChunk);
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
+    const uint32_t k = a.k, n = k + 1;
+    const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
+    const uint32_t stride = gridDim.x * kThreads;
+    for (uint32_t item = blockIdx.x * kThreads + threadIdx.x; item < a.total; item += stride) {
+        const uint32_t b = fdiv(item, a.div_cps);
+        const uint32_t c = item - b * a.cps;
+        const uint32_t miss = ~a.masks[b] & all;
+        const uint32_t nmiss = __popc(miss);
+        const uint32_t mi = miss ? (uint32_t)__ffs(miss) - 1 : 0;
+        const bool work = nmiss == 1 && mi < k;
+        const bool fail = nmiss > 1 && (miss & ((1u << k) - 1u));
+        if (c == 0) {
+            if (a.status) a.status[b] = fail ? -4 : 0;
+            if (fail) atomicOr(a.err, 1);
+        }
+        if (!work) continue;
+        uint8_t* blk = a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk;
+        uint4 acc = make_uint4(0, 0, 0, 0);
+        for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
+            uint4 x[kInGroup];
+#pragma unroll
+            for (int jj = 0; jj < kInGroup; ++jj) {
+                const uint32_t j = min(j0 + jj, k - 1);
+                x[jj] = ld16(blk + (uint64_t)(j + (j >= mi)) * a.ss);
+            }
+#pragma unroll
+            for (int jj = 0; jj < kInGroup; ++jj)
+                if (j0 + jj < k) {
+                    acc.x ^= x[jj].x;
+                    acc.y ^= x[jj].y;
+                    acc.z ^= x[jj].z;
+                    acc.w ^= x[jj].w;
+                }
+        }
+        store_chunk(blk + (uint64_t)mi * a.ss, acc, a.len - c * kChunk);
+    }
+}
+
+// ------------------------------------------------------------------ launchers
+template <int MAXM>
+static hipError_t enc_dispatch(const EncodeArgs& a, int grid, hipStream_t s) {
+    const size_t lds = (size_t)a.m * a.k * sizeof(gf::PermTab);
+    if (a.m * a.k <= (uint32_t)kMaxLdsTabs)
+        hipLaunchKernelGGL((rs_encode_kernel<MAXM, true>), dim3(grid), dim3(kThreads), lds, s, a);
+    else
+        hipLaunchKernelGGL((rs_encode_kernel<MAXM, false>), dim3(grid), dim3(kThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_rs_encode(const EncodeArgs& a, int grid, hipStream_t s) {
+    if (a.m <= 1) return enc_dispatch<1>(a, grid, s);
+    if (a.m <= 2) return enc_dispatch<2>(a, grid, s);
+    if (a.m <= 4) return enc_dispatch<4>(a, grid, s);
+    if (a.m <= 8) return enc_dispatch<8>(a, grid, s);
+    return enc_dispatch<16>(a, grid, s);   // caller splits m > 16
+}
+
+hipError_t launch_rs_plan(const PlanArgs& a, hipStream_t s) {
+    const int grid = (int)((a.nblocks + kThreads - 1) / kThreads);
+    if (grid == 0) return hipSuccess;
+    if (a.maxe <= 1) hipLaunchKernelGGL(rs_plan_kernel<1>, dim3(grid), dim3(kThreads), 0, s, a);
+    else if (a.maxe <= 2) hipLaunchKernelGGL(rs_plan_kernel<2>, dim3(grid), dim3(kThreads), 0, s, a);
+    else if (a.maxe <= 4) hipLaunchKernelGGL(rs_plan_kernel<4>, dim3(grid), dim3(kThreads), 0, s, a);
+    else if (a.maxe <= 8) hipLaunchKernelGGL(rs_plan_kernel<8>, dim3(grid), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL(rs_plan_kernel<16>, dim3(grid), dim3(kThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+static size_t recon_lds(const ReconArgs& a) {
+    return (size_t)a.g * a.maxe * a.k * sizeof(gf::PermTab) + (size_t)a.g * a.plan_stride;
+}
+
+hipError_t launch_rs_reconstruct(const ReconArgs& a, int grid, hipStream_t s) {
+    const size_t lds = recon_lds(a);
+    if (a.maxe <= 1) hipLaunchKernelGGL(rs_reconstruct_kernel<1>, dim3(grid), dim3(kThreads), lds, s, a);
+    else if (a.maxe <= 2) hipLaunchKernelGGL(rs_reconstruct_kernel<2>, dim3(grid), dim3(kThreads), lds, s, a);
+    else if (a.maxe <= 4) hipLaunchKernelGGL(rs_reconstruct_kernel<4>, dim3(grid), dim3(kThreads), lds, s, a);
+    else if (a.maxe <= 8) hipLaunchKernelGGL(rs_reconstruct_kernel<8>, dim3(grid), dim3(kThreads), lds, s, a);
+    else hipLaunchKernelGGL(rs_reconstruct_kernel<16>, dim3(grid), dim3(kThreads), lds, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_xor_encode(const XorArgs& a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(xor_encode_kernel, dim3(grid), dim3(kThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_xor_reconstruct(const XorArgs& a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(xor_reconstruct_kernel, dim3(grid), dim3(kThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+uint32_t pick_tile_blocks(uint32_t cps, uint32_t k, uint32_t maxe) {
+    // Blocks per tile: the smallest count that reaches the best lane utilisation of the
+    // G*cps items over 256 lanes within 8 rounds, bounded by 48 KiB of LDS per tile.
+    const size_t per_block = (size_t)maxe * k * sizeof(gf::PermTab) + plan_stride_bytes(k, maxe);
+    uint32_t gmax = (uint32_t)((48u * 1024u) / per_block);
+    if (gmax < 1) gmax = 1;
+    if (gmax > 256) gmax = 256;
+    uint32_t best = 1;
+    double best_u = -1.0;
+    for (uint32_t g = 1; g <= gmax; ++g) {
+        const uint32_t items = g * cps;
+        const uint32_t rounds = (items + kThreads - 1) / kThreads;
+        if (rounds > 8) break;
+        const double u = (double)items / (double)(rounds * kThreads);
+        if (u > best_u + 1e-3) {
+            best = g;
+            best_u = u;
+        }
+    }
+    return best;
+}
+
+int occupancy_grid(int device, int which, uint32_t sel, size_t lds) {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0)
+        ncu = 256;
+    int per = 0;
+    const void* fn = nullptr;
+    if (which == 0) {   // encode
+        if (sel <= 1) fn = (const void*)rs_encode_kernel<1, true>;
+        else if (sel <= 2) fn = (const void*)rs_encode_kernel<2, true>;
+        else if (sel <= 4) fn = (const void*)rs_encode_kernel<4, true>;
+        else if (sel <= 8) fn = (const void*)rs_encode_kernel<8, true>;
+        else fn = (const void*)rs_encode_kernel<16, true>;
+    } else if (which == 1) {
+        if (sel <= 1) fn = (const void*)rs_reconstruct_kernel<1>;
+        else if (sel <= 2) fn = (const void*)rs_reconstruct_kernel<2>;
+        else if (sel <= 4) fn = (const void*)rs_reconstruct_kernel<4>;
+        else if (sel <= 8) fn = (const void*)rs_reconstruct_kernel<8>;
+        else fn = (const void*)rs_reconstruct_kernel<16>;
+    } else {
+        fn = (const void*)xor_encode_kernel;
+    }
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kThreads, lds) != hipSuccess || per <= 0)
+        per = 4;
+    if (per > 8) per = 8;
+    return ncu * per;
+}
+
+}  // namespace fk

@@ -1,0 +1,211 @@
+"""GPU parity of the batch codec (C ABI, include/fec_hip.h) against the CPU oracle.
+
+Bit-exact comparison on seeded inputs, device-resident (FEC_DEVICE via torch CUDA tensors) and
+host-resident (FEC_HOST via numpy), over shapes that cover the reference's configurations
+(XOR(2,1), RS(6,2), RS(20,10) factories and tests: internal/fec/manager.go:54-90,
+reed_solomon_test.go) and the benchmark ones (RS(2,3)-style (2,1), (8,4), (16,8)),
+odd shard lengths (tail chunks), every erasure count, and the too-few-shards error.
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(1, 1), (2, 1), (3, 2), (6, 2), (8, 4), (16, 8), (20, 10), (5, 11), (31, 1), (10, 22)]
+LENS = [1, 2, 3, 15, 16, 17, 33, 1202, 1436]
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "GPU test needs a HIP device"
+    return t
+
+
+@pytest.fixture(scope="module")
+def codec(fec):
+    import torch
+    c = fec.Codec(0).use_torch_stream()
+    yield c
+    c.close()
+
+
+def _rand_shards(rng, B, n, S, L):
+    sh = np.zeros((B, n, S), dtype=np.uint8)
+    sh[:, :, :L] = rng.integers(0, 256, (B, n, L), dtype=np.uint8)
+    return sh
+
+
+def _random_masks(rng, B, k, m, max_loss=None):
+    n = k + m
+    max_loss = m if max_loss is None else max_loss
+    masks = np.empty(B, dtype=np.uint32)
+    for b in range(B):
+        e = int(rng.integers(0, max_loss + 1))
+        lost = rng.choice(n, size=e, replace=False)
+        masks[b] = ((1 << n) - 1) & ~int(sum(1 << int(i) for i in lost))
+    return masks
+
+
+@pytest.mark.parametrize("k,m", SHAPES)
+@pytest.mark.parametrize("L", LENS)
+def test_rs_encode_device_matches_oracle(codec, oracle, torch, k, m, L):
+    rng = np.random.default_rng(1000 * k + 10 * m + L)
+    n = k + m
+    S = (L + 15) // 16 * 16 + 16 * int(rng.integers(0, 2))
+    B = 37
+    sh = _rand_shards(rng, B, n, S, L)
+    sh[:, k:, :] = 0xA5                          # parity slots pre-filled: only [0, L) may change
+    ref = sh.copy()
+    oracle.rs_encode(k, m, ref)
+    ref[:, k:, L:] = 0xA5
+    d = torch.from_numpy(sh).cuda()
+    codec.rs_encode(k, m, d, shard_len=L)
+    codec.sync()
+    got = d.cpu().numpy()
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("k,m", SHAPES)
+@pytest.mark.parametrize("L", [1, 17, 1202])
+def test_rs_reconstruct_device_matches_oracle(codec, oracle, torch, k, m, L):
+    if k + m > 32:
+        pytest.skip("decode limited to n <= 32")
+    rng = np.random.default_rng(7 * k + m + L)
+    n = k + m
+    S = (L + 15) // 16 * 16
+    B = 301
+    sh = _rand_shards(rng, B, n, S, L)
+    oracle.rs_encode(k, m, sh)
+    masks = _random_masks(rng, B, k, m, max_loss=min(n, m + 1))
+    damaged = sh.copy()
+    for b in range(B):
+        for i in range(n):
+            if not (masks[b] >> i) & 1:
+                damaged[b, i, :] = 0x5A
+    ref = damaged.copy()
+    st_ref = oracle.rs_reconstruct(k, m, ref, masks, length=L)
+    d = torch.from_numpy(damaged).cuda()
+    dm = torch.from_numpy(masks.view(np.int32)).cuda()
+    ds = torch.full((B,), 99, dtype=torch.int32, device="cuda")
+    codec.rs_reconstruct(k, m, d, dm, status=ds, shard_len=L)
+    st = ds.cpu().numpy()
+    assert np.array_equal(st == 0, st_ref == 0)
+    assert set(np.unique(st)).issubset({0, -4})
+    got = d.cpu().numpy()
+    assert np.array_equal(got, ref)
+    # recovered blocks equal the original data
+    ok = st_ref == 0
+    assert np.array_equal(got[ok, :k, :L], sh[ok, :k, :L])
+    if (st_ref != 0).any():
+        from importlib import import_module
+        fec = import_module("0xfec_amd")
+        with pytest.raises(fec.FecError):
+            codec.sync()
+    else:
+        codec.sync()
+
+
+def test_rs_every_erasure_pattern_8_12(codec, oracle, torch):
+    """Every pattern of <= 4 losses of RS(8,12) (794 patterns), 1202-byte shards."""
+    k, m, L = 8, 4, 1202
+    n = k + m
+    pats = [p for r in range(0, m + 1) for p in itertools.combinations(range(n), r)]
+    B = len(pats)
+    rng = np.random.default_rng(0x0FEC)
+    S = 1216
+    sh = _rand_shards(rng, B, n, S, L)
+    oracle.rs_encode(k, m, sh)
+    masks = np.array([((1 << n) - 1) & ~sum(1 << i for i in p) for p in pats], dtype=np.uint32)
+    dmg = sh.copy()
+    for b, p in enumerate(pats):
+        for i in p:
+            dmg[b, i] = 0
+    d = torch.from_numpy(dmg).cuda()
+    codec.rs_reconstruct(k, m, d, torch.from_numpy(masks.view(np.int32)).cuda())
+    codec.sync()
+    got = d.cpu().numpy()
+    assert np.array_equal(got[:, :k, :L], sh[:, :k, :L])
+
+
+@pytest.mark.parametrize("k,m", [(2, 1), (6, 2), (8, 4), (20, 10)])
+def test_rs_host_path_matches_oracle(codec, oracle, k, m):
+    fec = __import__("importlib").import_module("0xfec_amd")
+    rng = np.random.default_rng(k * m)
+    n, L = k + m, 1202
+    B = 129
+    sh = _rand_shards(rng, B, n, L, L)       # packed host layout, stride == shard_len
+    ref = sh.copy()
+    oracle.rs_encode(k, m, ref)
+    codec.rs_encode(k, m, sh)
+    assert np.array_equal(sh, ref)
+    masks = _random_masks(rng, B, k, m)
+    dmg = sh.copy()
+    for b in range(B):
+        for i in range(n):
+            if not (masks[b] >> i) & 1:
+                dmg[b, i] = 0
+    st = np.full(B, 7, dtype=np.int32)
+    rc = codec.rs_reconstruct(k, m, dmg, masks, status=st)
+    assert rc == fec.FEC_OK and (st == 0).all()
+    assert np.array_equal(dmg[:, :k], sh[:, :k])
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 9, 31])
+@pytest.mark.parametrize("L", [1, 6, 18, 1202, 1436])
+def test_xor_device_matches_oracle(codec, oracle, torch, k, L):
+    rng = np.random.default_rng(k + L)
+    n = k + 1
+    S = (L + 15) // 16 * 16
+    B = 65
+    sh = _rand_shards(rng, B, n, S, L)
+    ref = sh.copy()
+    oracle.xor_encode(k, ref)
+    d = torch.from_numpy(sh).cuda()
+    codec.xor_encode(k, d, shard_len=L)
+    codec.sync()
+    enc = d.cpu().numpy()
+    assert np.array_equal(enc[:, :, :L], ref[:, :, :L])
+    masks = _random_masks(rng, B, k, 1, max_loss=2)
+    dmg = enc.copy()
+    for b in range(B):
+        for i in range(n):
+            if not (masks[b] >> i) & 1:
+                dmg[b, i] = 0x33
+    want = dmg.copy()
+    st_ref = oracle.xor_reconstruct(k, want, masks)
+    dd = torch.from_numpy(dmg).cuda()
+    ds = torch.zeros(B, dtype=torch.int32, device="cuda")
+    codec.xor_reconstruct(k, dd, torch.from_numpy(masks.view(np.int32)).cuda(), status=ds, shard_len=L)
+    try:
+        codec.sync()
+    except Exception:
+        pass
+    got = dd.cpu().numpy()
+    st = ds.cpu().numpy()
+    assert np.array_equal(st == 0, st_ref == 0)
+    ok = st_ref == 0
+    assert np.array_equal(got[ok][:, :, :L], want[ok][:, :, :L])
+
+
+def test_argument_errors(codec, torch, fec):
+    d = torch.zeros((4, 3, 32), dtype=torch.uint8, device="cuda")
+    with pytest.raises(fec.FecError) as e:
+        codec.rs_encode(0, 3, d)
+    assert e.value.code == fec.FEC_ERR_INV_SHARD_NUM
+    with pytest.raises(fec.FecError) as e:
+        codec.rs_encode_raw(200, 57, 16, 1, d.data_ptr(), 32, d.data_ptr(), 32, 16, fec.FEC_DEVICE)
+    assert e.value.code == fec.FEC_ERR_MAX_SHARD_NUM
+    with pytest.raises(fec.FecError) as e:
+        codec.rs_encode_raw(2, 1, 16, 1, d.data_ptr() + 1, 48, d.data_ptr() + 33, 48, 16, fec.FEC_DEVICE)
+    assert e.value.code == fec.FEC_ERR_ALIGNMENT
+    with pytest.raises(fec.FecError) as e:
+        codec.rs_encode_raw(2, 1, 0, 1, d.data_ptr(), 48, d.data_ptr() + 32, 48, 16, fec.FEC_DEVICE)
+    assert e.value.code == fec.FEC_ERR_SHARD_NO_DATA
+    assert codec.rs_reconstruct_raw(20, 13, 16, 1, d.data_ptr(), 48, 16, d.data_ptr(), None,
+                                    fec.FEC_DEVICE) == fec.FEC_ERR_MAX_SHARD_NUM
+    # empty batches are no-ops
+    codec.rs_encode_raw(2, 1, 16, 0, d.data_ptr(), 48, d.data_ptr() + 32, 48, 16, fec.FEC_DEVICE)
+    codec.sync()
