@@ -11,6 +11,16 @@ Import by name (the directory starts with a digit):
 import ctypes
 import os
 
+# PyTorch-ROCm ships its own libamdhip64.so (same SONAME, libamdhip64.so.7). Loading torch
+# first makes the dynamic linker bind this library to that one runtime, so device pointers,
+# streams and events are shared with torch; loading ours first would start a second HIP
+# runtime in the process, and torch then finds no GPU. Without torch (e.g. a cgo host) the
+# library binds to /opt/rocm's runtime.
+try:
+    import torch as _torch  # noqa: F401
+except ImportError:
+    _torch = None
+
 from ._build import LIB as _LIB_PATH
 
 if not os.path.exists(_LIB_PATH):
@@ -47,6 +57,7 @@ lib.fec_ctx_create.argtypes = [_i, ctypes.POINTER(_vp)]
 lib.fec_ctx_destroy.argtypes = [_vp]
 lib.fec_ctx_destroy.restype = None
 lib.fec_ctx_set_stream.argtypes = [_vp, _vp]
+lib.fec_ctx_reset_stream.argtypes = [_vp]
 lib.fec_ctx_stream.argtypes = [_vp]
 lib.fec_ctx_stream.restype = _vp
 lib.fec_sync.argtypes = [_vp]
@@ -141,7 +152,11 @@ class Codec:
         return lib.fec_ctx_stream(self._h)
 
     def set_stream(self, stream_ptr):
+        """Enqueue on an external hipStream_t (0/None = the null stream)."""
         _check(lib.fec_ctx_set_stream(self._h, stream_ptr or None))
+
+    def reset_stream(self):
+        _check(lib.fec_ctx_reset_stream(self._h))
 
     def use_torch_stream(self):
         """Enqueue on torch's current stream of this device, so codec calls order naturally

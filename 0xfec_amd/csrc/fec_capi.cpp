@@ -379,7 +379,13 @@ void fec_ctx_destroy(fec_ctx* ctx) {
 
 int fec_ctx_set_stream(fec_ctx* ctx, void* hip_stream) {
     if (!ctx) return FEC_ERR_INVALID_ARG;
-    ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own;
+    ctx->stream = (hipStream_t)hip_stream;
+    return FEC_OK;
+}
+
+int fec_ctx_reset_stream(fec_ctx* ctx) {
+    if (!ctx) return FEC_ERR_INVALID_ARG;
+    ctx->stream = ctx->own;
     return FEC_OK;
 }
 

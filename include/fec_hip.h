@@ -75,8 +75,10 @@ int fec_device_count(int *count);
 /* Context: device binding, one HIP stream, cached code matrices, workspace, pinned staging. */
 int fec_ctx_create(int device, fec_ctx **out);
 void fec_ctx_destroy(fec_ctx *ctx);
-/* Run subsequent work on an external hipStream_t (NULL restores the ctx-owned stream). */
+/* Run subsequent work on an external hipStream_t (NULL = the device's null stream). */
 int fec_ctx_set_stream(fec_ctx *ctx, void *hip_stream);
+/* Go back to the ctx-owned stream. */
+int fec_ctx_reset_stream(fec_ctx *ctx);
 void *fec_ctx_stream(fec_ctx *ctx);
 /* Wait for the ctx stream. Returns FEC_ERR_TOO_FEW_SHARDS if any FEC_DEVICE reconstruct
  * since the last fec_sync met a block with fewer than k present shards (then clears it). */
