@@ -6,6 +6,7 @@
 // entry point fails with FEC_ERR_NO_DEVICE / FEC_ERR_HIP.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -143,11 +144,20 @@ static int slot_of(uint32_t sel) { return sel <= 1 ? 0 : sel <= 2 ? 1 : sel <= 4
 
 static int grid_for(fec_ctx* ctx, int which, uint32_t sel, size_t lds) {
     int& g = ctx->grid_cache[which][slot_of(sel)];
-    if (g == 0) g = fk::occupancy_grid(ctx->device, which, sel, lds);
+    if (g == 0) g = fk::occupancy_grid(ctx->device, which, sel, lds) * std::max(1, fk::g_tune.grid_mult);
     return g;
 }
 
 static size_t round16(size_t x) { return (x + 15) & ~size_t(15); }
+
+// Workgroups for a flat (block, chunk) item launch.
+static int flat_grid(int resident, uint32_t total) {
+    const uint64_t all = ((uint64_t)total + fk::kThreads - 1) / fk::kThreads;
+    uint64_t g = (uint64_t)resident;
+    if (fk::g_tune.items_per_thread > 0) g = (all + fk::g_tune.items_per_thread - 1) / fk::g_tune.items_per_thread;
+    g = std::min<uint64_t>(g, all);
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>(g, 0x7FFFFFFF));
+}
 
 // ---------------------------------------------------------------- device-memory cores
 
@@ -173,9 +183,10 @@ static int rs_encode_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks
             a.total = (uint32_t)(nb * cps);
             a.div_cps = fk::make_fastdiv(cps);
             a.tabs = code->d_tabs + (size_t)r0 * k * 8;
+            a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
             const size_t lds = (size_t)mr * k * sizeof(gf::PermTab);
             int grid = grid_for(ctx, 0, (uint32_t)mr, lds <= 65536 ? lds : 0);
-            grid = (int)std::min<uint64_t>((uint64_t)grid, (a.total + fk::kThreads - 1) / fk::kThreads);
+            grid = flat_grid(grid, a.total);
             if (grid < 1) grid = 1;
             HIP_TRY(fk::launch_rs_encode(a, grid, ctx->stream));
         }
@@ -188,12 +199,13 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
     const uint32_t k = (uint32_t)code->k, m = (uint32_t)code->m;
     const uint32_t maxe = std::max<uint32_t>(1, std::min(k, m));
     const uint32_t cps = (uint32_t)((len + fk::kChunk - 1) / fk::kChunk);
-    const uint32_t ps = fk::plan_stride_bytes(k, maxe);
-    size_t per_launch = std::min<size_t>(kPlanBytes / ps, (size_t)(kMaxItems / cps));
+    const fk::PlanLayout lay = fk::plan_layout(k, maxe);
+    size_t per_launch = std::min<size_t>(kPlanBytes / lay.stride, (size_t)(kMaxItems / cps));
     per_launch = std::max<size_t>(1, std::min(per_launch, nblocks));
-    int rc = grow_plans(ctx, per_launch * ps);
+    int rc = grow_plans(ctx, per_launch * lay.stride);
     if (rc) return rc;
-    const uint32_t G = fk::pick_tile_blocks(cps, k, maxe);
+    const uint32_t G = fk::pick_tile_blocks(cps, k, maxe, lay);
+    const size_t lds = fk::recon_lds_bytes(G, k, maxe, lay);
     for (size_t b0 = 0; b0 < nblocks; b0 += per_launch) {
         const size_t nb = std::min(per_launch, nblocks - b0);
         fk::PlanArgs p{};
@@ -205,8 +217,8 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         p.k = k;
         p.m = m;
         p.nblocks = (uint32_t)nb;
-        p.plan_stride = ps;
         p.maxe = maxe;
+        p.lay = lay;
         HIP_TRY(fk::launch_rs_plan(p, ctx->stream));
         fk::ReconArgs a{};
         a.shards = shards + b0 * bs;
@@ -217,15 +229,18 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         a.len = (uint32_t)len;
         a.cps = cps;
         a.nblocks = (uint32_t)nb;
-        a.plan_stride = ps;
         a.maxe = maxe;
+        a.lay = lay;
         a.g = G;
         a.ntiles = (uint32_t)((nb + G - 1) / G);
         a.div_cps = fk::make_fastdiv(cps);
-        const size_t lds = (size_t)G * maxe * k * sizeof(gf::PermTab) + (size_t)G * ps;
-        int grid = grid_for(ctx, 1, maxe, lds);
-        grid = std::min<int>(grid, (int)a.ntiles);
-        if (grid < 1) grid = 1;
+        a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
+        int grid;
+        if (fk::g_tune.tiles_per_wg > 0)
+            grid = (int)((a.ntiles + fk::g_tune.tiles_per_wg - 1) / fk::g_tune.tiles_per_wg);
+        else
+            grid = grid_for(ctx, 1, maxe, lds);
+        grid = std::max(1, std::min<int>(grid, (int)a.ntiles));
         HIP_TRY(fk::launch_rs_reconstruct(a, grid, ctx->stream));
     }
     return FEC_OK;
@@ -248,8 +263,9 @@ static int xor_encode_device(fec_ctx* ctx, int k, size_t len, size_t nblocks, co
         a.cps = cps;
         a.total = (uint32_t)(nb * cps);
         a.div_cps = fk::make_fastdiv(cps);
+        a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
         int grid = grid_for(ctx, 2, 1, 0);
-        grid = (int)std::min<uint64_t>((uint64_t)grid, (a.total + fk::kThreads - 1) / fk::kThreads);
+        grid = flat_grid(grid, a.total);
         if (grid < 1) grid = 1;
         HIP_TRY(fk::launch_xor_encode(a, grid, ctx->stream));
     }
@@ -276,8 +292,9 @@ static int xor_reconstruct_device(fec_ctx* ctx, int k, size_t len, size_t nblock
         a.cps = cps;
         a.total = (uint32_t)(nb * cps);
         a.div_cps = fk::make_fastdiv(cps);
+        a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
         int grid = grid_for(ctx, 2, 1, 0);
-        grid = (int)std::min<uint64_t>((uint64_t)grid, (a.total + fk::kThreads - 1) / fk::kThreads);
+        grid = flat_grid(grid, a.total);
         if (grid < 1) grid = 1;
         HIP_TRY(fk::launch_xor_reconstruct(a, grid, ctx->stream));
     }
@@ -381,6 +398,24 @@ int fec_ctx_set_stream(fec_ctx* ctx, void* hip_stream) {
     if (!ctx) return FEC_ERR_INVALID_ARG;
     ctx->stream = (hipStream_t)hip_stream;
     return FEC_OK;
+}
+
+// Internal tuning knob (not part of the public ABI; process-wide): kernel variants and grid
+// sizing, A/B-tested by tools/kbench.py. Keys: 0 encode/XOR nt, 1 decode nt, 2 persistent grid
+// multiplier, 3 decode max rounds per tile, 4 zero-padded tail stores, 5 items per thread
+// (flat kernels, 0 = persistent), 6 tiles per workgroup (decode, 0 = persistent).
+// Returns the previous value.
+int fec__set_tuning(fec_ctx* ctx, int key, int value) {
+    if (!ctx) return FEC_ERR_INVALID_ARG;
+    int* slot = key == 0 ? &fk::g_tune.enc_nt : key == 1 ? &fk::g_tune.dec_nt
+              : key == 2 ? &fk::g_tune.grid_mult : key == 3 ? &fk::g_tune.dec_max_rounds
+              : key == 4 ? &fk::g_tune.pad_zero : key == 5 ? &fk::g_tune.items_per_thread
+              : key == 6 ? &fk::g_tune.tiles_per_wg : nullptr;
+    if (!slot) return FEC_ERR_INVALID_ARG;
+    const int old = *slot;
+    *slot = value;
+    memset(ctx->grid_cache, 0, sizeof(ctx->grid_cache));
+    return old;
 }
 
 int fec_ctx_reset_stream(fec_ctx* ctx) {

@@ -12,12 +12,16 @@
 //   * decode solves only the e x e system of the erased data shards per block
 //     (rs_plan_kernel), which is the same linear solution klauspost computes from the
 //     full k x k inverse of the first k present rows.
+// Grid shapes, non-temporal access and tail-store form were chosen by measurement
+// (tools/kbench.py; DESIGN.md "Kernel tuning").
 #include <hip/hip_runtime.h>
 
 #include "fec_kernels.hpp"
 #include "gf256.h"
 
 namespace fk {
+
+Tuning g_tune;
 
 FastDiv make_fastdiv(uint32_t d) {
     FastDiv f{d, 0, 0};
@@ -26,6 +30,16 @@ FastDiv make_fastdiv(uint32_t d) {
     f.shift = l;
     f.magic = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
     return f;
+}
+
+PlanLayout plan_layout(uint32_t k, uint32_t maxe) {
+    PlanLayout l;
+    l.in_off = 0;
+    l.out_off = 32;                                  // in slots: 32 bytes (k <= 31)
+    l.nout_off = l.out_off + maxe;
+    l.coef_off = (l.nout_off + 1 + 3) & ~3u;
+    l.stride = (l.coef_off + maxe * k + 15) & ~15u;
+    return l;
 }
 
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
@@ -41,30 +55,44 @@ __device__ __forceinline__ Idx split(uint32_t x) {
     return {x & 0x07070707u, (x >> 3) & 0x07070707u, (x >> 6) & 0x03030303u};
 }
 
-// c * x for four packed bytes, c given by its PermTab.
+// c * x for four packed bytes, c given by its PermTab words.
 __device__ __forceinline__ uint32_t gmul(const Idx& i, uint32_t t0lo, uint32_t t0hi, uint32_t t1lo,
                                          uint32_t t1hi, uint32_t t2) {
     return __builtin_amdgcn_perm(t0hi, t0lo, i.a) ^ __builtin_amdgcn_perm(t1hi, t1lo, i.b) ^
            __builtin_amdgcn_perm(t2, t2, i.c);
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
 __device__ __forceinline__ uint4 ld16(const uint8_t* p) {
-    return *reinterpret_cast<const uint4*>(p);
+    if constexpr (NT) {
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return *reinterpret_cast<const uint4*>(p);
+    }
 }
 
-__device__ __forceinline__ void st16(uint8_t* p, uint4 v) {
-    *reinterpret_cast<uint4*>(p) = v;
+template <bool NT>
+__device__ __forceinline__ void st16(uint8_t* p, const uint4& v) {
+    if constexpr (NT) {
+        const u32x4 w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+    } else {
+        *reinterpret_cast<uint4*>(p) = v;
+    }
 }
 
-__device__ __forceinline__ uint32_t lane_of(const uint4& v, int d) {
+__device__ __forceinline__ uint32_t word_of(const uint4& v, int d) {
     return d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
 }
 
-// Store the first nb (< 16) bytes of v.
+// Store the first nb (< 16) bytes of v, byte-exact.
 __device__ __forceinline__ void st_partial(uint8_t* p, const uint4& v, uint32_t nb) {
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-        const uint32_t w = lane_of(v, d);
+        const uint32_t w = word_of(v, d);
         if (4u * d + 4u <= nb) {
             *reinterpret_cast<uint32_t*>(p + 4 * d) = w;
         } else if (4u * d < nb) {
@@ -75,14 +103,30 @@ __device__ __forceinline__ void st_partial(uint8_t* p, const uint4& v, uint32_t 
     }
 }
 
-__device__ __forceinline__ void store_chunk(uint8_t* p, const uint4& v, uint32_t nb) {
+// Keep only the first nb bytes of v (zero the rest).
+__device__ __forceinline__ uint4 keep_bytes(const uint4& v, uint32_t nb) {
+    auto m = [nb](int d) -> uint32_t {
+        const int rem = (int)nb - 4 * d;
+        return rem >= 4 ? 0xFFFFFFFFu : rem <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * rem));
+    };
+    return make_uint4(v.x & m(0), v.y & m(1), v.z & m(2), v.w & m(3));
+}
+
+// Store one output chunk holding nb valid bytes. A partial tail chunk is either one full
+// 16-byte store with the bytes past nb zeroed (pad_zero: the slot padding up to the 16-byte
+// boundary is written as zeros, which avoids partially written cache lines) or a byte-exact
+// partial store.
+template <bool NT>
+__device__ __forceinline__ void store_chunk(uint8_t* p, const uint4& v, uint32_t nb, uint32_t pad_zero) {
     if (nb >= 16)
-        st16(p, v);
+        st16<NT>(p, v);
+    else if (pad_zero)
+        st16<NT>(p, keep_bytes(v, nb));
     else
         st_partial(p, v, nb);
 }
 
-// acc ^= tab * x, for one 16-byte chunk.
+// acc ^= c * x for one 16-byte chunk (c given by its PermTab, read from LDS).
 __device__ __forceinline__ void mac(uint4& acc, const Idx (&ix)[4], const gf::PermTab* t) {
     const uint4 lo = *reinterpret_cast<const uint4*>(t);   // t0lo t0hi t1lo t1hi
     const uint32_t t2 = t->t2;
@@ -94,7 +138,9 @@ __device__ __forceinline__ void mac(uint4& acc, const Idx (&ix)[4], const gf::Pe
 
 // ------------------------------------------------------------------ RS encode
 // One lane = one 16-byte column chunk of one block; all m parities accumulate in VGPRs.
-template <int MAXM, bool LDS_TABS>
+// Inputs are loaded 8 shards at a time (clamped, so loads are never predicated), then
+// each input updates every parity accumulator with its LDS-broadcast PermTab.
+template <int MAXM, bool LDS_TABS, bool NT>
 __global__ __launch_bounds__(kThreads) void rs_encode_kernel(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const gf::PermTab* tabs;
@@ -119,10 +165,7 @@ __global__ __launch_bounds__(kThreads) void rs_encode_kernel(EncodeArgs a) {
         for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
             uint4 x[kInGroup];
 #pragma unroll
-            for (int jj = 0; jj < kInGroup; ++jj) {
-                const uint32_t j = min(j0 + jj, k - 1);   // clamp: loads stay unconditional
-                x[jj] = ld16(src + (uint64_t)j * a.ss);
-            }
+            for (int jj = 0; jj < kInGroup; ++jj) x[jj] = ld16<NT>(src + (uint64_t)min(j0 + jj, k - 1) * a.ss);
 #pragma unroll
             for (int jj = 0; jj < kInGroup; ++jj) {
                 if (j0 + jj < k) {
@@ -137,7 +180,7 @@ __global__ __launch_bounds__(kThreads) void rs_encode_kernel(EncodeArgs a) {
         const uint32_t nb = a.len - c * kChunk;
 #pragma unroll
         for (int r = 0; r < MAXM; ++r)
-            if (r < (int)m) store_chunk(dst + (uint64_t)r * a.ss, acc[r], nb);
+            if (r < (int)m) store_chunk<NT>(dst + (uint64_t)r * a.ss, acc[r], nb, a.pad_zero);
     }
 }
 
@@ -145,7 +188,7 @@ __global__ __launch_bounds__(kThreads) void rs_encode_kernel(EncodeArgs a) {
 // One thread per block. From the present mask: E = erased data shards (e of them),
 // R = first e present parity shards; the first k present shards are then exactly
 // {present data} + R. Solve A[R][E] (e x e) and express each erased shard over those k
-// inputs. Writes the plan (see plan_stride_bytes).
+// inputs. Writes the plan record (PlanLayout).
 template <int MAXE>
 __global__ __launch_bounds__(kThreads) void rs_plan_kernel(PlanArgs a) {
     __shared__ uint8_t s_exp[512];
@@ -161,14 +204,14 @@ __global__ __launch_bounds__(kThreads) void rs_plan_kernel(PlanArgs a) {
     const uint32_t k = a.k, m = a.m, n = k + m;
     const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
     const uint32_t mask = a.masks[b] & all;
-    const uint32_t kmask = k >= 32 ? 0xFFFFFFFFu : ((1u << k) - 1u);
-    uint8_t* P = a.plans + (uint64_t)b * a.plan_stride;
+    const uint32_t kmask = (1u << k) - 1u;   // k <= 31
+    uint8_t* P = a.plans + (uint64_t)b * a.lay.stride;
     const uint32_t e = k - __popc(mask & kmask);
     int32_t st = 0;
     if (e == 0) {
-        P[0] = 0;
+        P[a.lay.nout_off] = 0;
     } else if ((uint32_t)__popc(mask) < k) {
-        P[0] = 0;
+        P[a.lay.nout_off] = 0;
         st = -4;  // FEC_ERR_TOO_FEW_SHARDS
         atomicOr(a.err, 1);
     } else {
@@ -201,10 +244,9 @@ __global__ __launch_bounds__(kThreads) void rs_plan_kernel(PlanArgs a) {
                 for (uint32_t i = 0; i < 2 * e; ++i) A[r][i] ^= (uint8_t)mul(f, A[col][i]);
             }
         }
-        // inputs: present data ascending, then parities R
-        uint8_t* out_idx = P + 4;
-        uint8_t* in_idx = P + 4 + a.maxe;
-        uint8_t* coef = P + 4 + a.maxe + k;
+        uint8_t* in_idx = P + a.lay.in_off;
+        uint8_t* out_idx = P + a.lay.out_off;
+        uint8_t* coef = P + a.lay.coef_off;
         uint32_t pos = 0;
         for (uint32_t j = 0; j < k; ++j) {
             if (!((mask >> j) & 1u)) continue;
@@ -221,7 +263,7 @@ __global__ __launch_bounds__(kThreads) void rs_plan_kernel(PlanArgs a) {
             for (uint32_t i = 0; i < e; ++i) coef[i * k + pos] = A[i][e + t];
         }
         for (uint32_t i = 0; i < e; ++i) out_idx[i] = E[i];
-        P[0] = (uint8_t)e;
+        P[a.lay.nout_off] = (uint8_t)e;
     }
     if (a.status) a.status[b] = st;
 }
@@ -231,20 +273,21 @@ __global__ __launch_bounds__(kThreads) void rs_plan_kernel(PlanArgs a) {
 // every coefficient to its PermTab once, then lanes sweep the G*cps (block, chunk) items.
 // Rows beyond a block's own erasure count carry zero tables, and each item loops only to
 // the wave's largest erasure count (ballot), so one-erasure batches do one row of work.
-template <int MAXE>
+template <int MAXE, bool NT>
 __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t k = a.k, G = a.g, maxe = a.maxe;
+    const PlanLayout lay = a.lay;
     gf::PermTab* tabs = reinterpret_cast<gf::PermTab*>(smem);                // G*maxe*k
-    uint8_t* plans = smem + (size_t)G * maxe * k * sizeof(gf::PermTab);      // G*plan_stride
+    uint8_t* plans = smem + (size_t)G * maxe * k * sizeof(gf::PermTab);      // G*stride
     for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
         const uint32_t b0 = tile * G;
         const uint32_t gt = min(G, a.nblocks - b0);
         __syncthreads();   // previous tile fully consumed
         {
-            const uint32_t nw = gt * a.plan_stride / 4;
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(a.plans + (uint64_t)b0 * a.plan_stride);
-            uint32_t* dst = reinterpret_cast<uint32_t*>(plans);
+            const uint32_t nw = gt * lay.stride / 16;
+            const uint4* src = reinterpret_cast<const uint4*>(a.plans + (uint64_t)b0 * lay.stride);
+            uint4* dst = reinterpret_cast<uint4*>(plans);
             for (uint32_t i = threadIdx.x; i < nw; i += kThreads) dst[i] = src[i];
         }
         __syncthreads();
@@ -254,8 +297,8 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
                 const uint32_t g = i / (maxe * k);
                 const uint32_t rem = i - g * maxe * k;
                 const uint32_t r = rem / k, j = rem - r * k;
-                const uint8_t* P = plans + g * a.plan_stride;
-                const uint8_t c = r < P[0] ? P[4 + maxe + k + r * k + j] : 0;
+                const uint8_t* P = plans + g * lay.stride;
+                const uint8_t c = r < P[lay.nout_off] ? P[lay.coef_off + r * k + j] : 0;
                 tabs[i] = gf::make_permtab(c);
             }
         }
@@ -266,25 +309,28 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
             const bool inr = t < nitems;
             const uint32_t g = inr ? fdiv(t, a.div_cps) : 0;
             const uint32_t c = t - g * a.cps;
-            const uint8_t* P = plans + g * a.plan_stride;
-            const uint32_t nout = inr ? P[0] : 0;
+            const uint8_t* P = plans + g * lay.stride;
+            const uint32_t nout = inr ? P[lay.nout_off] : 0;
             uint32_t rows = 0;
 #pragma unroll
             for (int r = 0; r < MAXE; ++r)
                 if (__any((int)nout > r)) rows = r + 1;
             if (nout == 0) continue;
-            const uint8_t* in_idx = P + 4 + maxe;
             const gf::PermTab* T = tabs + g * maxe * k;
             uint8_t* blk = a.shards + (uint64_t)(b0 + g) * a.bs + (uint64_t)c * kChunk;
             uint4 acc[MAXE];
 #pragma unroll
             for (int r = 0; r < MAXE; ++r) acc[r] = make_uint4(0, 0, 0, 0);
             for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
+                // the 8 input slots of this group, one ds_read_b64
+                const uint2 sl = *reinterpret_cast<const uint2*>(P + lay.in_off + j0);
                 uint4 x[kInGroup];
 #pragma unroll
                 for (int jj = 0; jj < kInGroup; ++jj) {
-                    const uint32_t j = min(j0 + jj, k - 1);
-                    x[jj] = ld16(blk + (uint64_t)in_idx[j] * a.ss);
+                    const uint32_t w = jj < 4 ? sl.x : sl.y;
+                    uint32_t slot = (w >> (8 * (jj & 3))) & 0xFFu;
+                    if (j0 + jj >= k) slot = (sl.x & 0xFFu);   // clamp to a valid shard
+                    x[jj] = ld16<NT>(blk + (uint64_t)slot * a.ss);
                 }
 #pragma unroll
                 for (int jj = 0; jj < kInGroup; ++jj) {
@@ -297,15 +343,16 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
                 }
             }
             const uint32_t nb = a.len - c * kChunk;
-            const uint8_t* out_idx = P + 4;
+            const uint8_t* out_idx = P + lay.out_off;
 #pragma unroll
             for (int r = 0; r < MAXE; ++r)
-                if (r < (int)nout) store_chunk(blk + (uint64_t)out_idx[r] * a.ss, acc[r], nb);
+                if (r < (int)nout) store_chunk<false>(blk + (uint64_t)out_idx[r] * a.ss, acc[r], nb, a.pad_zero);
         }
     }
 }
 
 // ------------------------------------------------------------------ XOR
+template <bool NT>
 __global__ __launch_bounds__(kThreads) void xor_encode_kernel(XorArgs a) {
     const uint32_t k = a.k;
     const uint32_t stride = gridDim.x * kThreads;
@@ -317,7 +364,7 @@ __global__ __launch_bounds__(kThreads) void xor_encode_kernel(XorArgs a) {
         for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
             uint4 x[kInGroup];
 #pragma unroll
-            for (int jj = 0; jj < kInGroup; ++jj) x[jj] = ld16(src + (uint64_t)min(j0 + jj, k - 1) * a.ss);
+            for (int jj = 0; jj < kInGroup; ++jj) x[jj] = ld16<NT>(src + (uint64_t)min(j0 + jj, k - 1) * a.ss);
 #pragma unroll
             for (int jj = 0; jj < kInGroup; ++jj)
                 if (j0 + jj < k) {
@@ -327,10 +374,11 @@ __global__ __launch_bounds__(kThreads) void xor_encode_kernel(XorArgs a) {
                     acc.w ^= x[jj].w;
                 }
         }
-        store_chunk(a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk, acc, a.len - c * kChunk);
+        store_chunk<NT>(a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk, acc, a.len - c * kChunk, a.pad_zero);
     }
 }
 
+template <bool NT>
 __global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
     const uint32_t k = a.k, n = k + 1;
     const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
@@ -355,7 +403,7 @@ __global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
 #pragma unroll
             for (int jj = 0; jj < kInGroup; ++jj) {
                 const uint32_t j = min(j0 + jj, k - 1);
-                x[jj] = ld16(blk + (uint64_t)(j + (j >= mi)) * a.ss);
+                x[jj] = ld16<NT>(blk + (uint64_t)(j + (j >= mi)) * a.ss);
             }
 #pragma unroll
             for (int jj = 0; jj < kInGroup; ++jj)
@@ -366,19 +414,26 @@ __global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
                     acc.w ^= x[jj].w;
                 }
         }
-        store_chunk(blk + (uint64_t)mi * a.ss, acc, a.len - c * kChunk);
+        store_chunk<false>(blk + (uint64_t)mi * a.ss, acc, a.len - c * kChunk, a.pad_zero);
     }
 }
 
 // ------------------------------------------------------------------ launchers
+template <int MAXM, bool NT>
+static hipError_t enc_dispatch2(const EncodeArgs& a, int grid, hipStream_t s) {
+    const bool lds_tabs = a.m * a.k <= (uint32_t)kMaxLdsTabs;
+    if (lds_tabs) {
+        const size_t lds = (size_t)a.m * a.k * sizeof(gf::PermTab);
+        hipLaunchKernelGGL((rs_encode_kernel<MAXM, true, NT>), dim3(grid), dim3(kThreads), lds, s, a);
+    } else {
+        hipLaunchKernelGGL((rs_encode_kernel<MAXM, false, NT>), dim3(grid), dim3(kThreads), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
 template <int MAXM>
 static hipError_t enc_dispatch(const EncodeArgs& a, int grid, hipStream_t s) {
-    const size_t lds = (size_t)a.m * a.k * sizeof(gf::PermTab);
-    if (a.m * a.k <= (uint32_t)kMaxLdsTabs)
-        hipLaunchKernelGGL((rs_encode_kernel<MAXM, true>), dim3(grid), dim3(kThreads), lds, s, a);
-    else
-        hipLaunchKernelGGL((rs_encode_kernel<MAXM, false>), dim3(grid), dim3(kThreads), 0, s, a);
-    return hipGetLastError();
+    return g_tune.enc_nt ? enc_dispatch2<MAXM, true>(a, grid, s) : enc_dispatch2<MAXM, false>(a, grid, s);
 }
 
 hipError_t launch_rs_encode(const EncodeArgs& a, int grid, hipStream_t s) {
@@ -400,34 +455,41 @@ hipError_t launch_rs_plan(const PlanArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-static size_t recon_lds(const ReconArgs& a) {
-    return (size_t)a.g * a.maxe * a.k * sizeof(gf::PermTab) + (size_t)a.g * a.plan_stride;
+size_t recon_lds_bytes(uint32_t g, uint32_t k, uint32_t maxe, const PlanLayout& lay) {
+    return (size_t)g * maxe * k * sizeof(gf::PermTab) + (size_t)g * lay.stride;
 }
 
-hipError_t launch_rs_reconstruct(const ReconArgs& a, int grid, hipStream_t s) {
-    const size_t lds = recon_lds(a);
-    if (a.maxe <= 1) hipLaunchKernelGGL(rs_reconstruct_kernel<1>, dim3(grid), dim3(kThreads), lds, s, a);
-    else if (a.maxe <= 2) hipLaunchKernelGGL(rs_reconstruct_kernel<2>, dim3(grid), dim3(kThreads), lds, s, a);
-    else if (a.maxe <= 4) hipLaunchKernelGGL(rs_reconstruct_kernel<4>, dim3(grid), dim3(kThreads), lds, s, a);
-    else if (a.maxe <= 8) hipLaunchKernelGGL(rs_reconstruct_kernel<8>, dim3(grid), dim3(kThreads), lds, s, a);
-    else hipLaunchKernelGGL(rs_reconstruct_kernel<16>, dim3(grid), dim3(kThreads), lds, s, a);
+template <bool NT>
+static hipError_t recon_dispatch(const ReconArgs& a, int grid, hipStream_t s) {
+    const size_t lds = recon_lds_bytes(a.g, a.k, a.maxe, a.lay);
+    if (a.maxe <= 1) hipLaunchKernelGGL((rs_reconstruct_kernel<1, NT>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (a.maxe <= 2) hipLaunchKernelGGL((rs_reconstruct_kernel<2, NT>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (a.maxe <= 4) hipLaunchKernelGGL((rs_reconstruct_kernel<4, NT>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (a.maxe <= 8) hipLaunchKernelGGL((rs_reconstruct_kernel<8, NT>), dim3(grid), dim3(kThreads), lds, s, a);
+    else hipLaunchKernelGGL((rs_reconstruct_kernel<16, NT>), dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 
+hipError_t launch_rs_reconstruct(const ReconArgs& a, int grid, hipStream_t s) {
+    return g_tune.dec_nt ? recon_dispatch<true>(a, grid, s) : recon_dispatch<false>(a, grid, s);
+}
+
 hipError_t launch_xor_encode(const XorArgs& a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(xor_encode_kernel, dim3(grid), dim3(kThreads), 0, s, a);
+    if (g_tune.enc_nt) hipLaunchKernelGGL(xor_encode_kernel<true>, dim3(grid), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL(xor_encode_kernel<false>, dim3(grid), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_xor_reconstruct(const XorArgs& a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(xor_reconstruct_kernel, dim3(grid), dim3(kThreads), 0, s, a);
+    if (g_tune.dec_nt) hipLaunchKernelGGL(xor_reconstruct_kernel<true>, dim3(grid), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL(xor_reconstruct_kernel<false>, dim3(grid), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }
 
-uint32_t pick_tile_blocks(uint32_t cps, uint32_t k, uint32_t maxe) {
+uint32_t pick_tile_blocks(uint32_t cps, uint32_t k, uint32_t maxe, const PlanLayout& lay) {
     // Blocks per tile: the smallest count that reaches the best lane utilisation of the
-    // G*cps items over 256 lanes within 8 rounds, bounded by 48 KiB of LDS per tile.
-    const size_t per_block = (size_t)maxe * k * sizeof(gf::PermTab) + plan_stride_bytes(k, maxe);
+    // G*cps items over 256 lanes within dec_max_rounds rounds, bounded by 48 KiB of LDS.
+    const size_t per_block = recon_lds_bytes(1, k, maxe, lay);
     uint32_t gmax = (uint32_t)((48u * 1024u) / per_block);
     if (gmax < 1) gmax = 1;
     if (gmax > 256) gmax = 256;
@@ -436,7 +498,7 @@ uint32_t pick_tile_blocks(uint32_t cps, uint32_t k, uint32_t maxe) {
     for (uint32_t g = 1; g <= gmax; ++g) {
         const uint32_t items = g * cps;
         const uint32_t rounds = (items + kThreads - 1) / kThreads;
-        if (rounds > 8) break;
+        if (rounds > (uint32_t)g_tune.dec_max_rounds && g > 1) break;
         const double u = (double)items / (double)(rounds * kThreads);
         if (u > best_u + 1e-3) {
             best = g;
@@ -452,20 +514,20 @@ int occupancy_grid(int device, int which, uint32_t sel, size_t lds) {
         ncu = 256;
     int per = 0;
     const void* fn = nullptr;
-    if (which == 0) {   // encode
-        if (sel <= 1) fn = (const void*)rs_encode_kernel<1, true>;
-        else if (sel <= 2) fn = (const void*)rs_encode_kernel<2, true>;
-        else if (sel <= 4) fn = (const void*)rs_encode_kernel<4, true>;
-        else if (sel <= 8) fn = (const void*)rs_encode_kernel<8, true>;
-        else fn = (const void*)rs_encode_kernel<16, true>;
+    if (which == 0) {
+        if (sel <= 1) fn = (const void*)rs_encode_kernel<1, true, true>;
+        else if (sel <= 2) fn = (const void*)rs_encode_kernel<2, true, true>;
+        else if (sel <= 4) fn = (const void*)rs_encode_kernel<4, true, true>;
+        else if (sel <= 8) fn = (const void*)rs_encode_kernel<8, true, true>;
+        else fn = (const void*)rs_encode_kernel<16, true, true>;
     } else if (which == 1) {
-        if (sel <= 1) fn = (const void*)rs_reconstruct_kernel<1>;
-        else if (sel <= 2) fn = (const void*)rs_reconstruct_kernel<2>;
-        else if (sel <= 4) fn = (const void*)rs_reconstruct_kernel<4>;
-        else if (sel <= 8) fn = (const void*)rs_reconstruct_kernel<8>;
-        else fn = (const void*)rs_reconstruct_kernel<16>;
+        if (sel <= 1) fn = (const void*)rs_reconstruct_kernel<1, false>;
+        else if (sel <= 2) fn = (const void*)rs_reconstruct_kernel<2, false>;
+        else if (sel <= 4) fn = (const void*)rs_reconstruct_kernel<4, false>;
+        else if (sel <= 8) fn = (const void*)rs_reconstruct_kernel<8, false>;
+        else fn = (const void*)rs_reconstruct_kernel<16, false>;
     } else {
-        fn = (const void*)xor_encode_kernel;
+        fn = (const void*)xor_encode_kernel<true>;
     }
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kThreads, lds) != hipSuccess || per <= 0)
         per = 4;

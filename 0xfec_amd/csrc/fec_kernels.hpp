@@ -18,33 +18,49 @@ struct FastDiv {
 };
 FastDiv make_fastdiv(uint32_t d);
 
+// Flat launches (encode, XOR): item = one 16-byte column chunk of one block,
+// item -> (block = item / cps, chunk = item % cps).
 struct EncodeArgs {
     const uint8_t* in;   // data shard 0 of block 0
     uint8_t* out;        // parity shard 0 of block 0
     uint64_t in_bs, out_bs, ss;
     uint32_t k, m, len, cps;   // cps = chunks per shard = ceil(len / 16)
-    uint32_t total;            // nblocks * cps (< 2^32 per launch)
+    uint32_t total;            // nblocks * cps (< 2^31 per launch)
     FastDiv div_cps;
     const uint32_t* tabs;      // m * k PermTabs (8 dwords each), device memory
+    uint32_t pad_zero;         // tail chunk: full 16-B store, bytes past len zeroed
 };
+
+// Decode plan, one record of `stride` bytes per block (offsets from plan_layout()):
+//   [in_off,   +32)       input shard slots = the first k present shards, in index order
+//   [out_off,  +maxe)     erased data shard slots (ascending)
+//   [nout_off]            number of erased data shards to rebuild (0: nothing / failed)
+//   [coef_off, +maxe*k)   GF coefficients, row r = output r, column j = input j
+struct PlanLayout {
+    uint32_t in_off, out_off, nout_off, coef_off, stride;
+};
+PlanLayout plan_layout(uint32_t k, uint32_t maxe);
 
 struct PlanArgs {
     const uint32_t* masks;
-    uint8_t* plans;            // nblocks * plan_stride bytes
+    uint8_t* plans;            // nblocks * lay.stride bytes
     int32_t* status;           // optional
     int* err;                  // sticky error word
     const uint8_t* prows;      // m x k parity rows of the systematic matrix
-    uint32_t k, m, nblocks, plan_stride, maxe;
+    uint32_t k, m, nblocks, maxe;
+    PlanLayout lay;
 };
 
 struct ReconArgs {
     uint8_t* shards;
     uint64_t bs, ss;
     const uint8_t* plans;
-    uint32_t k, len, cps, nblocks, plan_stride, maxe;
+    uint32_t k, len, cps, nblocks, maxe;
+    PlanLayout lay;
     uint32_t g;                // blocks per tile
     uint32_t ntiles;
     FastDiv div_cps;
+    uint32_t pad_zero;
 };
 
 struct XorArgs {
@@ -56,14 +72,21 @@ struct XorArgs {
     int* err;
     uint32_t k, len, cps, total;
     FastDiv div_cps;
+    uint32_t pad_zero;
 };
 
-// Plan layout per block (plan_stride bytes, 16-aligned):
-//   [0] nout   [4, 4+maxe) out slots   [4+maxe, 4+maxe+k) input slots
-//   [4+maxe+k, +maxe*k) coefficients, row r = output r, column = input position
-inline uint32_t plan_stride_bytes(uint32_t k, uint32_t maxe) {
-    return (4 + maxe + k + maxe * k + 15) & ~15u;
-}
+// Kernel-selection knobs. Defaults are the measured best (tools/kbench.py A/Bs them through
+// the internal fec__set_tuning() entry point; results in DESIGN.md).
+struct Tuning {
+    int enc_nt = 1;           // non-temporal loads/stores in encode and XOR kernels
+    int dec_nt = 0;           // non-temporal shard loads in rs_reconstruct_kernel
+    int grid_mult = 1;        // persistent grids: workgroups = grid_mult * CUs * resident/CU
+    int dec_max_rounds = 8;   // bound on item rounds per decode tile (pick_tile_blocks)
+    int pad_zero = 1;         // tail chunks: zero-padded full 16-B stores instead of partial
+    int items_per_thread = 1; // >0: flat grids = total / (256 * items_per_thread); 0: persistent
+    int tiles_per_wg = 1;     // >0: decode grid = ntiles / tiles_per_wg; 0: persistent
+};
+extern Tuning g_tune;
 
 hipError_t launch_rs_encode(const EncodeArgs& a, int grid, hipStream_t s);
 hipError_t launch_rs_plan(const PlanArgs& a, hipStream_t s);
@@ -72,8 +95,9 @@ hipError_t launch_xor_encode(const XorArgs& a, int grid, hipStream_t s);
 hipError_t launch_xor_reconstruct(const XorArgs& a, int grid, hipStream_t s);
 
 // Blocks per decode tile for shard chunk count `cps`, bounded by LDS.
-uint32_t pick_tile_blocks(uint32_t cps, uint32_t k, uint32_t maxe);
-// Resident workgroups per CU for the encode/reconstruct kernels (occupancy API).
+uint32_t pick_tile_blocks(uint32_t cps, uint32_t k, uint32_t maxe, const PlanLayout& lay);
+size_t recon_lds_bytes(uint32_t g, uint32_t k, uint32_t maxe, const PlanLayout& lay);
+// Resident workgroups on the device for kernel `which` (0 encode, 1 reconstruct, 2 XOR).
 int occupancy_grid(int device, int which, uint32_t m_or_maxe, size_t lds_bytes);
 
 }  // namespace fk

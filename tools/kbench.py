@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Kernel-level A/B bench (diagnostics, not the contract bench): times each codec kernel on
+one resident RS(8,12)-shaped batch, interleaved over rounds in one process, beside a torch
+copy of the same byte count for the box's achievable HBM rate."""
+import argparse
+import ctypes
+import importlib
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--blocks", type=int, default=1 << 20)
+    ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--m", type=int, default=4)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--enc", default="1:0:1,0:0:1,1:16:0,1:0:2",
+                    help="encode nt:grid_mult:items_per_thread (grid_mult 0 -> 1 with ipt)")
+    ap.add_argument("--dec", default="0:8:0:1,1:8:0:1,0:4:0:1,0:16:0:1,0:8:16:0",
+                    help="decode nt:rounds:grid_mult:tiles_per_wg")
+    ap.add_argument("--xor", default="0:1,16:0", help="xor grid_mult:items_per_thread")
+    args = ap.parse_args()
+    import torch
+    fec = importlib.import_module("0xfec_amd")
+    fec.lib.fec__set_tuning.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    B, k, m = args.blocks, args.k, args.m
+    n, L, S = k + m, 1202, 1216
+    codec = fec.Codec(0).use_torch_stream()
+    sh = torch.randint(0, 256, (B, n, S), dtype=torch.uint8, device="cuda")
+    erased = torch.randint(0, k, (B,), device="cuda")
+    masks = ((1 << n) - 1 - (1 << erased)).to(torch.int32)
+    base, bs = sh.data_ptr(), n * S
+    cp_src = torch.empty(B * k * S, dtype=torch.uint8, device="cuda")
+    cp_dst = torch.empty(B * m * S, dtype=torch.uint8, device="cuda")
+    rd = torch.empty(B * (k + m) * S // 4, dtype=torch.int32, device="cuda")
+
+    def t(fn):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        fn()
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(args.iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / args.iters
+
+    def tune(**kv):
+        keys = {"enc_nt": 0, "dec_nt": 1, "grid_mult": 2, "dec_max_rounds": 3, "pad_zero": 4,
+                "items_per_thread": 5, "tiles_per_wg": 6}
+        for key, val in kv.items():
+            fec.lib.fec__set_tuning(codec.handle, keys[key], val)
+
+    def enc(v, g, ipt):
+        def f():
+            tune(enc_nt=v, grid_mult=max(g, 1), items_per_thread=ipt, pad_zero=1)
+            codec.rs_encode_raw(k, m, L, B, base, bs, base + k * S, bs, S, fec.FEC_DEVICE)
+        return f
+
+    def dec(nt, rounds, g, tpw):
+        def f():
+            tune(dec_nt=nt, dec_max_rounds=rounds, grid_mult=max(g, 1), tiles_per_wg=tpw, pad_zero=1)
+            codec.rs_reconstruct_raw(k, m, L, B, base, bs, S, masks.data_ptr(), None, fec.FEC_DEVICE)
+        return f
+
+    def xor(g, ipt):
+        def f():
+            tune(grid_mult=max(g, 1), items_per_thread=ipt, pad_zero=1)
+            fec.lib.fec_xor_encode_batch(codec.handle, k, L, B, base, bs, base + k * S, bs, S, fec.FEC_DEVICE)
+        return f
+
+    cases = {}
+    for spec in args.enc.split(","):
+        v, g, ipt = [int(x) for x in spec.split(":")]
+        cases["rs_encode nt%d g%d ipt%d" % (v, g, ipt)] = (enc(v, g, ipt), B * n * L)
+    for spec in args.dec.split(","):
+        nt, r, g, tpw = [int(x) for x in spec.split(":")]
+        cases["rs_reconstruct nt%d r%d g%d tpw%d" % (nt, r, g, tpw)] = (dec(nt, r, g, tpw), B * (k + 1) * L)
+    for spec in args.xor.split(","):
+        g, ipt = [int(x) for x in spec.split(":")]
+        cases["xor_encode_k%d g%d ipt%d" % (k, g, ipt)] = (xor(g, ipt), B * (k + 1) * L)
+    cases["torch_copy_%dto%d" % (k, m)] = (lambda: cp_dst.copy_(cp_src[:cp_dst.numel()]), 2 * cp_dst.numel())
+    cases["torch_sum_read"] = (lambda: rd.sum(), rd.numel() * 4)
+    res = {name: [] for name in cases}
+    for _ in range(args.rounds):
+        for name, (fn, nbytes) in cases.items():
+            ms = t(fn)
+            res[name].append(nbytes / (ms / 1e3) / 1e9)
+    out = {name: {"GB/s_median": round(sorted(v)[len(v) // 2], 1), "GB/s_max": round(max(v), 1)} for name, v in res.items()}
+    print(json.dumps({"blocks": B, "k": k, "m": m, "results": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
