@@ -64,9 +64,9 @@ lib.fec_sync.argtypes = [_vp]
 lib.fec_rs_matrix.argtypes = [_i, _i, _vp]
 lib.fec_rs_prepare.argtypes = [_vp, _i, _i]
 lib.fec_rs_encode_batch.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _i]
-lib.fec_rs_reconstruct_batch.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _sz, _vp, _vp, _i]
+lib.fec_rs_reconstruct_batch.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _vp, _vp, _i]
 lib.fec_xor_encode_batch.argtypes = [_vp, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _i]
-lib.fec_xor_reconstruct_batch.argtypes = [_vp, _i, _sz, _sz, _vp, _sz, _sz, _vp, _vp, _i]
+lib.fec_xor_reconstruct_batch.argtypes = [_vp, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _vp, _vp, _i]
 
 
 class FecError(RuntimeError):
@@ -176,10 +176,12 @@ class Codec:
         return _check(lib.fec_rs_encode_batch(self._h, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss, flags),
                       "fec_rs_encode_batch")
 
-    def rs_reconstruct_raw(self, k, m, shard_len, nblocks, shards, bs, ss, masks, status, flags):
-        return lib.fec_rs_reconstruct_batch(self._h, k, m, shard_len, nblocks, shards, bs, ss, masks, status, flags)
+    def rs_reconstruct_raw(self, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss, masks, status, flags):
+        return lib.fec_rs_reconstruct_batch(self._h, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss,
+                                            masks, status, flags)
 
-    # ---- array conveniences: shards is [B, n, S]; shard_len defaults to S
+    # ---- array conveniences. Interleaved form: shards is [B, k+m, S]. Split form: data
+    # [B, k, S] and parity [B, m, S] in separate buffers. shard_len defaults to S.
     def rs_encode(self, k, m, shards, shard_len=None):
         B, n, S = _shape3(shards)
         assert n == k + m
@@ -187,19 +189,45 @@ class Codec:
         L = S if shard_len is None else shard_len
         return self.rs_encode_raw(k, m, L, B, a, n * S, a + k * S, n * S, S, kind)
 
+    def rs_encode_split(self, k, m, data, parity, shard_len=None):
+        B, kk, S = _shape3(data)
+        B2, mm, S2 = _shape3(parity)
+        assert (kk, mm, B, S) == (k, m, B2, S2)
+        d, kind = _addr(data)
+        p, kind2 = _addr(parity)
+        assert kind == kind2
+        L = S if shard_len is None else shard_len
+        return self.rs_encode_raw(k, m, L, B, d, k * S, p, m * S, S, kind)
+
+    def _recon(self, fn, what, k, m, B, S, d, dbs, p, pbs, kind, masks, status, shard_len):
+        ma, mkind = _addr(masks)
+        assert mkind == kind, "masks must live where the shards live"
+        sa = _addr(status)[0] if status is not None else None
+        L = S if shard_len is None else shard_len
+        rc = fn(B, L, d, dbs, p, pbs, S, ma, sa, kind)
+        if rc not in (FEC_OK, FEC_ERR_TOO_FEW_SHARDS):
+            _check(rc, what)
+        return rc
+
     def rs_reconstruct(self, k, m, shards, masks, status=None, shard_len=None):
         """Returns the C return code (FEC_OK or FEC_ERR_TOO_FEW_SHARDS for FEC_HOST)."""
         B, n, S = _shape3(shards)
         assert n == k + m
         a, kind = _addr(shards)
-        ma, mkind = _addr(masks)
-        assert mkind == kind, "masks must live where the shards live"
-        sa = _addr(status)[0] if status is not None else None
-        L = S if shard_len is None else shard_len
-        rc = self.rs_reconstruct_raw(k, m, L, B, a, n * S, S, ma, sa, kind)
-        if rc not in (FEC_OK, FEC_ERR_TOO_FEW_SHARDS):
-            _check(rc, "fec_rs_reconstruct_batch")
-        return rc
+        fn = lambda B_, L, d, dbs, p, pbs, ss, ma, sa, kd: lib.fec_rs_reconstruct_batch(
+            self._h, k, m, L, B_, d, dbs, p, pbs, ss, ma, sa, kd)
+        return self._recon(fn, "fec_rs_reconstruct_batch", k, m, B, S, a, n * S, a + k * S, n * S, kind,
+                           masks, status, shard_len)
+
+    def rs_reconstruct_split(self, k, m, data, parity, masks, status=None, shard_len=None):
+        B, kk, S = _shape3(data)
+        assert kk == k and tuple(parity.shape) == (B, m, S)
+        d, kind = _addr(data)
+        p, _ = _addr(parity)
+        fn = lambda B_, L, d_, dbs, p_, pbs, ss, ma, sa, kd: lib.fec_rs_reconstruct_batch(
+            self._h, k, m, L, B_, d_, dbs, p_, pbs, ss, ma, sa, kd)
+        return self._recon(fn, "fec_rs_reconstruct_batch", k, m, B, S, d, k * S, p, m * S, kind,
+                           masks, status, shard_len)
 
     def xor_encode(self, k, shards, shard_len=None):
         B, n, S = _shape3(shards)
@@ -213,10 +241,7 @@ class Codec:
         B, n, S = _shape3(shards)
         assert n == k + 1
         a, kind = _addr(shards)
-        ma, _ = _addr(masks)
-        sa = _addr(status)[0] if status is not None else None
-        L = S if shard_len is None else shard_len
-        rc = lib.fec_xor_reconstruct_batch(self._h, k, L, B, a, n * S, S, ma, sa, kind)
-        if rc not in (FEC_OK, FEC_ERR_TOO_FEW_SHARDS):
-            _check(rc, "fec_xor_reconstruct_batch")
-        return rc
+        fn = lambda B_, L, d, dbs, p, pbs, ss, ma, sa, kd: lib.fec_xor_reconstruct_batch(
+            self._h, k, L, B_, d, dbs, p, pbs, ss, ma, sa, kd)
+        return self._recon(fn, "fec_xor_reconstruct_batch", k, 1, B, S, a, n * S, a + k * S, n * S, kind,
+                           masks, status, shard_len)

@@ -194,8 +194,9 @@ static int rs_encode_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks
     return FEC_OK;
 }
 
-static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks, uint8_t* shards,
-                                 size_t bs, size_t ss, const uint32_t* masks, int32_t* status, int* err) {
+static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks, uint8_t* data,
+                                 size_t dbs, const uint8_t* parity, size_t pbs, size_t ss, const uint32_t* masks,
+                                 int32_t* status, int* err) {
     const uint32_t k = (uint32_t)code->k, m = (uint32_t)code->m;
     const uint32_t maxe = std::max<uint32_t>(1, std::min(k, m));
     const uint32_t cps = (uint32_t)((len + fk::kChunk - 1) / fk::kChunk);
@@ -221,8 +222,10 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         p.lay = lay;
         HIP_TRY(fk::launch_rs_plan(p, ctx->stream));
         fk::ReconArgs a{};
-        a.shards = shards + b0 * bs;
-        a.bs = bs;
+        a.data = data + b0 * dbs;
+        a.parity = parity + b0 * pbs;
+        a.dbs = dbs;
+        a.pbs = pbs;
         a.ss = ss;
         a.plans = ctx->d_plans;
         a.k = k;
@@ -272,17 +275,20 @@ static int xor_encode_device(fec_ctx* ctx, int k, size_t len, size_t nblocks, co
     return FEC_OK;
 }
 
-static int xor_reconstruct_device(fec_ctx* ctx, int k, size_t len, size_t nblocks, uint8_t* shards, size_t bs,
-                                  size_t ss, const uint32_t* masks, int32_t* status, int* err) {
+static int xor_reconstruct_device(fec_ctx* ctx, int k, size_t len, size_t nblocks, uint8_t* data, size_t dbs,
+                                  const uint8_t* parity, size_t pbs, size_t ss, const uint32_t* masks,
+                                  int32_t* status, int* err) {
     const uint32_t cps = (uint32_t)((len + fk::kChunk - 1) / fk::kChunk);
     const size_t per_launch = std::max<size_t>(1, (size_t)(kMaxItems / cps));
     for (size_t b0 = 0; b0 < nblocks; b0 += per_launch) {
         const size_t nb = std::min(per_launch, nblocks - b0);
         fk::XorArgs a{};
-        a.in = shards + b0 * bs;
-        a.out = shards + b0 * bs;
-        a.in_bs = bs;
-        a.out_bs = bs;
+        a.in = data + b0 * dbs;
+        a.out = data + b0 * dbs;
+        a.parity = parity + b0 * pbs;
+        a.in_bs = dbs;
+        a.out_bs = dbs;
+        a.par_bs = pbs;
         a.ss = ss;
         a.masks = masks + b0;
         a.status = status ? status + b0 : nullptr;
@@ -314,6 +320,60 @@ static int check_device_layout(const void* p, size_t bs, size_t ss, size_t len) 
 static size_t host_chunk_blocks(size_t slots, size_t ssd) {
     const size_t per_block = slots * ssd;
     return std::max<size_t>(1, kStageBytes / per_block);
+}
+
+// FEC_HOST reconstruct (RS when code != nullptr, else XOR(k,1)): stage the present shards of
+// each chunk of blocks into pinned memory as [block][n][ssd], run the device path, copy the
+// rebuilt data shards back.
+static int host_reconstruct(fec_ctx* ctx, Code* code, int k, int m, size_t len, size_t nblocks, uint8_t* data,
+                            size_t dbs, const uint8_t* parity, size_t pbs, size_t ss, const uint32_t* masks,
+                            int32_t* block_status) {
+    const size_t ssd = round16(len);
+    const size_t n = (size_t)k + m;
+    const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
+    const uint32_t kmask = (1u << k) - 1u;
+    const size_t chunk = host_chunk_blocks(n, ssd);
+    int rc;
+    if ((rc = grow_stage(ctx, std::min(chunk, nblocks) * n * ssd))) return rc;
+    if ((rc = grow_masks(ctx, std::min(chunk, nblocks)))) return rc;
+    HIP_TRY(hipMemsetAsync(ctx->d_err + 1, 0, sizeof(int), ctx->stream));
+    std::vector<int32_t> st;
+    auto slot = [&](size_t b, size_t i) -> const uint8_t* {
+        return i < (size_t)k ? data + b * dbs + i * ss : parity + b * pbs + (i - k) * ss;
+    };
+    for (size_t b0 = 0; b0 < nblocks; b0 += chunk) {
+        const size_t nb = std::min(chunk, nblocks - b0);
+        for (size_t b = 0; b < nb; ++b) {
+            const uint32_t mask = masks[b0 + b] & all;
+            if ((mask & kmask) == kmask) continue;   // nothing to rebuild: skip the copy
+            for (size_t i = 0; i < n; ++i)
+                if ((mask >> i) & 1u) memcpy(ctx->h_stage + (b * n + i) * ssd, slot(b0 + b, i), len);
+        }
+        HIP_TRY(hipMemcpyAsync(ctx->d_masks, masks + b0, nb * 4, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, nb * n * ssd, hipMemcpyHostToDevice, ctx->stream));
+        if (code)
+            rc = rs_reconstruct_device(ctx, code, len, nb, ctx->d_stage, n * ssd, ctx->d_stage + k * ssd, n * ssd,
+                                       ssd, ctx->d_masks, ctx->d_status, ctx->d_err + 1);
+        else
+            rc = xor_reconstruct_device(ctx, k, len, nb, ctx->d_stage, n * ssd, ctx->d_stage + k * ssd, n * ssd,
+                                        ssd, ctx->d_masks, ctx->d_status, ctx->d_err + 1);
+        if (rc) return rc;
+        st.resize(nb);
+        HIP_TRY(hipMemcpyAsync(st.data(), ctx->d_status, nb * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(ctx->h_stage, ctx->d_stage, nb * n * ssd, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        for (size_t b = 0; b < nb; ++b) {
+            if (block_status) block_status[b0 + b] = st[b];
+            if (st[b] != 0) continue;
+            const uint32_t mask = masks[b0 + b] & all;
+            for (int i = 0; i < k; ++i)
+                if (!((mask >> i) & 1u))
+                    memcpy(data + (b0 + b) * dbs + i * ss, ctx->h_stage + (b * n + i) * ssd, len);
+        }
+    }
+    int err = 0;
+    HIP_TRY(hipMemcpy(&err, ctx->d_err + 1, sizeof(int), hipMemcpyDeviceToHost));
+    return err ? FEC_ERR_TOO_FEW_SHARDS : FEC_OK;
 }
 
 // ---------------------------------------------------------------- C ABI
@@ -501,9 +561,9 @@ int fec_rs_encode_batch(fec_ctx* ctx, int k, int m, size_t shard_len, size_t nbl
     return FEC_OK;
 }
 
-int fec_rs_reconstruct_batch(fec_ctx* ctx, int k, int m, size_t shard_len, size_t nblocks, uint8_t* shards,
-                             size_t block_stride, size_t shard_stride, const uint32_t* present_mask,
-                             int32_t* block_status, int flags) {
+int fec_rs_reconstruct_batch(fec_ctx* ctx, int k, int m, size_t shard_len, size_t nblocks, uint8_t* data,
+                             size_t data_block_stride, const uint8_t* parity, size_t parity_block_stride,
+                             size_t shard_stride, const uint32_t* present_mask, int32_t* block_status, int flags) {
     if (k <= 0 || m < 0) return FEC_ERR_INV_SHARD_NUM;
     if (k + m > FEC_MAX_DECODE_SHARDS) return FEC_ERR_MAX_SHARD_NUM;
     if (flags != FEC_DEVICE && flags != FEC_HOST) return FEC_ERR_INVALID_ARG;
@@ -514,53 +574,16 @@ int fec_rs_reconstruct_batch(fec_ctx* ctx, int k, int m, size_t shard_len, size_
     Code* code = nullptr;
     if ((rc = get_code(ctx, k, m, &code))) return rc;
     if (nblocks == 0) return FEC_OK;
-    if (!shards || !present_mask) return FEC_ERR_INVALID_ARG;
+    if (!data || !present_mask || (m > 0 && !parity)) return FEC_ERR_INVALID_ARG;
+    if (m == 0) parity = data;   // never read: no parity slot exists
     if (flags == FEC_DEVICE) {
-        if ((rc = check_device_layout(shards, block_stride, shard_stride, shard_len))) return rc;
-        return rs_reconstruct_device(ctx, code, shard_len, nblocks, shards, block_stride, shard_stride,
-                                     present_mask, block_status, ctx->d_err);
+        if ((rc = check_device_layout(data, data_block_stride, shard_stride, shard_len))) return rc;
+        if ((rc = check_device_layout(parity, parity_block_stride, shard_stride, shard_len))) return rc;
+        return rs_reconstruct_device(ctx, code, shard_len, nblocks, data, data_block_stride, parity,
+                                     parity_block_stride, shard_stride, present_mask, block_status, ctx->d_err);
     }
-    const size_t ssd = round16(shard_len);
-    const size_t n = (size_t)k + m;
-    const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
-    const uint32_t kmask = (1u << k) - 1u;
-    const size_t chunk = host_chunk_blocks(n, ssd);
-    if ((rc = grow_stage(ctx, std::min(chunk, nblocks) * n * ssd))) return rc;
-    if ((rc = grow_masks(ctx, std::min(chunk, nblocks)))) return rc;
-    HIP_TRY(hipMemsetAsync(ctx->d_err + 1, 0, sizeof(int), ctx->stream));
-    std::vector<int32_t> st;
-    for (size_t b0 = 0; b0 < nblocks; b0 += chunk) {
-        const size_t nb = std::min(chunk, nblocks - b0);
-        for (size_t b = 0; b < nb; ++b) {
-            const uint32_t mask = present_mask[b0 + b] & all;
-            if ((mask & kmask) == kmask) continue;   // nothing to rebuild: skip the copy
-            for (size_t i = 0; i < n; ++i)
-                if ((mask >> i) & 1u)
-                    memcpy(ctx->h_stage + (b * n + i) * ssd, shards + (b0 + b) * block_stride + i * shard_stride,
-                           shard_len);
-        }
-        HIP_TRY(hipMemcpyAsync(ctx->d_masks, present_mask + b0, nb * 4, hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, nb * n * ssd, hipMemcpyHostToDevice, ctx->stream));
-        if ((rc = rs_reconstruct_device(ctx, code, shard_len, nb, ctx->d_stage, n * ssd, ssd, ctx->d_masks,
-                                        ctx->d_status, ctx->d_err + 1)))
-            return rc;
-        st.resize(nb);
-        HIP_TRY(hipMemcpyAsync(st.data(), ctx->d_status, nb * 4, hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(hipMemcpyAsync(ctx->h_stage, ctx->d_stage, nb * n * ssd, hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
-        for (size_t b = 0; b < nb; ++b) {
-            if (block_status) block_status[b0 + b] = st[b];
-            if (st[b] != 0) continue;
-            const uint32_t mask = present_mask[b0 + b] & all;
-            for (int i = 0; i < k; ++i)
-                if (!((mask >> i) & 1u))
-                    memcpy(shards + (b0 + b) * block_stride + i * shard_stride, ctx->h_stage + (b * n + i) * ssd,
-                           shard_len);
-        }
-    }
-    int err = 0;
-    HIP_TRY(hipMemcpy(&err, ctx->d_err + 1, sizeof(int), hipMemcpyDeviceToHost));
-    return err ? FEC_ERR_TOO_FEW_SHARDS : FEC_OK;
+    return host_reconstruct(ctx, code, k, m, shard_len, nblocks, data, data_block_stride, parity,
+                            parity_block_stride, shard_stride, present_mask, block_status);
 }
 
 int fec_xor_encode_batch(fec_ctx* ctx, int k, size_t shard_len, size_t nblocks, const uint8_t* data,
@@ -603,9 +626,9 @@ int fec_xor_encode_batch(fec_ctx* ctx, int k, size_t shard_len, size_t nblocks, 
     return FEC_OK;
 }
 
-int fec_xor_reconstruct_batch(fec_ctx* ctx, int k, size_t shard_len, size_t nblocks, uint8_t* shards,
-                              size_t block_stride, size_t shard_stride, const uint32_t* present_mask,
-                              int32_t* block_status, int flags) {
+int fec_xor_reconstruct_batch(fec_ctx* ctx, int k, size_t shard_len, size_t nblocks, uint8_t* data,
+                              size_t data_block_stride, const uint8_t* parity, size_t parity_block_stride,
+                              size_t shard_stride, const uint32_t* present_mask, int32_t* block_status, int flags) {
     if (k <= 0) return FEC_ERR_INV_SHARD_NUM;
     if (k + 1 > FEC_MAX_DECODE_SHARDS) return FEC_ERR_MAX_SHARD_NUM;
     if (flags != FEC_DEVICE && flags != FEC_HOST) return FEC_ERR_INVALID_ARG;
@@ -614,53 +637,15 @@ int fec_xor_reconstruct_batch(fec_ctx* ctx, int k, size_t shard_len, size_t nblo
     int rc = select_device(ctx);
     if (rc) return rc;
     if (nblocks == 0) return FEC_OK;
-    if (!shards || !present_mask) return FEC_ERR_INVALID_ARG;
+    if (!data || !parity || !present_mask) return FEC_ERR_INVALID_ARG;
     if (flags == FEC_DEVICE) {
-        if ((rc = check_device_layout(shards, block_stride, shard_stride, shard_len))) return rc;
-        return xor_reconstruct_device(ctx, k, shard_len, nblocks, shards, block_stride, shard_stride, present_mask,
-                                      block_status, ctx->d_err);
+        if ((rc = check_device_layout(data, data_block_stride, shard_stride, shard_len))) return rc;
+        if ((rc = check_device_layout(parity, parity_block_stride, shard_stride, shard_len))) return rc;
+        return xor_reconstruct_device(ctx, k, shard_len, nblocks, data, data_block_stride, parity,
+                                      parity_block_stride, shard_stride, present_mask, block_status, ctx->d_err);
     }
-    const size_t ssd = round16(shard_len);
-    const size_t n = (size_t)k + 1;
-    const uint32_t all = (1u << n) - 1u;
-    const uint32_t kmask = (1u << k) - 1u;
-    const size_t chunk = host_chunk_blocks(n, ssd);
-    if ((rc = grow_stage(ctx, std::min(chunk, nblocks) * n * ssd))) return rc;
-    if ((rc = grow_masks(ctx, std::min(chunk, nblocks)))) return rc;
-    HIP_TRY(hipMemsetAsync(ctx->d_err + 1, 0, sizeof(int), ctx->stream));
-    std::vector<int32_t> st;
-    for (size_t b0 = 0; b0 < nblocks; b0 += chunk) {
-        const size_t nb = std::min(chunk, nblocks - b0);
-        for (size_t b = 0; b < nb; ++b) {
-            const uint32_t mask = present_mask[b0 + b] & all;
-            if ((mask & kmask) == kmask) continue;
-            for (size_t i = 0; i < n; ++i)
-                if ((mask >> i) & 1u)
-                    memcpy(ctx->h_stage + (b * n + i) * ssd, shards + (b0 + b) * block_stride + i * shard_stride,
-                           shard_len);
-        }
-        HIP_TRY(hipMemcpyAsync(ctx->d_masks, present_mask + b0, nb * 4, hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, nb * n * ssd, hipMemcpyHostToDevice, ctx->stream));
-        if ((rc = xor_reconstruct_device(ctx, k, shard_len, nb, ctx->d_stage, n * ssd, ssd, ctx->d_masks,
-                                         ctx->d_status, ctx->d_err + 1)))
-            return rc;
-        st.resize(nb);
-        HIP_TRY(hipMemcpyAsync(st.data(), ctx->d_status, nb * 4, hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(hipMemcpyAsync(ctx->h_stage, ctx->d_stage, nb * n * ssd, hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
-        for (size_t b = 0; b < nb; ++b) {
-            if (block_status) block_status[b0 + b] = st[b];
-            if (st[b] != 0) continue;
-            const uint32_t mask = present_mask[b0 + b] & all;
-            for (int i = 0; i < k; ++i)
-                if (!((mask >> i) & 1u))
-                    memcpy(shards + (b0 + b) * block_stride + i * shard_stride, ctx->h_stage + (b * n + i) * ssd,
-                           shard_len);
-        }
-    }
-    int err = 0;
-    HIP_TRY(hipMemcpy(&err, ctx->d_err + 1, sizeof(int), hipMemcpyDeviceToHost));
-    return err ? FEC_ERR_TOO_FEW_SHARDS : FEC_OK;
+    return host_reconstruct(ctx, nullptr, k, 1, shard_len, nblocks, data, data_block_stride, parity,
+                            parity_block_stride, shard_stride, present_mask, block_status);
 }
 
 }  // extern "C"

@@ -317,7 +317,8 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
                 if (__any((int)nout > r)) rows = r + 1;
             if (nout == 0) continue;
             const gf::PermTab* T = tabs + g * maxe * k;
-            uint8_t* blk = a.shards + (uint64_t)(b0 + g) * a.bs + (uint64_t)c * kChunk;
+            uint8_t* dblk = a.data + (uint64_t)(b0 + g) * a.dbs + (uint64_t)c * kChunk;
+            const uint8_t* pblk = a.parity + (uint64_t)(b0 + g) * a.pbs + (uint64_t)c * kChunk;
             uint4 acc[MAXE];
 #pragma unroll
             for (int r = 0; r < MAXE; ++r) acc[r] = make_uint4(0, 0, 0, 0);
@@ -330,7 +331,7 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
                     const uint32_t w = jj < 4 ? sl.x : sl.y;
                     uint32_t slot = (w >> (8 * (jj & 3))) & 0xFFu;
                     if (j0 + jj >= k) slot = (sl.x & 0xFFu);   // clamp to a valid shard
-                    x[jj] = ld16<NT>(blk + (uint64_t)slot * a.ss);
+                    x[jj] = ld16<NT>(slot < k ? dblk + (uint64_t)slot * a.ss : pblk + (uint64_t)(slot - k) * a.ss);
                 }
 #pragma unroll
                 for (int jj = 0; jj < kInGroup; ++jj) {
@@ -346,7 +347,7 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
             const uint8_t* out_idx = P + lay.out_off;
 #pragma unroll
             for (int r = 0; r < MAXE; ++r)
-                if (r < (int)nout) store_chunk<false>(blk + (uint64_t)out_idx[r] * a.ss, acc[r], nb, a.pad_zero);
+                if (r < (int)nout) store_chunk<NT>(dblk + (uint64_t)out_idx[r] * a.ss, acc[r], nb, a.pad_zero);
         }
     }
 }
@@ -397,13 +398,15 @@ __global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
         }
         if (!work) continue;
         uint8_t* blk = a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk;
+        const uint8_t* par = a.parity + (uint64_t)b * a.par_bs + (uint64_t)c * kChunk;
         uint4 acc = make_uint4(0, 0, 0, 0);
         for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
             uint4 x[kInGroup];
 #pragma unroll
             for (int jj = 0; jj < kInGroup; ++jj) {
                 const uint32_t j = min(j0 + jj, k - 1);
-                x[jj] = ld16<NT>(blk + (uint64_t)(j + (j >= mi)) * a.ss);
+                const uint32_t s = j + (j >= mi);     // the k shards other than the missing one
+                x[jj] = ld16<NT>(s < k ? blk + (uint64_t)s * a.ss : par);
             }
 #pragma unroll
             for (int jj = 0; jj < kInGroup; ++jj)
@@ -414,7 +417,7 @@ __global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
                     acc.w ^= x[jj].w;
                 }
         }
-        store_chunk<false>(blk + (uint64_t)mi * a.ss, acc, a.len - c * kChunk, a.pad_zero);
+        store_chunk<NT>(blk + (uint64_t)mi * a.ss, acc, a.len - c * kChunk, a.pad_zero);
     }
 }
 

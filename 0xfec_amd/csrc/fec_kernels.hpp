@@ -52,8 +52,9 @@ struct PlanArgs {
 };
 
 struct ReconArgs {
-    uint8_t* shards;
-    uint64_t bs, ss;
+    uint8_t* data;             // data shard 0 of block 0 (rebuilt shards are written here)
+    const uint8_t* parity;     // parity shard 0 of block 0
+    uint64_t dbs, pbs, ss;
     const uint8_t* plans;
     uint32_t k, len, cps, nblocks, maxe;
     PlanLayout lay;
@@ -64,9 +65,11 @@ struct ReconArgs {
 };
 
 struct XorArgs {
-    const uint8_t* in;
-    uint8_t* out;
+    const uint8_t* in;         // data shard 0 of block 0
+    uint8_t* out;              // encode: parity shard 0; reconstruct: == in (rebuilt in place)
+    const uint8_t* parity;     // reconstruct: parity shard of block 0
     uint64_t in_bs, out_bs, ss;
+    uint64_t par_bs;           // reconstruct: parity block stride
     const uint32_t* masks;     // reconstruct only
     int32_t* status;           // reconstruct only, optional
     int* err;
@@ -79,7 +82,7 @@ struct XorArgs {
 // the internal fec__set_tuning() entry point; results in DESIGN.md).
 struct Tuning {
     int enc_nt = 1;           // non-temporal loads/stores in encode and XOR kernels
-    int dec_nt = 0;           // non-temporal shard loads in rs_reconstruct_kernel
+    int dec_nt = 1;           // non-temporal loads and stores in the reconstruct kernels
     int grid_mult = 1;        // persistent grids: workgroups = grid_mult * CUs * resident/CU
     int dec_max_rounds = 8;   // bound on item rounds per decode tile (pick_tile_blocks)
     int pad_zero = 1;         // tail chunks: zero-padded full 16-B stores instead of partial

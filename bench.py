@@ -48,21 +48,23 @@ def parse():
 
 
 def make_batch(torch, B, k, m, seed, device):
-    """[B, n, 1216] shards: data slots random payloads + trailer 0x04 0xB0, parity slots 0."""
+    """Data shards [B, k, 1216] (random 1200-byte payloads + trailer 0x04 0xB0, zero pad) and
+    parity shards [B, m, 1216] in a separate buffer; one random erased data shard per block."""
     n = k + m
     g = torch.Generator(device=device)
     g.manual_seed(seed)
-    sh = torch.zeros((B, n, SHARD_STRIDE), dtype=torch.uint8, device=device)
-    for b0 in range(0, B, 1 << 16):      # chunked to bound the int64 temporaries
+    data = torch.zeros((B, k, SHARD_STRIDE), dtype=torch.uint8, device=device)
+    for b0 in range(0, B, 1 << 16):      # chunked to bound the temporaries
         b1 = min(B, b0 + (1 << 16))
-        sh[b0:b1, :k, :PAYLOAD] = torch.randint(0, 256, (b1 - b0, k, PAYLOAD), generator=g,
-                                                device=device, dtype=torch.int16).to(torch.uint8)
-    sh[:, :k, PAYLOAD] = PAYLOAD >> 8
-    sh[:, :k, PAYLOAD + 1] = PAYLOAD & 0xFF
+        data[b0:b1, :, :PAYLOAD] = torch.randint(0, 256, (b1 - b0, k, PAYLOAD), generator=g,
+                                                 device=device, dtype=torch.int16).to(torch.uint8)
+    data[:, :, PAYLOAD] = PAYLOAD >> 8
+    data[:, :, PAYLOAD + 1] = PAYLOAD & 0xFF
+    parity = torch.zeros((B, m, SHARD_STRIDE), dtype=torch.uint8, device=device)
     erased = torch.randint(0, k, (B,), generator=g, device=device, dtype=torch.int64)
     full = (1 << n) - 1
     masks = (full - torch.bitwise_left_shift(torch.ones_like(erased), erased)).to(torch.int32)
-    return sh, erased, masks
+    return data, parity, erased, masks
 
 
 def host_threads():
@@ -128,18 +130,17 @@ def main():
     codec.use_torch_stream()
     stream = torch.cuda.current_stream(dev)
 
-    sh, erased, masks = make_batch(torch, B, k, m, args.seed + 7919 * rank, dev)
+    data, parity, erased, masks = make_batch(torch, B, k, m, args.seed + 7919 * rank, dev)
     torch.cuda.synchronize()
-    base = sh.data_ptr()
-    bs = n * SHARD_STRIDE
+    dptr, pptr = data.data_ptr(), parity.data_ptr()
+    dbs, pbs = k * SHARD_STRIDE, m * SHARD_STRIDE
 
     def encode():
-        codec.rs_encode_raw(k, m, SHARD_LEN, B, base, bs, base + k * SHARD_STRIDE, bs, SHARD_STRIDE,
-                            fec.FEC_DEVICE)
+        codec.rs_encode_raw(k, m, SHARD_LEN, B, dptr, dbs, pptr, pbs, SHARD_STRIDE, fec.FEC_DEVICE)
 
     def decode():
-        rc = codec.rs_reconstruct_raw(k, m, SHARD_LEN, B, base, bs, SHARD_STRIDE, masks.data_ptr(), None,
-                                      fec.FEC_DEVICE)
+        rc = codec.rs_reconstruct_raw(k, m, SHARD_LEN, B, dptr, dbs, pptr, pbs, SHARD_STRIDE, masks.data_ptr(),
+                                      None, fec.FEC_DEVICE)
         if rc != 0:
             raise fec.FecError(rc, "decode")
 
@@ -150,12 +151,12 @@ def main():
 
     # correctness at full size (outside the timed region): wipe every erased shard, decode,
     # and compare the data shards with a copy taken before the wipe
-    ref = sh[:, :k, :SHARD_LEN].clone()
+    ref = data[:, :, :SHARD_LEN].clone()
     rows = torch.arange(B, device=dev)
-    sh[rows, erased, :] = 0
+    data[rows, erased, :] = 0
     decode()
     codec.sync()
-    ok_roundtrip = bool(torch.equal(sh[:, :k, :SHARD_LEN], ref))
+    ok_roundtrip = bool(torch.equal(data[:, :, :SHARD_LEN], ref))
     del ref
     torch.cuda.empty_cache()
 
@@ -194,7 +195,7 @@ def main():
             import numpy as np
             from oracle import oracle as orc
             pick = torch.randperm(B, device=dev)[:64]
-            sample = sh[pick].cpu().numpy()
+            sample = torch.cat([data[pick], parity[pick]], dim=1).cpu().numpy()
             want = sample[:, :, :SHARD_LEN].copy()
             orc.rs_encode(k, m, want)
             ok_parity = bool(np.array_equal(sample[:, :, :SHARD_LEN], want))
@@ -227,7 +228,8 @@ def main():
             "data": "synthetic (torch Philox bytes, seed 0x0FEC + 7919*rank)",
             "config": {"workload": "RS(k=%d,n=%d) encode + random single-data-erasure decode" % (k, n),
                        "blocks_per_gpu": B, "payload_bytes": PAYLOAD, "shard_len": L,
-                       "shard_stride": SHARD_STRIDE, "parallelism": "independent block ranges per GPU"},
+                       "shard_stride": SHARD_STRIDE, "layout": "data [B][k][1216] + parity [B][m][1216] buffers",
+                       "parallelism": "independent block ranges per GPU"},
             "roofline": {"bound": "hbm", "achieved": round(dom_bw / 1e9, 1), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(dom_bw / HBM_PEAK, 4), "traffic": None,
                          "kernel": dominant, "algorithmic_bytes_per_launch": dom_bytes},

@@ -17,8 +17,11 @@
  *   fec_xor_encode_batch        xorScheme.xor loop          internal/fec/xor.go:28-33,44-56
  *   fec_xor_reconstruct_batch   xorScheme recover loops     internal/fec/xor.go:80-86
  *
- * Shard layout (all entry points). A batch is `nblocks` independent blocks. Shard i of
- * block b lives at  base + b*block_stride + i*shard_stride  and is `shard_len` bytes long
+ * Shard layout (all entry points). A batch is `nblocks` independent blocks of k data and m
+ * parity shards. Data shard j of block b lives at  data + b*data_block_stride + j*shard_stride,
+ * parity shard i at  parity + b*parity_block_stride + i*shard_stride; each is `shard_len`
+ * bytes long. One interleaved [block][k+m][shard_stride] array is the special case
+ * parity = data + k*shard_stride, parity_block_stride = data_block_stride. Shards are
  * (the reference's shard = payload | zero pad | big-endian uint16 length, i.e.
  * biggest+2 bytes: reed_solomon.go:70-89, xor.go:44-56). Bytes [0, shard_len) of every
  * output shard receive the result; with FEC_DEVICE, bytes [shard_len, round_up(shard_len,
@@ -101,14 +104,17 @@ int fec_rs_encode_batch(fec_ctx *ctx, int k, int m, size_t shard_len, size_t nbl
                         size_t shard_stride, int flags);
 
 /* RS ReconstructData, in place. present_mask[b] bit i set <=> shard i of block b present
- * (n = k + m <= 32). For each block, every missing DATA shard is rebuilt from the first k
- * present shards in index order; missing parity shards are not touched; a block with no
- * missing data shard is untouched. block_status (optional, same memory kind as the
- * masks) receives 0 or FEC_ERR_TOO_FEW_SHARDS per block. FEC_HOST: returns
- * FEC_ERR_TOO_FEW_SHARDS if any block failed (other blocks are still rebuilt). */
+ * (shards 0..k-1 data, k..k+m-1 parity; n = k + m <= 32). For each block, every missing DATA
+ * shard is rebuilt, into its own slot, from the first k present shards in index order;
+ * missing parity shards are not touched; a block with no missing data shard is untouched.
+ * block_status (optional, same memory kind as the masks) receives 0 or
+ * FEC_ERR_TOO_FEW_SHARDS per block. FEC_HOST: returns FEC_ERR_TOO_FEW_SHARDS if any block
+ * failed (the other blocks are still rebuilt). */
 int fec_rs_reconstruct_batch(fec_ctx *ctx, int k, int m, size_t shard_len, size_t nblocks,
-                             uint8_t *shards, size_t block_stride, size_t shard_stride,
-                             const uint32_t *present_mask, int32_t *block_status, int flags);
+                             uint8_t *data, size_t data_block_stride,
+                             const uint8_t *parity, size_t parity_block_stride,
+                             size_t shard_stride, const uint32_t *present_mask,
+                             int32_t *block_status, int flags);
 
 /* XOR(k, 1) encode: parity = XOR of the k data shards. */
 int fec_xor_encode_batch(fec_ctx *ctx, int k, size_t shard_len, size_t nblocks,
@@ -116,12 +122,14 @@ int fec_xor_encode_batch(fec_ctx *ctx, int k, size_t shard_len, size_t nblocks,
                          uint8_t *parity, size_t parity_block_stride,
                          size_t shard_stride, int flags);
 
-/* XOR(k, 1) recovery, in place over k + 1 shards per block: a single missing data shard is
- * the XOR of the other k. Two or more missing shards with a data shard among them ->
+/* XOR(k, 1) recovery, in place (shard k is the parity): a single missing data shard is the
+ * XOR of the other k shards. Two or more missing shards with a data shard among them ->
  * FEC_ERR_TOO_FEW_SHARDS for that block. */
 int fec_xor_reconstruct_batch(fec_ctx *ctx, int k, size_t shard_len, size_t nblocks,
-                              uint8_t *shards, size_t block_stride, size_t shard_stride,
-                              const uint32_t *present_mask, int32_t *block_status, int flags);
+                              uint8_t *data, size_t data_block_stride,
+                              const uint8_t *parity, size_t parity_block_stride,
+                              size_t shard_stride, const uint32_t *present_mask,
+                              int32_t *block_status, int flags);
 
 #ifdef __cplusplus
 }

@@ -211,8 +211,34 @@ def test_argument_errors(codec, torch, fec):
     with pytest.raises(fec.FecError) as e:
         codec.rs_encode_raw(2, 1, 0, 1, d.data_ptr(), 48, d.data_ptr() + 32, 48, 16, fec.FEC_DEVICE)
     assert e.value.code == fec.FEC_ERR_SHARD_NO_DATA
-    assert codec.rs_reconstruct_raw(20, 13, 16, 1, d.data_ptr(), 48, 16, d.data_ptr(), None,
+    assert codec.rs_reconstruct_raw(20, 13, 16, 1, d.data_ptr(), 48, d.data_ptr(), 48, 16, d.data_ptr(), None,
                                     fec.FEC_DEVICE) == fec.FEC_ERR_MAX_SHARD_NUM
     # empty batches are no-ops
     codec.rs_encode_raw(2, 1, 16, 0, d.data_ptr(), 48, d.data_ptr() + 32, 48, 16, fec.FEC_DEVICE)
     codec.sync()
+
+
+@pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10)])
+def test_rs_split_layout_matches_interleaved(codec, oracle, torch, k, m):
+    """Data and parity in separate buffers (the bench layout) give the same bytes."""
+    rng = np.random.default_rng(99 + k)
+    n, L, S, B = k + m, 1202, 1216, 203
+    sh = _rand_shards(rng, B, n, S, L)
+    oracle.rs_encode(k, m, sh)
+    data = torch.from_numpy(np.ascontiguousarray(sh[:, :k])).cuda()
+    par = torch.zeros((B, m, S), dtype=torch.uint8, device="cuda")
+    codec.rs_encode_split(k, m, data, par, shard_len=L)
+    codec.sync()
+    assert np.array_equal(par.cpu().numpy()[:, :, :L], sh[:, k:, :L])
+    masks = _random_masks(rng, B, k, m)
+    want = sh.copy()
+    for b in range(B):
+        for i in range(k):
+            if not (masks[b] >> i) & 1:
+                data[b, i] = 0x77
+    st = torch.zeros(B, dtype=torch.int32, device="cuda")
+    codec.rs_reconstruct_split(k, m, data, par, torch.from_numpy(masks.view(np.int32)).cuda(), status=st,
+                               shard_len=L)
+    codec.sync()
+    assert (st.cpu().numpy() == 0).all()
+    assert np.array_equal(data.cpu().numpy()[:, :, :L], want[:, :k, :L])

@@ -19,11 +19,11 @@ def main():
     ap.add_argument("--m", type=int, default=4)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--enc", default="1:0:1,0:0:1,1:16:0,1:0:2",
+    ap.add_argument("--enc", default="1:0:1",
                     help="encode nt:grid_mult:items_per_thread (grid_mult 0 -> 1 with ipt)")
-    ap.add_argument("--dec", default="0:8:0:1,1:8:0:1,0:4:0:1,0:16:0:1,0:8:16:0",
+    ap.add_argument("--dec", default="0:8:0:1,1:8:0:1",
                     help="decode nt:rounds:grid_mult:tiles_per_wg")
-    ap.add_argument("--xor", default="0:1,16:0", help="xor grid_mult:items_per_thread")
+    ap.add_argument("--xor", default="0:1", help="xor grid_mult:items_per_thread")
     args = ap.parse_args()
     import torch
     fec = importlib.import_module("0xfec_amd")
@@ -65,7 +65,8 @@ def main():
     def dec(nt, rounds, g, tpw):
         def f():
             tune(dec_nt=nt, dec_max_rounds=rounds, grid_mult=max(g, 1), tiles_per_wg=tpw, pad_zero=1)
-            codec.rs_reconstruct_raw(k, m, L, B, base, bs, S, masks.data_ptr(), None, fec.FEC_DEVICE)
+            codec.rs_reconstruct_raw(k, m, L, B, base, bs, base + k * S, bs, S, masks.data_ptr(), None,
+                                     fec.FEC_DEVICE)
         return f
 
     def xor(g, ipt):
@@ -74,7 +75,24 @@ def main():
             fec.lib.fec_xor_encode_batch(codec.handle, k, L, B, base, bs, base + k * S, bs, S, fec.FEC_DEVICE)
         return f
 
+    dsplit = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device="cuda")
+    psplit = torch.randint(0, 256, (B, m, S), dtype=torch.uint8, device="cuda")
+
+    def enc_split():
+        tune(enc_nt=1, grid_mult=1, items_per_thread=1, pad_zero=1)
+        codec.rs_encode_raw(k, m, L, B, dsplit.data_ptr(), k * S, psplit.data_ptr(), m * S, S, fec.FEC_DEVICE)
+
+    def dec_split(nt):
+        def f():
+            tune(dec_nt=nt, dec_max_rounds=8, grid_mult=1, tiles_per_wg=1, pad_zero=1)
+            codec.rs_reconstruct_raw(k, m, L, B, dsplit.data_ptr(), k * S, psplit.data_ptr(), m * S, S,
+                                     masks.data_ptr(), None, fec.FEC_DEVICE)
+        return f
+
     cases = {}
+    cases["rs_encode split"] = (enc_split, B * n * L)
+    cases["rs_reconstruct split nt1"] = (dec_split(1), B * (k + 1) * L)
+    cases["rs_reconstruct split nt0"] = (dec_split(0), B * (k + 1) * L)
     for spec in args.enc.split(","):
         v, g, ipt = [int(x) for x in spec.split(":")]
         cases["rs_encode nt%d g%d ipt%d" % (v, g, ipt)] = (enc(v, g, ipt), B * n * L)
