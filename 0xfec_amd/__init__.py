@@ -65,6 +65,7 @@ lib.fec_rs_matrix.argtypes = [_i, _i, _vp]
 lib.fec_rs_prepare.argtypes = [_vp, _i, _i]
 lib.fec_rs_encode_batch.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _i]
 lib.fec_rs_reconstruct_batch.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _vp, _vp, _i]
+lib.fec_rs_recover_batch.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _vp, _vp, _sz, _i, _vp, _i]
 lib.fec_xor_encode_batch.argtypes = [_vp, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _i]
 lib.fec_xor_reconstruct_batch.argtypes = [_vp, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _vp, _vp, _i]
 
@@ -228,6 +229,23 @@ class Codec:
             self._h, k, m, L, B_, d_, dbs, p_, pbs, ss, ma, sa, kd)
         return self._recon(fn, "fec_rs_reconstruct_batch", k, m, B, S, d, k * S, p, m * S, kind,
                            masks, status, shard_len)
+
+    def rs_recover_raw(self, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss, masks, out, out_bs, out_slots,
+                       status, flags=FEC_DEVICE):
+        return lib.fec_rs_recover_batch(self._h, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss, masks,
+                                        out, out_bs, out_slots, status, flags)
+
+    def rs_recover_split(self, k, m, data, parity, masks, out, status=None, shard_len=None):
+        """Rebuild the erased data shards of each block into out [B, slots, S] (ascending order);
+        status[b] = number rebuilt, or a negative error code."""
+        B, kk, S = _shape3(data)
+        B2, slots, S2 = _shape3(out)
+        assert kk == k and tuple(parity.shape) == (B, m, S) and (B2, S2) == (B, S)
+        L = S if shard_len is None else shard_len
+        sa = _addr(status)[0] if status is not None else None
+        rc = self.rs_recover_raw(k, m, L, B, _addr(data)[0], k * S, _addr(parity)[0], m * S, S, _addr(masks)[0],
+                                 _addr(out)[0], slots * S, slots, sa)
+        return _check(rc, "fec_rs_recover_batch")
 
     def xor_encode(self, k, shards, shard_len=None):
         B, n, S = _shape3(shards)

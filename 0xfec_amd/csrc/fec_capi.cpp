@@ -196,7 +196,8 @@ static int rs_encode_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks
 
 static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks, uint8_t* data,
                                  size_t dbs, const uint8_t* parity, size_t pbs, size_t ss, const uint32_t* masks,
-                                 int32_t* status, int* err) {
+                                 int32_t* status, int* err, uint8_t* out = nullptr, size_t out_bs = 0,
+                                 uint32_t out_slots = 0) {
     const uint32_t k = (uint32_t)code->k, m = (uint32_t)code->m;
     const uint32_t maxe = std::max<uint32_t>(1, std::min(k, m));
     const uint32_t cps = (uint32_t)((len + fk::kChunk - 1) / fk::kChunk);
@@ -220,6 +221,7 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         p.nblocks = (uint32_t)nb;
         p.maxe = maxe;
         p.lay = lay;
+        p.max_out = out ? out_slots : 0;
         HIP_TRY(fk::launch_rs_plan(p, ctx->stream));
         fk::ReconArgs a{};
         a.data = data + b0 * dbs;
@@ -238,6 +240,8 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         a.ntiles = (uint32_t)((nb + G - 1) / G);
         a.div_cps = fk::make_fastdiv(cps);
         a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
+        a.out = out ? out + b0 * out_bs : nullptr;
+        a.out_bs = out_bs;
         int grid;
         if (fk::g_tune.tiles_per_wg > 0)
             grid = (int)((a.ntiles + fk::g_tune.tiles_per_wg - 1) / fk::g_tune.tiles_per_wg);
@@ -494,7 +498,7 @@ int fec_sync(fec_ctx* ctx) {
     HIP_TRY(hipMemcpy(&err, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (err) {
         HIP_TRY(hipMemset(ctx->d_err, 0, sizeof(int)));
-        return FEC_ERR_TOO_FEW_SHARDS;
+        return (err & 1) ? FEC_ERR_TOO_FEW_SHARDS : FEC_ERR_INVALID_ARG;
     }
     return FEC_OK;
 }
@@ -584,6 +588,30 @@ int fec_rs_reconstruct_batch(fec_ctx* ctx, int k, int m, size_t shard_len, size_
     }
     return host_reconstruct(ctx, code, k, m, shard_len, nblocks, data, data_block_stride, parity,
                             parity_block_stride, shard_stride, present_mask, block_status);
+}
+
+int fec_rs_recover_batch(fec_ctx* ctx, int k, int m, size_t shard_len, size_t nblocks, const uint8_t* data,
+                         size_t data_block_stride, const uint8_t* parity, size_t parity_block_stride,
+                         size_t shard_stride, const uint32_t* present_mask, uint8_t* out, size_t out_block_stride,
+                         int out_slots, int32_t* block_status, int flags) {
+    if (k <= 0 || m < 0) return FEC_ERR_INV_SHARD_NUM;
+    if (k + m > FEC_MAX_DECODE_SHARDS) return FEC_ERR_MAX_SHARD_NUM;
+    if (flags != FEC_DEVICE) return FEC_ERR_INVALID_ARG;
+    if (shard_len == 0) return FEC_ERR_SHARD_NO_DATA;
+    if (shard_len > (size_t(1) << 30) || out_slots <= 0) return FEC_ERR_INVALID_ARG;
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    Code* code = nullptr;
+    if ((rc = get_code(ctx, k, m, &code))) return rc;
+    if (nblocks == 0) return FEC_OK;
+    if (!data || !present_mask || !out || (m > 0 && !parity)) return FEC_ERR_INVALID_ARG;
+    if (m == 0) parity = data;
+    if ((rc = check_device_layout(data, data_block_stride, shard_stride, shard_len))) return rc;
+    if ((rc = check_device_layout(parity, parity_block_stride, shard_stride, shard_len))) return rc;
+    if ((rc = check_device_layout(out, out_block_stride, shard_stride, shard_len))) return rc;
+    return rs_reconstruct_device(ctx, code, shard_len, nblocks, const_cast<uint8_t*>(data), data_block_stride,
+                                 parity, parity_block_stride, shard_stride, present_mask, block_status, ctx->d_err,
+                                 out, out_block_stride, (uint32_t)out_slots);
 }
 
 int fec_xor_encode_batch(fec_ctx* ctx, int k, size_t shard_len, size_t nblocks, const uint8_t* data,

@@ -185,87 +185,118 @@ __global__ __launch_bounds__(kThreads) void rs_encode_kernel(EncodeArgs a) {
 }
 
 // ------------------------------------------------------------------ RS reconstruct plan
-// One thread per block. From the present mask: E = erased data shards (e of them),
-// R = first e present parity shards; the first k present shards are then exactly
-// {present data} + R. Solve A[R][E] (e x e) and express each erased shard over those k
-// inputs. Writes the plan record (PlanLayout).
+// One thread per block, one wave per workgroup. From the present mask: E = erased data
+// shards (e of them), R = first e present parity shards; the first k present shards are
+// then exactly {present data} + R. Solve A[R][E] (e x e) and express each erased shard over
+// those k inputs. Each lane assembles its record in LDS (byte writes), then the wave copies
+// its 64 consecutive records to HBM with 16-byte stores.
+constexpr int kPlanThreads = 64;
+
 template <int MAXE>
-__global__ __launch_bounds__(kThreads) void rs_plan_kernel(PlanArgs a) {
-    __shared__ uint8_t s_exp[512];
-    __shared__ uint8_t s_log[256];
-    for (int i = threadIdx.x; i < 512; i += kThreads) s_exp[i] = gf::kTables.exp[i];
-    for (int i = threadIdx.x; i < 256; i += kThreads) s_log[i] = gf::kTables.log[i];
+__global__ __launch_bounds__(kPlanThreads) void rs_plan_kernel(PlanArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t* s_exp = smem;                 // 512
+    uint8_t* s_log = smem + 512;           // 256
+    uint8_t* recs = smem + 768;            // kPlanThreads * stride
+    for (int i = threadIdx.x; i < 512; i += kPlanThreads) s_exp[i] = gf::kTables.exp[i];
+    for (int i = threadIdx.x; i < 256; i += kPlanThreads) s_log[i] = gf::kTables.log[i];
     __syncthreads();
-    const uint32_t b = blockIdx.x * kThreads + threadIdx.x;
-    if (b >= a.nblocks) return;
     auto mul = [&](uint32_t x, uint32_t y) -> uint32_t {
         return (x && y) ? s_exp[s_log[x] + s_log[y]] : 0u;
     };
+    const PlanLayout lay = a.lay;
+    const uint32_t b0 = blockIdx.x * kPlanThreads;
+    const uint32_t b = b0 + threadIdx.x;
+    uint8_t* P = recs + threadIdx.x * lay.stride;
     const uint32_t k = a.k, m = a.m, n = k + m;
-    const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
-    const uint32_t mask = a.masks[b] & all;
-    const uint32_t kmask = (1u << k) - 1u;   // k <= 31
-    uint8_t* P = a.plans + (uint64_t)b * a.lay.stride;
-    const uint32_t e = k - __popc(mask & kmask);
-    int32_t st = 0;
-    if (e == 0) {
-        P[a.lay.nout_off] = 0;
-    } else if ((uint32_t)__popc(mask) < k) {
-        P[a.lay.nout_off] = 0;
-        st = -4;  // FEC_ERR_TOO_FEW_SHARDS
-        atomicOr(a.err, 1);
-    } else {
-        uint8_t E[MAXE], R[MAXE];
-        uint32_t ne = 0, nr = 0;
-        for (uint32_t i = 0; i < k; ++i)
-            if (!((mask >> i) & 1u)) E[ne++] = (uint8_t)i;
-        for (uint32_t p = 0; p < m && nr < e; ++p)
-            if ((mask >> (k + p)) & 1u) R[nr++] = (uint8_t)p;
-        // Gauss-Jordan on [A | I], A[t][i] = prows[R[t]][E[i]]
-        uint8_t A[MAXE][2 * MAXE];
-        for (uint32_t t = 0; t < e; ++t)
-            for (uint32_t i = 0; i < 2 * e; ++i)
-                A[t][i] = i < e ? a.prows[R[t] * k + E[i]] : (uint8_t)(i - e == t);
-        for (uint32_t col = 0; col < e; ++col) {
-            uint32_t piv = col;
-            while (piv < e && A[piv][col] == 0) ++piv;
-            if (piv != col)
-                for (uint32_t i = 0; i < 2 * e; ++i) {
-                    const uint8_t tmp = A[piv][i];
-                    A[piv][i] = A[col][i];
-                    A[col][i] = tmp;
+    if (b < a.nblocks) {
+        const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
+        const uint32_t mask = a.masks[b] & all;
+        const uint32_t kmask = (1u << k) - 1u;   // k <= 31
+        const uint32_t e = k - __popc(mask & kmask);
+        int32_t st = a.max_out ? (int32_t)e : 0;   // recover reports the rebuilt count
+        if (e == 0) {
+            P[lay.nout_off] = 0;
+        } else if ((uint32_t)__popc(mask) < k) {
+            P[lay.nout_off] = 0;
+            st = -4;  // FEC_ERR_TOO_FEW_SHARDS
+            atomicOr(a.err, 1);
+        } else if (a.max_out && e > a.max_out) {
+            P[lay.nout_off] = 0;
+            st = -1;  // FEC_ERR_INVALID_ARG: more erasures than output slots
+            atomicOr(a.err, 2);
+        } else if (e == 1) {
+            // one erasure: x_E = inv(A[R0][E0]) * (p_R0 ^ sum_j A[R0][j] x_j)
+            const uint32_t E0 = __ffs(~mask & kmask) - 1;
+            const uint32_t R0 = __ffs(mask >> k) - 1;
+            const uint8_t* row = a.prows + R0 * k;
+            const uint32_t inv = s_exp[255 - s_log[row[E0]]];
+            for (uint32_t j = 0, pos = 0; j < k; ++j) {
+                if (j == E0) continue;
+                P[lay.in_off + pos] = (uint8_t)j;
+                P[lay.coef_off + pos] = (uint8_t)mul(inv, row[j]);
+                ++pos;
+            }
+            P[lay.in_off + k - 1] = (uint8_t)(k + R0);
+            P[lay.coef_off + k - 1] = (uint8_t)inv;
+            P[lay.out_off] = (uint8_t)E0;
+            P[lay.nout_off] = 1;
+        } else {
+            uint8_t E[MAXE], R[MAXE];
+            uint32_t ne = 0, nr = 0;
+            for (uint32_t i = 0; i < k; ++i)
+                if (!((mask >> i) & 1u)) E[ne++] = (uint8_t)i;
+            for (uint32_t p = 0; p < m && nr < e; ++p)
+                if ((mask >> (k + p)) & 1u) R[nr++] = (uint8_t)p;
+            // Gauss-Jordan on [A | I], A[t][i] = prows[R[t]][E[i]]
+            uint8_t A[MAXE][2 * MAXE];
+            for (uint32_t t = 0; t < e; ++t)
+                for (uint32_t i = 0; i < 2 * e; ++i)
+                    A[t][i] = i < e ? a.prows[R[t] * k + E[i]] : (uint8_t)(i - e == t);
+            for (uint32_t col = 0; col < e; ++col) {
+                uint32_t piv = col;
+                while (piv < e && A[piv][col] == 0) ++piv;
+                if (piv != col)
+                    for (uint32_t i = 0; i < 2 * e; ++i) {
+                        const uint8_t tmp = A[piv][i];
+                        A[piv][i] = A[col][i];
+                        A[col][i] = tmp;
+                    }
+                const uint32_t inv = s_exp[255 - s_log[A[col][col]]];
+                for (uint32_t i = 0; i < 2 * e; ++i) A[col][i] = (uint8_t)mul(inv, A[col][i]);
+                for (uint32_t r = 0; r < e; ++r) {
+                    if (r == col) continue;
+                    const uint32_t f = A[r][col];
+                    if (!f) continue;
+                    for (uint32_t i = 0; i < 2 * e; ++i) A[r][i] ^= (uint8_t)mul(f, A[col][i]);
                 }
-            const uint32_t inv = s_exp[255 - s_log[A[col][col]]];
-            for (uint32_t i = 0; i < 2 * e; ++i) A[col][i] = (uint8_t)mul(inv, A[col][i]);
-            for (uint32_t r = 0; r < e; ++r) {
-                if (r == col) continue;
-                const uint32_t f = A[r][col];
-                if (!f) continue;
-                for (uint32_t i = 0; i < 2 * e; ++i) A[r][i] ^= (uint8_t)mul(f, A[col][i]);
             }
-        }
-        uint8_t* in_idx = P + a.lay.in_off;
-        uint8_t* out_idx = P + a.lay.out_off;
-        uint8_t* coef = P + a.lay.coef_off;
-        uint32_t pos = 0;
-        for (uint32_t j = 0; j < k; ++j) {
-            if (!((mask >> j) & 1u)) continue;
-            in_idx[pos] = (uint8_t)j;
-            for (uint32_t i = 0; i < e; ++i) {
-                uint32_t c = 0;
-                for (uint32_t t = 0; t < e; ++t) c ^= mul(A[i][e + t], a.prows[R[t] * k + j]);
-                coef[i * k + pos] = (uint8_t)c;
+            uint32_t pos = 0;
+            for (uint32_t j = 0; j < k; ++j) {
+                if (!((mask >> j) & 1u)) continue;
+                P[lay.in_off + pos] = (uint8_t)j;
+                for (uint32_t i = 0; i < e; ++i) {
+                    uint32_t c = 0;
+                    for (uint32_t t = 0; t < e; ++t) c ^= mul(A[i][e + t], a.prows[R[t] * k + j]);
+                    P[lay.coef_off + i * k + pos] = (uint8_t)c;
+                }
+                ++pos;
             }
-            ++pos;
+            for (uint32_t t = 0; t < e; ++t, ++pos) {
+                P[lay.in_off + pos] = (uint8_t)(k + R[t]);
+                for (uint32_t i = 0; i < e; ++i) P[lay.coef_off + i * k + pos] = A[i][e + t];
+            }
+            for (uint32_t i = 0; i < e; ++i) P[lay.out_off + i] = E[i];
+            P[lay.nout_off] = (uint8_t)e;
         }
-        for (uint32_t t = 0; t < e; ++t, ++pos) {
-            in_idx[pos] = (uint8_t)(k + R[t]);
-            for (uint32_t i = 0; i < e; ++i) coef[i * k + pos] = A[i][e + t];
-        }
-        for (uint32_t i = 0; i < e; ++i) out_idx[i] = E[i];
-        P[a.lay.nout_off] = (uint8_t)e;
+        if (a.status) a.status[b] = st;
     }
-    if (a.status) a.status[b] = st;
+    __syncthreads();
+    const uint32_t nrec = min((uint32_t)kPlanThreads, a.nblocks - b0);
+    const uint32_t nw = nrec * lay.stride / 16;
+    const uint4* src = reinterpret_cast<const uint4*>(recs);
+    uint4* dst = reinterpret_cast<uint4*>(a.plans + (uint64_t)b0 * lay.stride);
+    for (uint32_t i = threadIdx.x; i < nw; i += kPlanThreads) dst[i] = src[i];
 }
 
 // ------------------------------------------------------------------ RS reconstruct
@@ -345,9 +376,12 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
             }
             const uint32_t nb = a.len - c * kChunk;
             const uint8_t* out_idx = P + lay.out_off;
+            uint8_t* oblk = a.out ? a.out + (uint64_t)(b0 + g) * a.out_bs + (uint64_t)c * kChunk : nullptr;
 #pragma unroll
             for (int r = 0; r < MAXE; ++r)
-                if (r < (int)nout) store_chunk<NT>(dblk + (uint64_t)out_idx[r] * a.ss, acc[r], nb, a.pad_zero);
+                if (r < (int)nout)
+                    store_chunk<NT>(oblk ? oblk + (uint64_t)r * a.ss : dblk + (uint64_t)out_idx[r] * a.ss, acc[r],
+                                    nb, a.pad_zero);
         }
     }
 }
@@ -448,13 +482,15 @@ hipError_t launch_rs_encode(const EncodeArgs& a, int grid, hipStream_t s) {
 }
 
 hipError_t launch_rs_plan(const PlanArgs& a, hipStream_t s) {
-    const int grid = (int)((a.nblocks + kThreads - 1) / kThreads);
+    const int grid = (int)((a.nblocks + kPlanThreads - 1) / kPlanThreads);
     if (grid == 0) return hipSuccess;
-    if (a.maxe <= 1) hipLaunchKernelGGL(rs_plan_kernel<1>, dim3(grid), dim3(kThreads), 0, s, a);
-    else if (a.maxe <= 2) hipLaunchKernelGGL(rs_plan_kernel<2>, dim3(grid), dim3(kThreads), 0, s, a);
-    else if (a.maxe <= 4) hipLaunchKernelGGL(rs_plan_kernel<4>, dim3(grid), dim3(kThreads), 0, s, a);
-    else if (a.maxe <= 8) hipLaunchKernelGGL(rs_plan_kernel<8>, dim3(grid), dim3(kThreads), 0, s, a);
-    else hipLaunchKernelGGL(rs_plan_kernel<16>, dim3(grid), dim3(kThreads), 0, s, a);
+    const size_t lds = 768 + (size_t)kPlanThreads * a.lay.stride;
+    const dim3 g(grid), t(kPlanThreads);
+    if (a.maxe <= 1) hipLaunchKernelGGL(rs_plan_kernel<1>, g, t, lds, s, a);
+    else if (a.maxe <= 2) hipLaunchKernelGGL(rs_plan_kernel<2>, g, t, lds, s, a);
+    else if (a.maxe <= 4) hipLaunchKernelGGL(rs_plan_kernel<4>, g, t, lds, s, a);
+    else if (a.maxe <= 8) hipLaunchKernelGGL(rs_plan_kernel<8>, g, t, lds, s, a);
+    else hipLaunchKernelGGL(rs_plan_kernel<16>, g, t, lds, s, a);
     return hipGetLastError();
 }
 

@@ -49,6 +49,7 @@ struct PlanArgs {
     const uint8_t* prows;      // m x k parity rows of the systematic matrix
     uint32_t k, m, nblocks, maxe;
     PlanLayout lay;
+    uint32_t max_out;          // recover: output slots per block (0: in place, unlimited)
 };
 
 struct ReconArgs {
@@ -62,6 +63,8 @@ struct ReconArgs {
     uint32_t ntiles;
     FastDiv div_cps;
     uint32_t pad_zero;
+    uint8_t* out;              // recover: rebuilt shard r of block b at out + b*out_bs + r*ss
+    uint64_t out_bs;           //          (nullptr: rebuild in place into the data region)
 };
 
 struct XorArgs {

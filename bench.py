@@ -7,8 +7,11 @@ Workload (configs[2]): RS(k=8, n=12), 2^20 blocks per GPU, 1200-byte payloads fr
 random single data-shard erasure per block.
 
 One step = one pass of the hot path over the resident batch:
-    encode      fec_rs_encode_batch   (klauspost Encode,          reed_solomon.go:51)
-    decode      fec_rs_reconstruct_batch (klauspost ReconstructData, reed_solomon.go:124)
+    encode  fec_rs_encode_batch   (klauspost Encode, reed_solomon.go:51): data -> parity
+    decode  fec_rs_recover_batch  (ReconstructData + copy-out of recoverSymbolPayloads,
+            reed_solomon.go:92-136): the erased data shard of every block rebuilt from the
+            first k present shards into a recovered-shard buffer
+The in-place form (fec_rs_reconstruct_batch) is timed separately and reported beside it.
 Inputs are resident in HBM before timing starts. value = payload GiB/s over all ranks
 = N * B * k * 1200 / 2^30 / step time (max over ranks). Multi-GPU: every rank owns its own
 2^20 contiguous blocks (weak scaling), no collective on the data path.
@@ -64,7 +67,8 @@ def make_batch(torch, B, k, m, seed, device):
     erased = torch.randint(0, k, (B,), generator=g, device=device, dtype=torch.int64)
     full = (1 << n) - 1
     masks = (full - torch.bitwise_left_shift(torch.ones_like(erased), erased)).to(torch.int32)
-    return data, parity, erased, masks
+    recovered = torch.zeros((B, 1, SHARD_STRIDE), dtype=torch.uint8, device=device)
+    return data, parity, erased, masks, recovered
 
 
 def host_threads():
@@ -130,33 +134,40 @@ def main():
     codec.use_torch_stream()
     stream = torch.cuda.current_stream(dev)
 
-    data, parity, erased, masks = make_batch(torch, B, k, m, args.seed + 7919 * rank, dev)
+    data, parity, erased, masks, recovered = make_batch(torch, B, k, m, args.seed + 7919 * rank, dev)
     torch.cuda.synchronize()
-    dptr, pptr = data.data_ptr(), parity.data_ptr()
+    dptr, pptr, optr = data.data_ptr(), parity.data_ptr(), recovered.data_ptr()
     dbs, pbs = k * SHARD_STRIDE, m * SHARD_STRIDE
 
     def encode():
         codec.rs_encode_raw(k, m, SHARD_LEN, B, dptr, dbs, pptr, pbs, SHARD_STRIDE, fec.FEC_DEVICE)
 
     def decode():
+        rc = codec.rs_recover_raw(k, m, SHARD_LEN, B, dptr, dbs, pptr, pbs, SHARD_STRIDE, masks.data_ptr(),
+                                  optr, SHARD_STRIDE, 1, None)
+        if rc != 0:
+            raise fec.FecError(rc, "decode")
+
+    def decode_inplace():
         rc = codec.rs_reconstruct_raw(k, m, SHARD_LEN, B, dptr, dbs, pptr, pbs, SHARD_STRIDE, masks.data_ptr(),
                                       None, fec.FEC_DEVICE)
         if rc != 0:
-            raise fec.FecError(rc, "decode")
+            raise fec.FecError(rc, "decode_inplace")
 
     for _ in range(args.warmup):
         encode()
         decode()
     codec.sync()
 
-    # correctness at full size (outside the timed region): wipe every erased shard, decode,
-    # and compare the data shards with a copy taken before the wipe
-    ref = data[:, :, :SHARD_LEN].clone()
+    # correctness at full size (outside the timed region): the recovered shard of every block
+    # equals the erased original; then wipe every erased shard, rebuild in place, compare
     rows = torch.arange(B, device=dev)
+    ok_recover = bool(torch.equal(recovered[:, 0, :SHARD_LEN], data[rows, erased, :SHARD_LEN]))
+    ref = data[:, :, :SHARD_LEN].clone()
     data[rows, erased, :] = 0
-    decode()
+    decode_inplace()
     codec.sync()
-    ok_roundtrip = bool(torch.equal(data[:, :, :SHARD_LEN], ref))
+    ok_roundtrip = bool(torch.equal(data[:, :, :SHARD_LEN], ref)) and ok_recover
     del ref
     torch.cuda.empty_cache()
 
@@ -180,10 +191,19 @@ def main():
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
     step_ms = wall * 1000.0 / args.steps
+    # in-place reconstruct, timed on its own (not part of the step)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = max(3, args.steps // 2)
+    e0.record(stream)
+    for _ in range(reps):
+        decode_inplace()
+    e1.record(stream)
+    codec.sync()
+    inplace_ms = e0.elapsed_time(e1) / reps
     if world > 1:
-        t = torch.tensor([step_ms, enc_ms, dec_ms], device=dev, dtype=torch.float64)
+        t = torch.tensor([step_ms, enc_ms, dec_ms, inplace_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        step_ms, enc_ms, dec_ms = t.tolist()
+        step_ms, enc_ms, dec_ms, inplace_ms = t.tolist()
         okt = torch.tensor([1 if ok_roundtrip else 0], device=dev)
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok_roundtrip = bool(okt.item())
@@ -209,7 +229,7 @@ def main():
     value = payload_gib / (step_ms / 1000.0)
     enc_bw = enc_bytes / (enc_ms / 1000.0)
     dec_bw = dec_bytes / (dec_ms / 1000.0)
-    dominant = "rs_encode_kernel" if enc_ms >= dec_ms else "rs_reconstruct(plan+kernel)"
+    dominant = "rs_encode_kernel" if enc_ms >= dec_ms else "rs_plan_kernel+rs_reconstruct_kernel (recover)"
     dom_bw, dom_bytes = (enc_bw, enc_bytes) if enc_ms >= dec_ms else (dec_bw, dec_bytes)
 
     if rank == 0:
@@ -237,7 +257,10 @@ def main():
                 "encode": {"ms": round(enc_ms, 4), "GB/s": round(enc_bw / 1e9, 1), "bytes": enc_bytes,
                            "frac": round(enc_bw / HBM_PEAK, 4)},
                 "decode": {"ms": round(dec_ms, 4), "GB/s": round(dec_bw / 1e9, 1), "bytes": dec_bytes,
-                           "frac": round(dec_bw / HBM_PEAK, 4)},
+                           "frac": round(dec_bw / HBM_PEAK, 4), "api": "fec_rs_recover_batch (plan + kernel)"},
+                "decode_inplace": {"ms": round(inplace_ms, 4),
+                                   "GB/s": round(dec_bytes / (inplace_ms / 1e3) / 1e9, 1),
+                                   "api": "fec_rs_reconstruct_batch (plan + kernel), not in the step"},
                 "step_frac": round((enc_bytes + dec_bytes) / ((enc_ms + dec_ms) / 1000.0) / HBM_PEAK, 4),
             },
             "check": {"roundtrip_full_batch": ok_roundtrip, "encode_vs_oracle_64_blocks": ok_parity},

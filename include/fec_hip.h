@@ -14,6 +14,8 @@
  *                                                           internal/fec/manager.go:60,83
  *   fec_rs_encode_batch         Encoder.Encode(shards)      internal/fec/reed_solomon.go:51
  *   fec_rs_reconstruct_batch    Encoder.ReconstructData     internal/fec/reed_solomon.go:124
+ *   fec_rs_recover_batch        ReconstructData + the copy-out of recoverSymbolPayloads
+ *                                                           internal/fec/reed_solomon.go:124-133
  *   fec_xor_encode_batch        xorScheme.xor loop          internal/fec/xor.go:28-33,44-56
  *   fec_xor_reconstruct_batch   xorScheme recover loops     internal/fec/xor.go:80-86
  *
@@ -86,7 +88,9 @@ int fec_ctx_set_stream(fec_ctx *ctx, void *hip_stream);
 int fec_ctx_reset_stream(fec_ctx *ctx);
 void *fec_ctx_stream(fec_ctx *ctx);
 /* Wait for the ctx stream. Returns FEC_ERR_TOO_FEW_SHARDS if any FEC_DEVICE reconstruct
- * since the last fec_sync met a block with fewer than k present shards (then clears it). */
+ * since the last fec_sync met a block with fewer than k present shards, or
+ * FEC_ERR_INVALID_ARG if a recover met a block with more erasures than output slots
+ * (then clears it). */
 int fec_sync(fec_ctx *ctx);
 
 /* The n x k systematic matrix of RS(k, m) (n = k + m), row-major, host memory. No device
@@ -115,6 +119,21 @@ int fec_rs_reconstruct_batch(fec_ctx *ctx, int k, int m, size_t shard_len, size_
                              const uint8_t *parity, size_t parity_block_stride,
                              size_t shard_stride, const uint32_t *present_mask,
                              int32_t *block_status, int flags);
+
+/* Out-of-place RS recovery: the device form of reedSolomonScheme.recoverSymbolPayloads
+ * (internal/fec/reed_solomon.go:92-136), whose result is the erased source payloads in
+ * ascending shard order. For block b the e erased data shards are rebuilt (same arithmetic
+ * as fec_rs_reconstruct_batch) into  out + b*out_block_stride + r*shard_stride, r = 0..e-1,
+ * in ascending shard order; data and parity are only read. out_slots = shard slots per block
+ * in `out`. block_status (optional) receives e (>= 0) or FEC_ERR_TOO_FEW_SHARDS, or
+ * FEC_ERR_INVALID_ARG when e > out_slots (that block is not written). FEC_DEVICE only;
+ * fec_sync() reports any failed block. */
+int fec_rs_recover_batch(fec_ctx *ctx, int k, int m, size_t shard_len, size_t nblocks,
+                         const uint8_t *data, size_t data_block_stride,
+                         const uint8_t *parity, size_t parity_block_stride,
+                         size_t shard_stride, const uint32_t *present_mask,
+                         uint8_t *out, size_t out_block_stride, int out_slots,
+                         int32_t *block_status, int flags);
 
 /* XOR(k, 1) encode: parity = XOR of the k data shards. */
 int fec_xor_encode_batch(fec_ctx *ctx, int k, size_t shard_len, size_t nblocks,

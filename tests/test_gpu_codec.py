@@ -242,3 +242,45 @@ def test_rs_split_layout_matches_interleaved(codec, oracle, torch, k, m):
     codec.sync()
     assert (st.cpu().numpy() == 0).all()
     assert np.array_equal(data.cpu().numpy()[:, :, :L], want[:, :k, :L])
+
+
+@pytest.mark.parametrize("k,m,slots", [(8, 4, 1), (8, 4, 4), (16, 8, 8), (20, 10, 3)])
+def test_rs_recover_out_of_place(codec, oracle, torch, fec, k, m, slots):
+    """fec_rs_recover_batch writes the erased data shards, ascending, to a separate buffer
+    (the shape of recoverSymbolPayloads' result) and leaves the inputs untouched."""
+    rng = np.random.default_rng(7 * k + slots)
+    n, L, S, B = k + m, 1202, 1216, 257
+    sh = _rand_shards(rng, B, n, S, L)
+    oracle.rs_encode(k, m, sh)
+    masks = _random_masks(rng, B, k, m)
+    data_np = np.ascontiguousarray(sh[:, :k]).copy()
+    for b in range(B):
+        for i in range(k):
+            if not (masks[b] >> i) & 1:
+                data_np[b, i] = 0x11
+    data = torch.from_numpy(data_np).cuda()
+    par = torch.from_numpy(np.ascontiguousarray(sh[:, k:])).cuda()
+    out = torch.full((B, slots, S), 0xEE, dtype=torch.uint8, device="cuda")
+    st = torch.full((B,), 99, dtype=torch.int32, device="cuda")
+    codec.rs_recover_split(k, m, data, par, torch.from_numpy(masks.view(np.int32)).cuda(), out, status=st,
+                           shard_len=L)
+    over = False
+    try:
+        codec.sync()
+    except fec.FecError as e:
+        assert e.code == fec.FEC_ERR_INVALID_ARG
+        over = True
+    st = st.cpu().numpy()
+    got = out.cpu().numpy()
+    assert np.array_equal(data.cpu().numpy(), data_np)          # inputs untouched
+    saw_over = False
+    for b in range(B):
+        miss = [i for i in range(k) if not (masks[b] >> i) & 1]
+        if len(miss) > slots:
+            assert st[b] == fec.FEC_ERR_INVALID_ARG
+            saw_over = True
+            continue
+        assert st[b] == len(miss)
+        for r, i in enumerate(miss):
+            assert np.array_equal(got[b, r, :L], sh[b, i, :L])
+    assert saw_over == over

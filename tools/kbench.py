@@ -89,7 +89,15 @@ def main():
                                      masks.data_ptr(), None, fec.FEC_DEVICE)
         return f
 
+    outb = torch.empty((B, 1, S), dtype=torch.uint8, device="cuda")
+
+    def rec_split():
+        tune(dec_nt=1, dec_max_rounds=8, grid_mult=1, tiles_per_wg=1, pad_zero=1)
+        codec.rs_recover_raw(k, m, L, B, dsplit.data_ptr(), k * S, psplit.data_ptr(), m * S, S,
+                             masks.data_ptr(), outb.data_ptr(), S, 1, None)
+
     cases = {}
+    cases["rs_recover split nt1"] = (rec_split, B * (k + 1) * L)
     cases["rs_encode split"] = (enc_split, B * n * L)
     cases["rs_reconstruct split nt1"] = (dec_split(1), B * (k + 1) * L)
     cases["rs_reconstruct split nt0"] = (dec_split(0), B * (k + 1) * L)
