@@ -1,0 +1,691 @@
+// fec_scheme.cpp — C++ mirror of internal/fec (block.go, reed_solomon.go, xor.go,
+// manager.go) over the HIP codec, plus the C ABI of include/fec_scheme.h.
+//
+// Every function cites the reference lines it restates. Where the Go code would panic
+// (index or slice out of range on malformed input), this mirror returns an error instead;
+// those cases are listed in DESIGN.md ("Divergences").
+#include "../../include/fec_scheme.hpp"
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "../../include/fec_hip.h"
+#include "../../include/fec_scheme.h"
+
+namespace fec {
+
+static std::string fmt(const char* f, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, f);
+    vsnprintf(buf, sizeof(buf), f, ap);
+    va_end(ap);
+    return buf;
+}
+
+static Error codec_error(int rc) {
+    Error e;
+    e.code = rc;
+    e.msg = fec_strerror(rc);
+    return e;
+}
+
+// ------------------------------------------------------------------ Slice
+
+Slice Slice::make(size_t len, size_t cap) {
+    Slice s;
+    s.buf = std::make_shared<std::vector<uint8_t>>(std::max(len, cap), 0);
+    s.len = len;
+    s.cap = std::max(len, cap);
+    return s;
+}
+
+Slice Slice::from(const uint8_t* p, size_t len, size_t cap) {
+    Slice s = make(len, cap);
+    if (len) memcpy(s.data(), p, len);
+    return s;
+}
+
+Slice Slice::reslice(size_t lo, size_t hi) const {
+    Slice s = *this;
+    s.off = off + lo;
+    s.len = hi - lo;
+    s.cap = cap - lo;
+    return s;
+}
+
+// ------------------------------------------------------------------ Block (block.go)
+
+Block Block::New(BlockID id, int totNumSourceSymbols, int totNumRepairSymbols) {   // block.go:36-49
+    Block b;
+    b.id = id;
+    b.smallestSSID = (SourceSymbolID)id * (SourceSymbolID)totNumSourceSymbols;
+    b.largestSSID = b.smallestSSID + (SourceSymbolID)totNumSourceSymbols - 1;
+    b.totNumSourceSymbols = (int)((int64_t)b.largestSSID - (int64_t)b.smallestSSID + 1);
+    b.totNumRepairSymbols = totNumRepairSymbols;
+    b.biggestSourceSymbolLenSoFar = 0;
+    return b;
+}
+
+Error Block::addSourceSymbol(const SourceSymbolFrame& f) {   // block.go:56-70
+    if (f.ssid < smallestSSID || f.ssid > largestSSID)
+        return Error::text(fmt("source symbol was provided to the wrong block. Expecting SID within the range "
+                               "[%llu, %llu] and got %llu",
+                               (unsigned long long)smallestSSID, (unsigned long long)largestSSID,
+                               (unsigned long long)f.ssid));
+    if (!ssidToSourcePayload.count(f.ssid)) {
+        ssidToSourcePayload[f.ssid] = f.payload;
+        if (biggestSourceSymbolLenSoFar < (int)f.payload.len) biggestSourceSymbolLenSoFar = (int)f.payload.len;
+    }
+    return Error::nil();
+}
+
+Error Block::addRepairSymbol(const RepairFrame& f) {   // block.go:73-85
+    if (id != f.block_id)
+        return Error::text(fmt("the repair symbol was provided to the wrong block. Expecting %llu and got %llu",
+                               (unsigned long long)id, (unsigned long long)f.block_id));
+    if (!pidToRepairPayload.count(f.parity_id)) {
+        pidToRepairPayload[f.parity_id] = f.payload;
+        biggestSourceSymbolLenSoFar = (int)f.payload.len - (int)kRepairPayloadMetadataLen;
+    }
+    return Error::nil();
+}
+
+bool Block::isRecoverable() const {   // block.go:88-90
+    return (int)(ssidToSourcePayload.size() + pidToRepairPayload.size()) >= totNumSourceSymbols;
+}
+
+bool Block::isComplete() const {   // block.go:93-95
+    return (int)ssidToSourcePayload.size() == totNumSourceSymbols;
+}
+
+// ------------------------------------------------------------------ Engine
+
+Engine::~Engine() {
+    if (ctx_) fec_ctx_destroy(ctx_);
+}
+
+Error Engine::ctx(fec_ctx** out) {
+    if (!ctx_) {
+        const int rc = fec_ctx_create(device_, &ctx_);
+        if (rc) {
+            ctx_ = nullptr;
+            return codec_error(rc);
+        }
+    }
+    *out = ctx_;
+    return Error::nil();
+}
+
+// ------------------------------------------------------------------ Reed-Solomon (reed_solomon.go)
+
+static const char* kIncomplete = "block does not have enough source symbols to generate repair symbols";
+static const char* kNotRecoverable = "not enough present symbols to repair the missing ones";
+
+static Error too_big(int biggest) {
+    return Error::text(fmt("source symbol payload len is greater is too big for FEC headers. Max %d and got %d",
+                           (int)kMaxFECPacketBufferSize, biggest));
+}
+
+Error ReedSolomonScheme::New(int k, int m, std::shared_ptr<Engine> engine, std::unique_ptr<ReedSolomonScheme>* out) {
+    // reed_solomon.go:15-23 -> reedsolomon.New(k, m) validation
+    if (k <= 0 || m < 0) return codec_error(FEC_ERR_INV_SHARD_NUM);
+    if (k + m > 256) return codec_error(FEC_ERR_MAX_SHARD_NUM);
+    out->reset(new ReedSolomonScheme(k, m, std::move(engine)));
+    return Error::nil();
+}
+
+Error ReedSolomonScheme::addLengthToSourceSymbolPayload(Block& b, SourceSymbolID ssid, Slice* out) {
+    // reed_solomon.go:70-89
+    auto it = b.ssidToSourcePayload.find(ssid);
+    if (it == b.ssidToSourcePayload.end())
+        return Error::text(fmt("block [%llu, %llu] is complete but SID %llu does not exist",
+                               (unsigned long long)b.smallestSSID, (unsigned long long)b.largestSSID,
+                               (unsigned long long)ssid));
+    Slice& payload = it->second;
+    const uint16_t payloadLen = (uint16_t)payload.len;
+    const int shardLen = (int)kRepairPayloadMetadataLen + b.biggestSourceSymbolLenSoFar;
+    if (shardLen > (int)payload.cap)
+        return Error::text(fmt("shard len (%d) is greater than capacity of payload (%d)", shardLen, (int)payload.cap));
+    if (shardLen < (int)kRepairPayloadMetadataLen)   // Go: negative slice bound panics
+        return Error::text(fmt("shard len (%d) is negative", shardLen - 2));
+    Slice shard = payload.reslice(0, (size_t)shardLen);
+    shard.data()[b.biggestSourceSymbolLenSoFar] = (uint8_t)(payloadLen >> 8);
+    shard.data()[b.biggestSourceSymbolLenSoFar + 1] = (uint8_t)(payloadLen & 0xFF);
+    *out = shard;
+    return Error::nil();
+}
+
+Error ReedSolomonScheme::repairSymbols(Block& b, std::vector<RepairFrame>* out) {   // reed_solomon.go:26-68
+    out->clear();
+    if (!b.isComplete()) return Error::text(kIncomplete);
+    if (b.biggestSourceSymbolLenSoFar > (int)kMaxFECPacketBufferSize) return too_big(b.biggestSourceSymbolLenSoFar);
+    const int nsh = b.totNumSourceSymbols + b.totNumRepairSymbols;
+    std::vector<Slice> shards(nsh > 0 ? nsh : 0);
+    for (int i = 0; i < b.totNumSourceSymbols; ++i) {
+        Error e = addLengthToSourceSymbolPayload(b, b.smallestSSID + (SourceSymbolID)i, &shards[i]);
+        if (!e.ok()) return e;
+    }
+    const size_t L = kRepairPayloadMetadataLen + (size_t)b.biggestSourceSymbolLenSoFar;
+    for (int i = 0; i < b.totNumRepairSymbols; ++i)
+        shards[b.totNumSourceSymbols + i] = Slice::make(0, kMaxPacketBufferSize).reslice(0, L);
+    // enc.Encode(shards): klauspost checks the shard count, then encodes shards[k:] from shards[:k]
+    if (nsh != k_ + m_) return Error::text(std::string("unable to make parity shards: ") + fec_strerror(FEC_ERR_TOO_FEW_SHARDS));
+    if (L == 0) return Error::text(std::string("unable to make parity shards: ") + fec_strerror(FEC_ERR_SHARD_NO_DATA));
+    if (m_ > 0) {
+        fec_ctx* ctx = nullptr;
+        Error e = engine_->ctx(&ctx);
+        if (!e.ok()) return e;
+        std::vector<uint8_t> host((size_t)nsh * L);
+        for (int i = 0; i < k_; ++i) memcpy(&host[(size_t)i * L], shards[i].data(), L);
+        const int rc = fec_rs_encode_batch(ctx, k_, m_, L, 1, host.data(), (size_t)nsh * L, host.data() + (size_t)k_ * L,
+                                           (size_t)nsh * L, L, FEC_HOST);
+        if (rc) return Error{std::string("unable to make parity shards: ") + fec_strerror(rc), rc};
+        for (int i = k_; i < nsh; ++i) memcpy(shards[i].data(), &host[(size_t)i * L], L);
+    }
+    out->resize(b.totNumRepairSymbols);
+    for (int i = 0; i < b.totNumRepairSymbols; ++i) {
+        (*out)[i].block_id = b.id;
+        (*out)[i].parity_id = (ParityID)i;
+        (*out)[i].payload = shards[b.totNumSourceSymbols + i];
+    }
+    return Error::nil();
+}
+
+Error ReedSolomonScheme::recoverSymbolPayloads(Block& b, Slice* out) {   // reed_solomon.go:92-136
+    *out = Slice{};
+    if (!b.isRecoverable()) return Error::text(kNotRecoverable);
+    if (b.isComplete()) return Error::nil();
+    const int nsh = b.totNumSourceSymbols + b.totNumRepairSymbols;
+    std::vector<Slice> shards(nsh > 0 ? nsh : 0);
+    std::vector<int> missing;
+    for (int i = 0; i < b.totNumSourceSymbols; ++i) {
+        const SourceSymbolID ssid = b.smallestSSID + (SourceSymbolID)i;
+        if (!b.ssidToSourcePayload.count(ssid)) {
+            missing.push_back(i);
+            continue;
+        }
+        Error e = addLengthToSourceSymbolPayload(b, ssid, &shards[i]);
+        if (!e.ok()) return e;
+    }
+    for (auto& kv : b.pidToRepairPayload) {
+        const uint64_t i = (uint64_t)b.totNumSourceSymbols + kv.first;
+        if (i >= (uint64_t)nsh)   // Go: index out of range panic
+            return Error::text(fmt("parity id %llu out of range for %d repair symbols",
+                                   (unsigned long long)kv.first, b.totNumRepairSymbols));
+        shards[i] = kv.second;
+    }
+    // enc.ReconstructData(shards): klauspost shard-count / size / presence checks
+    if (nsh != k_ + m_) return codec_error(FEC_ERR_TOO_FEW_SHARDS);
+    size_t L = 0;
+    for (auto& s : shards)
+        if (!s.nil() && s.len) { L = s.len; break; }
+    if (L == 0) return codec_error(FEC_ERR_SHARD_NO_DATA);
+    uint32_t mask = 0;
+    int present = 0;
+    for (int i = 0; i < nsh; ++i) {
+        if (shards[i].nil() || shards[i].len == 0) continue;
+        if (shards[i].len != L) return codec_error(FEC_ERR_SHARD_SIZE);
+        mask |= 1u << i;
+        ++present;
+    }
+    if (present < k_) return codec_error(FEC_ERR_TOO_FEW_SHARDS);
+    if (nsh > FEC_MAX_DECODE_SHARDS) return codec_error(FEC_ERR_MAX_SHARD_NUM);
+    fec_ctx* ctx = nullptr;
+    Error e = engine_->ctx(&ctx);
+    if (!e.ok()) return e;
+    std::vector<uint8_t> host((size_t)nsh * L, 0);
+    for (int i = 0; i < nsh; ++i)
+        if (mask >> i & 1u) memcpy(&host[(size_t)i * L], shards[i].data(), L);
+    int32_t st = 0;
+    const int rc = fec_rs_reconstruct_batch(ctx, k_, m_, L, 1, host.data(), (size_t)nsh * L, host.data() + (size_t)k_ * L,
+                                            (size_t)nsh * L, L, &mask, &st, FEC_HOST);
+    if (rc) return codec_error(rc);
+    // concatenation of the rebuilt payloads, each cut to its trailer length
+    const int big = b.biggestSourceSymbolLenSoFar;
+    Slice res = Slice::make(0, missing.size() * (size_t)std::max(big, 0));
+    std::vector<uint8_t> acc;
+    for (int i : missing) {
+        const uint8_t* sh = &host[(size_t)i * L];
+        if (big < 0 || (size_t)big + 2 > L)   // Go: index out of range panic
+            return Error::text(fmt("length trailer at %d outside shard of %zu bytes", big, L));
+        const size_t payloadLen = ((size_t)sh[big] << 8) | sh[big + 1];
+        if (payloadLen > L)   // Go: slice bounds out of range panic
+            return Error::text(fmt("recovered payload length %zu exceeds shard length %zu", payloadLen, L));
+        acc.insert(acc.end(), sh, sh + payloadLen);
+    }
+    res = Slice::from(acc.data(), acc.size(), std::max(acc.size(), missing.size() * (size_t)std::max(big, 0)));
+    *out = res;
+    return Error::nil();
+}
+
+// ------------------------------------------------------------------ XOR (xor.go)
+
+// One source payload as the XOR scheme folds it in (xor.go:44-56): payload bytes at
+// [0, len), big-endian uint16(len) XORed at [biggest, biggest+2), in an L-byte shard.
+static bool xor_frame(const Slice& p, int biggest, size_t L, uint8_t* dst) {
+    if (biggest < 0 || (size_t)biggest + 2 > L || p.len > L) return false;
+    memset(dst, 0, L);
+    if (p.len) memcpy(dst, p.data(), p.len);
+    const uint16_t ln = (uint16_t)p.len;
+    dst[biggest] ^= (uint8_t)(ln >> 8);
+    dst[biggest + 1] ^= (uint8_t)(ln & 0xFF);
+    return true;
+}
+
+static Error xor_reduce(std::shared_ptr<Engine>& engine, std::vector<uint8_t>& shards, int count, size_t L,
+                        uint8_t* out) {
+    if (count == 0) {
+        memset(out, 0, L);
+        return Error::nil();
+    }
+    fec_ctx* ctx = nullptr;
+    Error e = engine->ctx(&ctx);
+    if (!e.ok()) return e;
+    const int rc = fec_xor_encode_batch(ctx, count, L, 1, shards.data(), (size_t)count * L, out, L, L, FEC_HOST);
+    return rc ? codec_error(rc) : Error::nil();
+}
+
+Error XorScheme::repairSymbols(Block& b, std::vector<RepairFrame>* out) {   // xor.go:14-42
+    out->clear();
+    if (!b.isComplete()) return Error::text(kIncomplete);
+    if (b.totNumRepairSymbols != 1)
+        return Error::text(fmt("xor only supports 1 repair symbol. Expected 1, received %d", b.totNumRepairSymbols));
+    if (b.biggestSourceSymbolLenSoFar > (int)kMaxFECPacketBufferSize) return too_big(b.biggestSourceSymbolLenSoFar);
+    if (b.biggestSourceSymbolLenSoFar < 0) return Error::text("negative repair payload length");
+    const size_t L = kRepairPayloadMetadataLen + (size_t)b.biggestSourceSymbolLenSoFar;
+    const int count = (int)b.ssidToSourcePayload.size();
+    std::vector<uint8_t> shards((size_t)count * L);
+    int i = 0;
+    for (auto& kv : b.ssidToSourcePayload)
+        if (!xor_frame(kv.second, b.biggestSourceSymbolLenSoFar, L, &shards[(size_t)(i++) * L]))
+            return Error::text(fmt("source payload of %zu bytes overruns the %zu-byte repair symbol",
+                                   kv.second.len, L));   // Go: index out of range panic
+    Slice rep = Slice::make(L, L);
+    Error e = xor_reduce(engine_, shards, count, L, rep.data());
+    if (!e.ok()) return e;
+    out->resize(1);
+    (*out)[0].block_id = b.id;
+    (*out)[0].parity_id = 0;
+    (*out)[0].payload = rep;
+    return Error::nil();
+}
+
+Error XorScheme::recoverSymbolPayloads(Block& b, Slice* out) {   // xor.go:66-104
+    *out = Slice{};
+    if (!b.isRecoverable()) return Error::text(kNotRecoverable);
+    if (b.isComplete()) return Error::nil();
+    const size_t L = kMaxPacketBufferSize;
+    const int count = (int)(b.pidToRepairPayload.size() + b.ssidToSourcePayload.size());
+    std::vector<uint8_t> shards((size_t)count * L, 0);
+    int i = 0;
+    for (auto& kv : b.pidToRepairPayload) {   // xorRepair: whole repair payload
+        if (kv.second.len > L) return Error::text("repair payload longer than the packet buffer");
+        if (kv.second.len) memcpy(&shards[(size_t)i * L], kv.second.data(), kv.second.len);
+        ++i;
+    }
+    for (auto& kv : b.ssidToSourcePayload)
+        if (!xor_frame(kv.second, b.biggestSourceSymbolLenSoFar, L, &shards[(size_t)(i++) * L]))
+            return Error::text("source payload overruns the packet buffer");
+    Slice rec = Slice::make(L, L);
+    Error e = xor_reduce(engine_, shards, count, L, rec.data());
+    if (!e.ok()) return e;
+    const int big = b.biggestSourceSymbolLenSoFar;
+    if (big < 0 || (size_t)big + 2 > L) return Error::text("length trailer outside the packet buffer");
+    const size_t payloadLen = ((size_t)rec.data()[big] << 8) | rec.data()[big + 1];
+    if (payloadLen > L) return Error::text("recovered payload length exceeds the packet buffer");
+    Slice recovered = rec.reslice(0, payloadLen);
+    for (SourceSymbolID ssid = b.smallestSSID;; ++ssid) {
+        if (!b.ssidToSourcePayload.count(ssid)) b.ssidToSourcePayload[ssid] = recovered;
+        if (ssid == b.largestSSID) break;
+    }
+    if (!b.isComplete()) return Error::text("block is not complete after recovery");
+    *out = recovered;
+    return Error::nil();
+}
+
+// ------------------------------------------------------------------ manager (manager.go)
+
+Error Manager::New(std::unique_ptr<BlockFECScheme> scheme, int k, int m, std::unique_ptr<Manager>* out) {
+    // manager.go:96-109
+    if (k < 0 || m < 0)
+        return Error::text(fmt("numTotSourceSymbols (%d) and numTotRepairSymbols (%d) may not be negative", k, m));
+    std::unique_ptr<Manager> mg(new Manager());
+    mg->scheme_ = std::move(scheme);
+    mg->numTotSourceSymbols_ = k;
+    mg->numTotRepairSymbols_ = m;
+    *out = std::move(mg);
+    return Error::nil();
+}
+
+SourceSymbolID Manager::NextSSID() {   // manager.go:111-117
+    std::lock_guard<std::mutex> g(nextSIDMutex_);
+    return nextSID_++;
+}
+
+BlockID Manager::sidToBlockID(SourceSymbolID sid) const {   // manager.go:119-121
+    return numTotSourceSymbols_ > 0 ? sid / (uint64_t)numTotSourceSymbols_ : 0;   // Go: divide-by-zero panic
+}
+
+Manager::BlockStatus& Manager::statusFor(BlockID id) {
+    auto it = blockStatuses_.find(id);
+    if (it == blockStatuses_.end()) {
+        BlockStatus st;
+        st.block.reset(new Block(Block::New(id, numTotSourceSymbols_, numTotRepairSymbols_)));
+        it = blockStatuses_.emplace(id, std::move(st)).first;
+    }
+    return it->second;
+}
+
+Error Manager::AddSourceSymbolFrame(const SourceSymbolFrame& f, std::vector<RepairFrame>* out) {   // :123-158
+    out->clear();
+    BlockStatus& bs = statusFor(sidToBlockID(f.ssid));
+    if (bs.isProcessed) return Error::nil();
+    Error e = bs.block->addSourceSymbol(f);
+    if (!e.ok()) return e;
+    if (bs.block->isComplete()) {
+        std::vector<RepairFrame> rep;
+        e = scheme_->repairSymbols(*bs.block, &rep);
+        if (!e.ok()) return e;
+        bs.block.reset();
+        bs.isProcessed = true;
+        *out = std::move(rep);
+    }
+    return Error::nil();
+}
+
+Error Manager::HandleRepairFrame(const RepairFrame& f, Slice* out) {   // manager.go:160-198
+    *out = Slice{};
+    BlockStatus& bs = statusFor(f.block_id);
+    if (bs.isProcessed) return Error::nil();
+    Error e = bs.block->addRepairSymbol(f);
+    if (!e.ok()) return e;
+    if (bs.block->isRecoverable()) {
+        Slice rec;
+        e = scheme_->recoverSymbolPayloads(*bs.block, &rec);
+        if (!e.ok()) return e;
+        bs.block.reset();
+        bs.isProcessed = true;
+        *out = rec;
+    }
+    return Error::nil();
+}
+
+Error Manager::HandleSourceSymbolFrame(const SourceSymbolFrame& f, Slice* out) {   // manager.go:200-227
+    *out = Slice{};
+    BlockStatus& bs = statusFor(sidToBlockID(f.ssid));
+    if (bs.isProcessed) return Error::nil();
+    Error e = bs.block->addSourceSymbol(f);
+    if (!e.ok()) return e;
+    if (bs.block->isComplete()) {
+        bs.block.reset();
+        bs.isProcessed = true;
+    }
+    *out = f.payload;
+    return Error::nil();
+}
+
+static Error new_manager(DecoderFECScheme id, std::shared_ptr<Engine> engine, std::unique_ptr<Manager>* out) {
+    // manager.go:50-94 (NewSender and NewReceiver are identical)
+    out->reset();
+    switch (id) {
+        case FECDisabled:
+            return Error::nil();
+        case XORFECScheme:
+            return Manager::New(std::unique_ptr<BlockFECScheme>(new XorScheme(std::move(engine))), 2, 1, out);
+        case ReedSolomonFECScheme: {
+            std::unique_ptr<ReedSolomonScheme> rs;
+            Error e = ReedSolomonScheme::New(20, 10, std::move(engine), &rs);
+            if (!e.ok()) return e;
+            return Manager::New(std::move(rs), 20, 10, out);
+        }
+        default:
+            return Error::text(fmt("unknown FEC scheme: %d", (int)id));
+    }
+}
+
+Error NewSender(DecoderFECScheme id, std::shared_ptr<Engine> engine, std::unique_ptr<Manager>* out) {
+    return new_manager(id, std::move(engine), out);
+}
+
+Error NewReceiver(DecoderFECScheme id, std::shared_ptr<Engine> engine, std::unique_ptr<Manager>* out) {
+    return new_manager(id, std::move(engine), out);
+}
+
+}  // namespace fec
+
+// ------------------------------------------------------------------ C ABI (include/fec_scheme.h)
+
+struct fec_block {
+    fec::Block b;
+};
+struct fec_scheme {
+    std::unique_ptr<fec::BlockFECScheme> s;
+};
+struct fec_manager {
+    std::unique_ptr<fec::Manager> m;
+};
+struct fec_frames {
+    std::vector<fec::RepairFrame> f;
+};
+struct fec_bytes {
+    fec::Slice s;
+};
+
+static thread_local std::string t_last_error;
+
+static int report(const fec::Error& e) {
+    if (e.ok()) {
+        t_last_error.clear();
+        return FEC_OK;
+    }
+    t_last_error = e.msg;
+    return e.code ? e.code : FEC_ERR_SCHEME;
+}
+
+static std::shared_ptr<fec::Engine> engine_for(int device) {
+    // one engine (one fec_ctx, created lazily) per device per thread
+    static thread_local std::map<int, std::shared_ptr<fec::Engine>> engines;
+    auto& e = engines[device];
+    if (!e) e = std::make_shared<fec::Engine>(device);
+    return e;
+}
+
+extern "C" {
+
+const char* fec_last_error(void) { return t_last_error.c_str(); }
+
+fec_block* fec_block_new(uint64_t id, int tot_src, int tot_rep) {
+    fec_block* b = new fec_block();
+    b->b = fec::Block::New(id, tot_src, tot_rep);
+    return b;
+}
+
+fec_block* fec_block_literal(uint64_t id, int tot_src, int tot_rep, int biggest, uint64_t smallest, uint64_t largest) {
+    fec_block* b = new fec_block();
+    b->b.id = id;
+    b->b.totNumSourceSymbols = tot_src;
+    b->b.totNumRepairSymbols = tot_rep;
+    b->b.biggestSourceSymbolLenSoFar = biggest;
+    b->b.smallestSSID = smallest;
+    b->b.largestSSID = largest;
+    return b;
+}
+
+void fec_block_free(fec_block* b) { delete b; }
+
+int fec_block_put_source(fec_block* b, uint64_t ssid, const uint8_t* p, size_t len, size_t cap) {
+    if (!b || (len && !p)) return FEC_ERR_INVALID_ARG;
+    b->b.ssidToSourcePayload[ssid] = fec::Slice::from(p, len, cap);
+    return FEC_OK;
+}
+
+int fec_block_put_repair(fec_block* b, uint64_t pid, const uint8_t* p, size_t len) {
+    if (!b || (len && !p)) return FEC_ERR_INVALID_ARG;
+    b->b.pidToRepairPayload[pid] = fec::Slice::from(p, len, len);
+    return FEC_OK;
+}
+
+int fec_block_add_source_symbol(fec_block* b, uint64_t ssid, const uint8_t* p, size_t len, size_t cap) {
+    if (!b || (len && !p)) return FEC_ERR_INVALID_ARG;
+    fec::SourceSymbolFrame f{ssid, fec::Slice::from(p, len, cap)};
+    return report(b->b.addSourceSymbol(f));
+}
+
+int fec_block_add_repair_symbol(fec_block* b, uint64_t block_id, uint64_t pid, const uint8_t* p, size_t len) {
+    if (!b || (len && !p)) return FEC_ERR_INVALID_ARG;
+    fec::RepairFrame f{block_id, pid, fec::Slice::from(p, len, len)};
+    return report(b->b.addRepairSymbol(f));
+}
+
+int fec_block_is_recoverable(const fec_block* b) { return b && b->b.isRecoverable(); }
+int fec_block_is_complete(const fec_block* b) { return b && b->b.isComplete(); }
+int fec_block_biggest(const fec_block* b) { return b ? b->b.biggestSourceSymbolLenSoFar : 0; }
+int fec_block_num_sources(const fec_block* b) { return b ? (int)b->b.ssidToSourcePayload.size() : 0; }
+
+long fec_block_get_source(const fec_block* b, uint64_t ssid, uint8_t* out, size_t out_cap) {
+    if (!b) return -1;
+    auto it = b->b.ssidToSourcePayload.find(ssid);
+    if (it == b->b.ssidToSourcePayload.end()) return -1;
+    const size_t n = std::min(out_cap, it->second.len);
+    if (n && out) memcpy(out, it->second.data(), n);
+    return (long)it->second.len;
+}
+
+fec_scheme* fec_scheme_new(int scheme_id, int k, int m, int device) {
+    fec_scheme* s = new fec_scheme();
+    if (scheme_id == fec::XORFECScheme) {
+        s->s.reset(new fec::XorScheme(engine_for(device)));
+    } else if (scheme_id == fec::ReedSolomonFECScheme) {
+        std::unique_ptr<fec::ReedSolomonScheme> rs;
+        if (report(fec::ReedSolomonScheme::New(k, m, engine_for(device), &rs)) != FEC_OK) {
+            delete s;
+            return nullptr;
+        }
+        s->s = std::move(rs);
+    } else {
+        report(fec::Error::text(fec::fmt("unknown FEC scheme: %d", scheme_id)));
+        delete s;
+        return nullptr;
+    }
+    t_last_error.clear();
+    return s;
+}
+
+void fec_scheme_free(fec_scheme* s) { delete s; }
+
+int fec_scheme_repair_symbols(fec_scheme* s, fec_block* b, fec_frames** out) {
+    if (!s || !b || !out) return FEC_ERR_INVALID_ARG;
+    *out = nullptr;
+    std::vector<fec::RepairFrame> f;
+    const int rc = report(s->s->repairSymbols(b->b, &f));
+    if (rc == FEC_OK) *out = new fec_frames{std::move(f)};
+    return rc;
+}
+
+int fec_scheme_recover_symbol_payloads(fec_scheme* s, fec_block* b, fec_bytes** out) {
+    if (!s || !b || !out) return FEC_ERR_INVALID_ARG;
+    *out = nullptr;
+    fec::Slice r;
+    const int rc = report(s->s->recoverSymbolPayloads(b->b, &r));
+    if (rc == FEC_OK && !r.nil()) *out = new fec_bytes{r};
+    return rc;
+}
+
+size_t fec_frames_count(const fec_frames* f) { return f ? f->f.size() : 0; }
+
+int fec_frames_get(const fec_frames* f, size_t i, uint64_t* block_id, uint64_t* parity_id, const uint8_t** payload,
+                   size_t* len) {
+    if (!f || i >= f->f.size()) return FEC_ERR_INVALID_ARG;
+    const fec::RepairFrame& r = f->f[i];
+    if (block_id) *block_id = r.block_id;
+    if (parity_id) *parity_id = r.parity_id;
+    if (payload) *payload = r.payload.data();
+    if (len) *len = r.payload.len;
+    return FEC_OK;
+}
+
+void fec_frames_free(fec_frames* f) { delete f; }
+
+const uint8_t* fec_bytes_data(const fec_bytes* b) { return b ? b->s.data() : nullptr; }
+size_t fec_bytes_len(const fec_bytes* b) { return b ? b->s.len : 0; }
+void fec_bytes_free(fec_bytes* b) { delete b; }
+
+static fec_manager* make_manager(fec::Error (*fn)(fec::DecoderFECScheme, std::shared_ptr<fec::Engine>,
+                                                  std::unique_ptr<fec::Manager>*),
+                                 int scheme_id, int device, int* err) {
+    std::unique_ptr<fec::Manager> m;
+    const int rc = report(fn((fec::DecoderFECScheme)scheme_id, engine_for(device), &m));
+    if (err) *err = rc;
+    if (rc != FEC_OK || !m) return nullptr;
+    return new fec_manager{std::move(m)};
+}
+
+fec_manager* fec_manager_new_sender(int scheme_id, int device, int* err) {
+    return make_manager(fec::NewSender, scheme_id, device, err);
+}
+
+fec_manager* fec_manager_new_receiver(int scheme_id, int device, int* err) {
+    return make_manager(fec::NewReceiver, scheme_id, device, err);
+}
+
+fec_manager* fec_manager_new(int scheme_id, int k, int m, int device, int* err) {
+    std::unique_ptr<fec::BlockFECScheme> s;
+    fec::Error e;
+    if (scheme_id == fec::XORFECScheme) {
+        s.reset(new fec::XorScheme(engine_for(device)));
+    } else if (scheme_id == fec::ReedSolomonFECScheme) {
+        std::unique_ptr<fec::ReedSolomonScheme> rs;
+        e = fec::ReedSolomonScheme::New(k, m, engine_for(device), &rs);
+        s = std::move(rs);
+    } else {
+        e = fec::Error::text(fec::fmt("unknown FEC scheme: %d", scheme_id));
+    }
+    std::unique_ptr<fec::Manager> mg;
+    if (e.ok()) e = fec::Manager::New(std::move(s), k, m, &mg);
+    const int rc = report(e);
+    if (err) *err = rc;
+    return rc == FEC_OK ? new fec_manager{std::move(mg)} : nullptr;
+}
+
+void fec_manager_free(fec_manager* m) { delete m; }
+
+uint64_t fec_manager_next_ssid(fec_manager* m) { return m ? m->m->NextSSID() : 0; }
+
+uint64_t fec_manager_block_id(const fec_manager* m, uint64_t ssid) { return m ? m->m->sidToBlockID(ssid) : 0; }
+
+int fec_manager_add_source_symbol_frame(fec_manager* m, uint64_t ssid, const uint8_t* p, size_t len, size_t cap,
+                                        fec_frames** out) {
+    if (!m || !out || (len && !p)) return FEC_ERR_INVALID_ARG;
+    *out = nullptr;
+    std::vector<fec::RepairFrame> f;
+    const int rc = report(m->m->AddSourceSymbolFrame(fec::SourceSymbolFrame{ssid, fec::Slice::from(p, len, cap)}, &f));
+    if (rc == FEC_OK && !f.empty()) *out = new fec_frames{std::move(f)};
+    return rc;
+}
+
+int fec_manager_handle_repair_frame(fec_manager* m, uint64_t block_id, uint64_t pid, const uint8_t* p, size_t len,
+                                    fec_bytes** out) {
+    if (!m || !out || (len && !p)) return FEC_ERR_INVALID_ARG;
+    *out = nullptr;
+    fec::Slice r;
+    const int rc = report(m->m->HandleRepairFrame(fec::RepairFrame{block_id, pid, fec::Slice::from(p, len, len)}, &r));
+    if (rc == FEC_OK && !r.nil()) *out = new fec_bytes{r};
+    return rc;
+}
+
+int fec_manager_handle_source_symbol_frame(fec_manager* m, uint64_t ssid, const uint8_t* p, size_t len, size_t cap,
+                                           fec_bytes** out) {
+    if (!m || !out || (len && !p)) return FEC_ERR_INVALID_ARG;
+    *out = nullptr;
+    fec::Slice r;
+    const int rc =
+        report(m->m->HandleSourceSymbolFrame(fec::SourceSymbolFrame{ssid, fec::Slice::from(p, len, cap)}, &r));
+    if (rc == FEC_OK && !r.nil()) *out = new fec_bytes{r};
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,175 @@
+// fec_scheme.hpp — C++ mirror of the reference's internal/fec scheme and manager layer.
+//
+// ddritzenhoff/0xFEC keeps its block bookkeeping in Go (internal/fec/block.go,
+// manager.go) and its arithmetic in klauspost/reedsolomon + Go byte loops
+// (reed_solomon.go, xor.go). The Go toolchain is absent from this build image, so the
+// layer above the C ABI is restated here in C++ with the same names, argument meaning,
+// error texts and error ordering; the arithmetic goes through lib0xfec_hip.so
+// (include/fec_hip.h) on the GPU. A Go integration keeps its own Go code and binds only
+// fec_hip.h; this mirror is what the parity tests drive.
+//
+// Go slices are modelled by Slice (shared backing array, len, cap) because the reference
+// relies on slice aliasing: addLengthToSourceSymbolPayload writes the length trailer into
+// the payload's spare capacity (reed_solomon.go:70-89) and xorScheme.recoverSymbolPayloads
+// stores the recovered slice into the block map (xor.go:91-96).
+#pragma once
+
+#include <stdint.h>
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+struct fec_ctx;
+
+namespace fec {
+
+// internal/protocol/protocol.go:111,136-140
+constexpr size_t kMaxPacketBufferSize = 1452;
+constexpr size_t kMaxFECHeaderOverhead = 18;
+constexpr size_t kMaxFECPacketBufferSize = kMaxPacketBufferSize - kMaxFECHeaderOverhead;   // 1434
+constexpr size_t kRepairPayloadMetadataLen = 2;
+
+// internal/protocol/fec.go:8-27
+using SourceSymbolID = uint64_t;
+using BlockID = uint64_t;
+using ParityID = uint64_t;
+enum DecoderFECScheme : uint8_t { FECDisabled = 0, XORFECScheme = 1, ReedSolomonFECScheme = 2 };
+
+// A Go []byte: a window [off, off+len) of a shared backing array with capacity cap.
+struct Slice {
+    std::shared_ptr<std::vector<uint8_t>> buf;
+    size_t off = 0, len = 0, cap = 0;
+
+    static Slice make(size_t len, size_t cap);                    // make([]byte, len, cap), zeroed
+    static Slice from(const uint8_t* p, size_t len, size_t cap);  // copy of p, spare capacity zeroed
+    bool nil() const { return !buf; }
+    uint8_t* data() { return buf ? buf->data() + off : nullptr; }
+    const uint8_t* data() const { return buf ? buf->data() + off : nullptr; }
+    Slice reslice(size_t lo, size_t hi) const;                    // s[lo:hi], hi <= cap
+    std::vector<uint8_t> bytes() const { return std::vector<uint8_t>(data(), data() + len); }
+};
+
+// A Go error: ok() when nil.
+struct Error {
+    std::string msg;
+    int code = 0;   // 0: scheme/bookkeeping error (msg); < 0: fec_hip.h codec code
+    bool ok() const { return msg.empty() && code == 0; }
+    static Error nil() { return Error{}; }
+    static Error text(std::string m) { return Error{std::move(m), 0}; }
+};
+
+// internal/wire/fec_repair_frame.go:11-14, fec_source_symbol_frame.go:11-17
+struct RepairFrame {
+    BlockID block_id = 0;
+    ParityID parity_id = 0;
+    Slice payload;
+};
+
+struct SourceSymbolFrame {
+    SourceSymbolID ssid = 0;
+    Slice payload;
+};
+
+// internal/fec/block.go:23-95
+struct Block {
+    BlockID id = 0;
+    std::map<SourceSymbolID, Slice> ssidToSourcePayload;
+    std::map<ParityID, Slice> pidToRepairPayload;
+    SourceSymbolID smallestSSID = 0, largestSSID = 0;
+    int totNumSourceSymbols = 0;
+    int totNumRepairSymbols = 0;
+    int biggestSourceSymbolLenSoFar = 0;
+
+    static Block New(BlockID id, int totNumSourceSymbols, int totNumRepairSymbols);   // newBlock
+    Error addSourceSymbol(const SourceSymbolFrame& f);
+    Error addRepairSymbol(const RepairFrame& f);
+    bool isRecoverable() const;
+    bool isComplete() const;
+};
+
+// internal/fec/scheme.go:5-10
+class BlockFECScheme {
+public:
+    virtual ~BlockFECScheme() = default;
+    virtual Error repairSymbols(Block& b, std::vector<RepairFrame>* out) = 0;
+    // *out stays nil (Slice::nil()) when the reference returns nil, nil.
+    virtual Error recoverSymbolPayloads(Block& b, Slice* out) = 0;
+};
+
+// Device binding shared by the schemes of one process thread: one fec_ctx per device,
+// created on first compute (a scheme can be built and validated without a GPU).
+class Engine {
+public:
+    explicit Engine(int device) : device_(device) {}
+    ~Engine();
+    Error ctx(fec_ctx** out);
+    int device() const { return device_; }
+
+private:
+    int device_;
+    fec_ctx* ctx_ = nullptr;
+};
+
+// internal/fec/reed_solomon.go:11-136 (klauspost Encode/ReconstructData -> HIP kernels)
+class ReedSolomonScheme : public BlockFECScheme {
+public:
+    // NewReedSolomonScheme (reed_solomon.go:15-23); klauspost New validation.
+    static Error New(int numTotSourceSymbols, int numTotRepairSymbols, std::shared_ptr<Engine> engine,
+                     std::unique_ptr<ReedSolomonScheme>* out);
+    Error repairSymbols(Block& b, std::vector<RepairFrame>* out) override;
+    Error recoverSymbolPayloads(Block& b, Slice* out) override;
+    int dataShards() const { return k_; }
+    int parityShards() const { return m_; }
+
+private:
+    ReedSolomonScheme(int k, int m, std::shared_ptr<Engine> e) : k_(k), m_(m), engine_(std::move(e)) {}
+    Error addLengthToSourceSymbolPayload(Block& b, SourceSymbolID ssid, Slice* out);
+    int k_, m_;
+    std::shared_ptr<Engine> engine_;
+};
+
+// internal/fec/xor.go:10-104 (byte loops -> HIP XOR kernel)
+class XorScheme : public BlockFECScheme {
+public:
+    explicit XorScheme(std::shared_ptr<Engine> engine) : engine_(std::move(engine)) {}
+    Error repairSymbols(Block& b, std::vector<RepairFrame>* out) override;
+    Error recoverSymbolPayloads(Block& b, Slice* out) override;
+
+private:
+    std::shared_ptr<Engine> engine_;
+};
+
+// internal/fec/manager.go:13-227
+class Manager {
+public:
+    static Error New(std::unique_ptr<BlockFECScheme> scheme, int numTotSourceSymbols, int numTotRepairSymbols,
+                     std::unique_ptr<Manager>* out);
+    SourceSymbolID NextSSID();
+    Error AddSourceSymbolFrame(const SourceSymbolFrame& f, std::vector<RepairFrame>* out);
+    Error HandleRepairFrame(const RepairFrame& f, Slice* out);
+    Error HandleSourceSymbolFrame(const SourceSymbolFrame& f, Slice* out);
+    BlockID sidToBlockID(SourceSymbolID sid) const;
+    size_t trackedBlocks() const { return blockStatuses_.size(); }
+
+private:
+    struct BlockStatus {
+        std::unique_ptr<Block> block;
+        bool isProcessed = false;
+    };
+    BlockStatus& statusFor(BlockID id);
+    std::unique_ptr<BlockFECScheme> scheme_;
+    std::mutex nextSIDMutex_;
+    SourceSymbolID nextSID_ = 0;
+    int numTotSourceSymbols_ = 0;
+    int numTotRepairSymbols_ = 0;
+    std::map<BlockID, BlockStatus> blockStatuses_;
+};
+
+// manager.go:50-94: XOR -> (2,1), ReedSolomon -> (20,10); FECDisabled -> nil manager, nil error.
+Error NewSender(DecoderFECScheme id, std::shared_ptr<Engine> engine, std::unique_ptr<Manager>* out);
+Error NewReceiver(DecoderFECScheme id, std::shared_ptr<Engine> engine, std::unique_ptr<Manager>* out);
+
+}  // namespace fec
