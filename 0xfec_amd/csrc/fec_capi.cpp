@@ -184,6 +184,7 @@ static int rs_encode_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks
             a.div_cps = fk::make_fastdiv(cps);
             a.tabs = code->d_tabs + (size_t)r0 * k * 8;
             a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
+            a.rot = fk::g_tune.rotate ? fk::line_rotation(ss, cps) : 0;
             const size_t lds = (size_t)mr * k * sizeof(gf::PermTab);
             int grid = grid_for(ctx, 0, (uint32_t)mr, lds <= 65536 ? lds : 0);
             grid = flat_grid(grid, a.total);
@@ -240,6 +241,7 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         a.ntiles = (uint32_t)((nb + G - 1) / G);
         a.div_cps = fk::make_fastdiv(cps);
         a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
+        a.rot = fk::g_tune.rotate ? fk::line_rotation(ss, cps) : 0;
         a.out = out ? out + b0 * out_bs : nullptr;
         a.out_bs = out_bs;
         int grid;
@@ -271,6 +273,7 @@ static int xor_encode_device(fec_ctx* ctx, int k, size_t len, size_t nblocks, co
         a.total = (uint32_t)(nb * cps);
         a.div_cps = fk::make_fastdiv(cps);
         a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
+        a.rot = fk::g_tune.rotate ? fk::line_rotation(ss, cps) : 0;
         int grid = grid_for(ctx, 2, 1, 0);
         grid = flat_grid(grid, a.total);
         if (grid < 1) grid = 1;
@@ -303,6 +306,7 @@ static int xor_reconstruct_device(fec_ctx* ctx, int k, size_t len, size_t nblock
         a.total = (uint32_t)(nb * cps);
         a.div_cps = fk::make_fastdiv(cps);
         a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
+        a.rot = fk::g_tune.rotate ? fk::line_rotation(ss, cps) : 0;
         int grid = grid_for(ctx, 2, 1, 0);
         grid = flat_grid(grid, a.total);
         if (grid < 1) grid = 1;
@@ -474,7 +478,7 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
     int* slot = key == 0 ? &fk::g_tune.enc_nt : key == 1 ? &fk::g_tune.dec_nt
               : key == 2 ? &fk::g_tune.grid_mult : key == 3 ? &fk::g_tune.dec_max_rounds
               : key == 4 ? &fk::g_tune.pad_zero : key == 5 ? &fk::g_tune.items_per_thread
-              : key == 6 ? &fk::g_tune.tiles_per_wg : nullptr;
+              : key == 6 ? &fk::g_tune.tiles_per_wg : key == 7 ? &fk::g_tune.rotate : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

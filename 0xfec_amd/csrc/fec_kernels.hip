@@ -35,7 +35,7 @@ FastDiv make_fastdiv(uint32_t d) {
 PlanLayout plan_layout(uint32_t k, uint32_t maxe) {
     PlanLayout l;
     l.in_off = 0;
-    l.out_off = 32;                                  // in slots: 32 bytes (k <= 31)
+    l.out_off = (k + 7) & ~7u;                       // in slots, read 8 at a time
     l.nout_off = l.out_off + maxe;
     l.coef_off = (l.nout_off + 1 + 3) & ~3u;
     l.stride = (l.coef_off + maxe * k + 15) & ~15u;
@@ -45,6 +45,14 @@ PlanLayout plan_layout(uint32_t k, uint32_t maxe) {
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
     const uint32_t t = __umulhi(n, f.magic);
     return (uint32_t)(((uint64_t)t + n) >> f.shift);
+}
+
+// Item order inside a block: the first `rot` items take the last `rot` chunks of the shard,
+// so a shard's tail and the next shard's head — which share a 128-byte line when the shard
+// stride is an odd multiple of 64 (1216 = 9.5 lines) — are loaded by neighbouring lanes of
+// one wave on consecutive instructions, and the line is fetched from HBM once.
+__device__ __forceinline__ uint32_t rotate_chunk(uint32_t c, uint32_t cps, uint32_t rot) {
+    return c < rot ? c + (cps - rot) : c - rot;
 }
 
 struct Idx {
@@ -140,8 +148,10 @@ __device__ __forceinline__ void mac(uint4& acc, const Idx (&ix)[4], const gf::Pe
 // One lane = one 16-byte column chunk of one block; all m parities accumulate in VGPRs.
 // Inputs are loaded 8 shards at a time (clamped, so loads are never predicated), then
 // each input updates every parity accumulator with its LDS-broadcast PermTab.
-template <int MAXM, bool LDS_TABS, bool NT>
+// POL: bit 0 non-temporal loads, bit 1 non-temporal stores.
+template <int MAXM, bool LDS_TABS, int POL>
 __global__ __launch_bounds__(kThreads) void rs_encode_kernel(EncodeArgs a) {
+    constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const gf::PermTab* tabs;
     if constexpr (LDS_TABS) {
@@ -157,7 +167,7 @@ __global__ __launch_bounds__(kThreads) void rs_encode_kernel(EncodeArgs a) {
     const uint32_t stride = gridDim.x * kThreads;
     for (uint32_t item = blockIdx.x * kThreads + threadIdx.x; item < a.total; item += stride) {
         const uint32_t b = fdiv(item, a.div_cps);
-        const uint32_t c = item - b * a.cps;
+        const uint32_t c = rotate_chunk(item - b * a.cps, a.cps, a.rot);
         const uint8_t* src = a.in + (uint64_t)b * a.in_bs + (uint64_t)c * kChunk;
         uint4 acc[MAXM];
 #pragma unroll
@@ -165,7 +175,7 @@ __global__ __launch_bounds__(kThreads) void rs_encode_kernel(EncodeArgs a) {
         for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
             uint4 x[kInGroup];
 #pragma unroll
-            for (int jj = 0; jj < kInGroup; ++jj) x[jj] = ld16<NT>(src + (uint64_t)min(j0 + jj, k - 1) * a.ss);
+            for (int jj = 0; jj < kInGroup; ++jj) x[jj] = ld16<NTL>(src + (uint64_t)min(j0 + jj, k - 1) * a.ss);
 #pragma unroll
             for (int jj = 0; jj < kInGroup; ++jj) {
                 if (j0 + jj < k) {
@@ -180,7 +190,7 @@ __global__ __launch_bounds__(kThreads) void rs_encode_kernel(EncodeArgs a) {
         const uint32_t nb = a.len - c * kChunk;
 #pragma unroll
         for (int r = 0; r < MAXM; ++r)
-            if (r < (int)m) store_chunk<NT>(dst + (uint64_t)r * a.ss, acc[r], nb, a.pad_zero);
+            if (r < (int)m) store_chunk<NTS>(dst + (uint64_t)r * a.ss, acc[r], nb, a.pad_zero);
     }
 }
 
@@ -304,8 +314,9 @@ __global__ __launch_bounds__(kPlanThreads) void rs_plan_kernel(PlanArgs a) {
 // every coefficient to its PermTab once, then lanes sweep the G*cps (block, chunk) items.
 // Rows beyond a block's own erasure count carry zero tables, and each item loops only to
 // the wave's largest erasure count (ballot), so one-erasure batches do one row of work.
-template <int MAXE, bool NT>
+template <int MAXE, int POL>
 __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
+    constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t k = a.k, G = a.g, maxe = a.maxe;
     const PlanLayout lay = a.lay;
@@ -339,7 +350,7 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
             const uint32_t t = base + threadIdx.x;
             const bool inr = t < nitems;
             const uint32_t g = inr ? fdiv(t, a.div_cps) : 0;
-            const uint32_t c = t - g * a.cps;
+            const uint32_t c = rotate_chunk(t - g * a.cps, a.cps, a.rot);
             const uint8_t* P = plans + g * lay.stride;
             const uint32_t nout = inr ? P[lay.nout_off] : 0;
             uint32_t rows = 0;
@@ -362,7 +373,7 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
                     const uint32_t w = jj < 4 ? sl.x : sl.y;
                     uint32_t slot = (w >> (8 * (jj & 3))) & 0xFFu;
                     if (j0 + jj >= k) slot = (sl.x & 0xFFu);   // clamp to a valid shard
-                    x[jj] = ld16<NT>(slot < k ? dblk + (uint64_t)slot * a.ss : pblk + (uint64_t)(slot - k) * a.ss);
+                    x[jj] = ld16<NTL>(slot < k ? dblk + (uint64_t)slot * a.ss : pblk + (uint64_t)(slot - k) * a.ss);
                 }
 #pragma unroll
                 for (int jj = 0; jj < kInGroup; ++jj) {
@@ -380,26 +391,27 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
 #pragma unroll
             for (int r = 0; r < MAXE; ++r)
                 if (r < (int)nout)
-                    store_chunk<NT>(oblk ? oblk + (uint64_t)r * a.ss : dblk + (uint64_t)out_idx[r] * a.ss, acc[r],
+                    store_chunk<NTS>(oblk ? oblk + (uint64_t)r * a.ss : dblk + (uint64_t)out_idx[r] * a.ss, acc[r],
                                     nb, a.pad_zero);
         }
     }
 }
 
 // ------------------------------------------------------------------ XOR
-template <bool NT>
+template <int POL>
 __global__ __launch_bounds__(kThreads) void xor_encode_kernel(XorArgs a) {
+    constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     const uint32_t k = a.k;
     const uint32_t stride = gridDim.x * kThreads;
     for (uint32_t item = blockIdx.x * kThreads + threadIdx.x; item < a.total; item += stride) {
         const uint32_t b = fdiv(item, a.div_cps);
-        const uint32_t c = item - b * a.cps;
+        const uint32_t c = rotate_chunk(item - b * a.cps, a.cps, a.rot);
         const uint8_t* src = a.in + (uint64_t)b * a.in_bs + (uint64_t)c * kChunk;
         uint4 acc = make_uint4(0, 0, 0, 0);
         for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
             uint4 x[kInGroup];
 #pragma unroll
-            for (int jj = 0; jj < kInGroup; ++jj) x[jj] = ld16<NT>(src + (uint64_t)min(j0 + jj, k - 1) * a.ss);
+            for (int jj = 0; jj < kInGroup; ++jj) x[jj] = ld16<NTL>(src + (uint64_t)min(j0 + jj, k - 1) * a.ss);
 #pragma unroll
             for (int jj = 0; jj < kInGroup; ++jj)
                 if (j0 + jj < k) {
@@ -409,18 +421,19 @@ __global__ __launch_bounds__(kThreads) void xor_encode_kernel(XorArgs a) {
                     acc.w ^= x[jj].w;
                 }
         }
-        store_chunk<NT>(a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk, acc, a.len - c * kChunk, a.pad_zero);
+        store_chunk<NTS>(a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk, acc, a.len - c * kChunk, a.pad_zero);
     }
 }
 
-template <bool NT>
+template <int POL>
 __global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
+    constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     const uint32_t k = a.k, n = k + 1;
     const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
     const uint32_t stride = gridDim.x * kThreads;
     for (uint32_t item = blockIdx.x * kThreads + threadIdx.x; item < a.total; item += stride) {
         const uint32_t b = fdiv(item, a.div_cps);
-        const uint32_t c = item - b * a.cps;
+        const uint32_t c = rotate_chunk(item - b * a.cps, a.cps, a.rot);
         const uint32_t miss = ~a.masks[b] & all;
         const uint32_t nmiss = __popc(miss);
         const uint32_t mi = miss ? (uint32_t)__ffs(miss) - 1 : 0;
@@ -440,7 +453,7 @@ __global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
             for (int jj = 0; jj < kInGroup; ++jj) {
                 const uint32_t j = min(j0 + jj, k - 1);
                 const uint32_t s = j + (j >= mi);     // the k shards other than the missing one
-                x[jj] = ld16<NT>(s < k ? blk + (uint64_t)s * a.ss : par);
+                x[jj] = ld16<NTL>(s < k ? blk + (uint64_t)s * a.ss : par);
             }
 #pragma unroll
             for (int jj = 0; jj < kInGroup; ++jj)
@@ -451,26 +464,31 @@ __global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
                     acc.w ^= x[jj].w;
                 }
         }
-        store_chunk<NT>(blk + (uint64_t)mi * a.ss, acc, a.len - c * kChunk, a.pad_zero);
+        store_chunk<NTS>(blk + (uint64_t)mi * a.ss, acc, a.len - c * kChunk, a.pad_zero);
     }
 }
 
 // ------------------------------------------------------------------ launchers
-template <int MAXM, bool NT>
+template <int MAXM, int POL>
 static hipError_t enc_dispatch2(const EncodeArgs& a, int grid, hipStream_t s) {
     const bool lds_tabs = a.m * a.k <= (uint32_t)kMaxLdsTabs;
     if (lds_tabs) {
         const size_t lds = (size_t)a.m * a.k * sizeof(gf::PermTab);
-        hipLaunchKernelGGL((rs_encode_kernel<MAXM, true, NT>), dim3(grid), dim3(kThreads), lds, s, a);
+        hipLaunchKernelGGL((rs_encode_kernel<MAXM, true, POL>), dim3(grid), dim3(kThreads), lds, s, a);
     } else {
-        hipLaunchKernelGGL((rs_encode_kernel<MAXM, false, NT>), dim3(grid), dim3(kThreads), 0, s, a);
+        hipLaunchKernelGGL((rs_encode_kernel<MAXM, false, POL>), dim3(grid), dim3(kThreads), 0, s, a);
     }
     return hipGetLastError();
 }
 
 template <int MAXM>
 static hipError_t enc_dispatch(const EncodeArgs& a, int grid, hipStream_t s) {
-    return g_tune.enc_nt ? enc_dispatch2<MAXM, true>(a, grid, s) : enc_dispatch2<MAXM, false>(a, grid, s);
+    switch (g_tune.enc_nt & 3) {
+        case 0: return enc_dispatch2<MAXM, 0>(a, grid, s);
+        case 1: return enc_dispatch2<MAXM, 1>(a, grid, s);
+        case 2: return enc_dispatch2<MAXM, 2>(a, grid, s);
+        default: return enc_dispatch2<MAXM, 3>(a, grid, s);
+    }
 }
 
 hipError_t launch_rs_encode(const EncodeArgs& a, int grid, hipStream_t s) {
@@ -498,30 +516,35 @@ size_t recon_lds_bytes(uint32_t g, uint32_t k, uint32_t maxe, const PlanLayout& 
     return (size_t)g * maxe * k * sizeof(gf::PermTab) + (size_t)g * lay.stride;
 }
 
-template <bool NT>
+template <int POL>
 static hipError_t recon_dispatch(const ReconArgs& a, int grid, hipStream_t s) {
     const size_t lds = recon_lds_bytes(a.g, a.k, a.maxe, a.lay);
-    if (a.maxe <= 1) hipLaunchKernelGGL((rs_reconstruct_kernel<1, NT>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (a.maxe <= 2) hipLaunchKernelGGL((rs_reconstruct_kernel<2, NT>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (a.maxe <= 4) hipLaunchKernelGGL((rs_reconstruct_kernel<4, NT>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (a.maxe <= 8) hipLaunchKernelGGL((rs_reconstruct_kernel<8, NT>), dim3(grid), dim3(kThreads), lds, s, a);
-    else hipLaunchKernelGGL((rs_reconstruct_kernel<16, NT>), dim3(grid), dim3(kThreads), lds, s, a);
+    if (a.maxe <= 1) hipLaunchKernelGGL((rs_reconstruct_kernel<1, POL>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (a.maxe <= 2) hipLaunchKernelGGL((rs_reconstruct_kernel<2, POL>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (a.maxe <= 4) hipLaunchKernelGGL((rs_reconstruct_kernel<4, POL>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (a.maxe <= 8) hipLaunchKernelGGL((rs_reconstruct_kernel<8, POL>), dim3(grid), dim3(kThreads), lds, s, a);
+    else hipLaunchKernelGGL((rs_reconstruct_kernel<16, POL>), dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_rs_reconstruct(const ReconArgs& a, int grid, hipStream_t s) {
-    return g_tune.dec_nt ? recon_dispatch<true>(a, grid, s) : recon_dispatch<false>(a, grid, s);
+    switch (g_tune.dec_nt & 3) {
+        case 0: return recon_dispatch<0>(a, grid, s);
+        case 1: return recon_dispatch<1>(a, grid, s);
+        case 2: return recon_dispatch<2>(a, grid, s);
+        default: return recon_dispatch<3>(a, grid, s);
+    }
 }
 
 hipError_t launch_xor_encode(const XorArgs& a, int grid, hipStream_t s) {
-    if (g_tune.enc_nt) hipLaunchKernelGGL(xor_encode_kernel<true>, dim3(grid), dim3(kThreads), 0, s, a);
-    else hipLaunchKernelGGL(xor_encode_kernel<false>, dim3(grid), dim3(kThreads), 0, s, a);
+    if (g_tune.enc_nt & 3) hipLaunchKernelGGL(xor_encode_kernel<3>, dim3(grid), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL(xor_encode_kernel<0>, dim3(grid), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_xor_reconstruct(const XorArgs& a, int grid, hipStream_t s) {
-    if (g_tune.dec_nt) hipLaunchKernelGGL(xor_reconstruct_kernel<true>, dim3(grid), dim3(kThreads), 0, s, a);
-    else hipLaunchKernelGGL(xor_reconstruct_kernel<false>, dim3(grid), dim3(kThreads), 0, s, a);
+    if (g_tune.dec_nt & 3) hipLaunchKernelGGL(xor_reconstruct_kernel<3>, dim3(grid), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL(xor_reconstruct_kernel<0>, dim3(grid), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }
 
@@ -554,19 +577,19 @@ int occupancy_grid(int device, int which, uint32_t sel, size_t lds) {
     int per = 0;
     const void* fn = nullptr;
     if (which == 0) {
-        if (sel <= 1) fn = (const void*)rs_encode_kernel<1, true, true>;
-        else if (sel <= 2) fn = (const void*)rs_encode_kernel<2, true, true>;
-        else if (sel <= 4) fn = (const void*)rs_encode_kernel<4, true, true>;
-        else if (sel <= 8) fn = (const void*)rs_encode_kernel<8, true, true>;
-        else fn = (const void*)rs_encode_kernel<16, true, true>;
+        if (sel <= 1) fn = (const void*)rs_encode_kernel<1, true, 3>;
+        else if (sel <= 2) fn = (const void*)rs_encode_kernel<2, true, 3>;
+        else if (sel <= 4) fn = (const void*)rs_encode_kernel<4, true, 3>;
+        else if (sel <= 8) fn = (const void*)rs_encode_kernel<8, true, 3>;
+        else fn = (const void*)rs_encode_kernel<16, true, 3>;
     } else if (which == 1) {
-        if (sel <= 1) fn = (const void*)rs_reconstruct_kernel<1, false>;
-        else if (sel <= 2) fn = (const void*)rs_reconstruct_kernel<2, false>;
-        else if (sel <= 4) fn = (const void*)rs_reconstruct_kernel<4, false>;
-        else if (sel <= 8) fn = (const void*)rs_reconstruct_kernel<8, false>;
-        else fn = (const void*)rs_reconstruct_kernel<16, false>;
+        if (sel <= 1) fn = (const void*)rs_reconstruct_kernel<1, 3>;
+        else if (sel <= 2) fn = (const void*)rs_reconstruct_kernel<2, 3>;
+        else if (sel <= 4) fn = (const void*)rs_reconstruct_kernel<4, 3>;
+        else if (sel <= 8) fn = (const void*)rs_reconstruct_kernel<8, 3>;
+        else fn = (const void*)rs_reconstruct_kernel<16, 3>;
     } else {
-        fn = (const void*)xor_encode_kernel<true>;
+        fn = (const void*)xor_encode_kernel<3>;
     }
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kThreads, lds) != hipSuccess || per <= 0)
         per = 4;

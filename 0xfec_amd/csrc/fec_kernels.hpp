@@ -29,10 +29,11 @@ struct EncodeArgs {
     FastDiv div_cps;
     const uint32_t* tabs;      // m * k PermTabs (8 dwords each), device memory
     uint32_t pad_zero;         // tail chunk: full 16-B store, bytes past len zeroed
+    uint32_t rot;              // chunk rotation inside a block (line_rotation())
 };
 
 // Decode plan, one record of `stride` bytes per block (offsets from plan_layout()):
-//   [in_off,   +32)       input shard slots = the first k present shards, in index order
+//   [in_off,   +rup8(k))  input shard slots = the first k present shards, in index order
 //   [out_off,  +maxe)     erased data shard slots (ascending)
 //   [nout_off]            number of erased data shards to rebuild (0: nothing / failed)
 //   [coef_off, +maxe*k)   GF coefficients, row r = output r, column j = input j
@@ -63,6 +64,7 @@ struct ReconArgs {
     uint32_t ntiles;
     FastDiv div_cps;
     uint32_t pad_zero;
+    uint32_t rot;
     uint8_t* out;              // recover: rebuilt shard r of block b at out + b*out_bs + r*ss
     uint64_t out_bs;           //          (nullptr: rebuild in place into the data region)
 };
@@ -79,19 +81,28 @@ struct XorArgs {
     uint32_t k, len, cps, total;
     FastDiv div_cps;
     uint32_t pad_zero;
+    uint32_t rot;
 };
 
 // Kernel-selection knobs. Defaults are the measured best (tools/kbench.py A/Bs them through
 // the internal fec__set_tuning() entry point; results in DESIGN.md).
 struct Tuning {
-    int enc_nt = 1;           // non-temporal loads/stores in encode and XOR kernels
-    int dec_nt = 1;           // non-temporal loads and stores in the reconstruct kernels
+    int enc_nt = 3;           // encode/XOR cache policy: bit 0 non-temporal loads, bit 1 nt stores
+    int dec_nt = 3;           // reconstruct cache policy, same bits
     int grid_mult = 1;        // persistent grids: workgroups = grid_mult * CUs * resident/CU
     int dec_max_rounds = 8;   // bound on item rounds per decode tile (pick_tile_blocks)
     int pad_zero = 1;         // tail chunks: zero-padded full 16-B stores instead of partial
     int items_per_thread = 1; // >0: flat grids = total / (256 * items_per_thread); 0: persistent
     int tiles_per_wg = 1;     // >0: decode grid = ntiles / tiles_per_wg; 0: persistent
+    int rotate = 0;           // rotate chunk order so shard boundaries share a wave (measured: no gain)
 };
+
+// Chunks to rotate for shard stride ss: the chunks after the last 128-byte line boundary of a
+// line-aligned shard, when they fit in the shard's chunk range.
+inline uint32_t line_rotation(uint64_t ss, uint32_t cps) {
+    const uint32_t r = (uint32_t)((ss & 127) >> 4);
+    return r < cps ? r : 0;
+}
 extern Tuning g_tune;
 
 hipError_t launch_rs_encode(const EncodeArgs& a, int grid, hipStream_t s);

@@ -19,9 +19,9 @@ def main():
     ap.add_argument("--m", type=int, default=4)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--enc", default="1:0:1",
+    ap.add_argument("--enc", default="3:0:1,2:0:1,1:0:1,0:0:1",
                     help="encode nt:grid_mult:items_per_thread (grid_mult 0 -> 1 with ipt)")
-    ap.add_argument("--dec", default="0:8:0:1,1:8:0:1",
+    ap.add_argument("--dec", default="3:8:0:1,2:8:0:1",
                     help="decode nt:rounds:grid_mult:tiles_per_wg")
     ap.add_argument("--xor", default="0:1", help="xor grid_mult:items_per_thread")
     args = ap.parse_args()
@@ -52,7 +52,7 @@ def main():
 
     def tune(**kv):
         keys = {"enc_nt": 0, "dec_nt": 1, "grid_mult": 2, "dec_max_rounds": 3, "pad_zero": 4,
-                "items_per_thread": 5, "tiles_per_wg": 6}
+                "items_per_thread": 5, "tiles_per_wg": 6, "rotate": 7}
         for key, val in kv.items():
             fec.lib.fec__set_tuning(codec.handle, keys[key], val)
 
@@ -78,9 +78,11 @@ def main():
     dsplit = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device="cuda")
     psplit = torch.randint(0, 256, (B, m, S), dtype=torch.uint8, device="cuda")
 
-    def enc_split():
-        tune(enc_nt=1, grid_mult=1, items_per_thread=1, pad_zero=1)
-        codec.rs_encode_raw(k, m, L, B, dsplit.data_ptr(), k * S, psplit.data_ptr(), m * S, S, fec.FEC_DEVICE)
+    def enc_split(pol, rot=1):
+        def f():
+            tune(enc_nt=pol, grid_mult=1, items_per_thread=1, pad_zero=1, rotate=rot)
+            codec.rs_encode_raw(k, m, L, B, dsplit.data_ptr(), k * S, psplit.data_ptr(), m * S, S, fec.FEC_DEVICE)
+        return f
 
     def dec_split(nt):
         def f():
@@ -91,23 +93,25 @@ def main():
 
     outb = torch.empty((B, 1, S), dtype=torch.uint8, device="cuda")
 
-    def rec_split():
-        tune(dec_nt=1, dec_max_rounds=8, grid_mult=1, tiles_per_wg=1, pad_zero=1)
-        codec.rs_recover_raw(k, m, L, B, dsplit.data_ptr(), k * S, psplit.data_ptr(), m * S, S,
-                             masks.data_ptr(), outb.data_ptr(), S, 1, None)
+    def rec_split(pol, rot=1):
+        def f():
+            tune(dec_nt=pol, dec_max_rounds=8, grid_mult=1, tiles_per_wg=1, pad_zero=1, rotate=rot)
+            codec.rs_recover_raw(k, m, L, B, dsplit.data_ptr(), k * S, psplit.data_ptr(), m * S, S,
+                                 masks.data_ptr(), outb.data_ptr(), S, 1, None)
+        return f
 
     cases = {}
-    cases["rs_recover split nt1"] = (rec_split, B * (k + 1) * L)
-    cases["rs_encode split"] = (enc_split, B * n * L)
-    cases["rs_reconstruct split nt1"] = (dec_split(1), B * (k + 1) * L)
-    cases["rs_reconstruct split nt0"] = (dec_split(0), B * (k + 1) * L)
-    for spec in args.enc.split(","):
+    for rot in (1, 0):
+        cases["rs_recover split rot%d" % rot] = (rec_split(3, rot), B * (k + 1) * L)
+        cases["rs_encode split rot%d" % rot] = (enc_split(3, rot), B * n * L)
+    cases["rs_reconstruct split pol3"] = (dec_split(3), B * (k + 1) * L)
+    for spec in [x for x in args.enc.split(",") if x]:
         v, g, ipt = [int(x) for x in spec.split(":")]
         cases["rs_encode nt%d g%d ipt%d" % (v, g, ipt)] = (enc(v, g, ipt), B * n * L)
-    for spec in args.dec.split(","):
+    for spec in [x for x in args.dec.split(",") if x]:
         nt, r, g, tpw = [int(x) for x in spec.split(":")]
         cases["rs_reconstruct nt%d r%d g%d tpw%d" % (nt, r, g, tpw)] = (dec(nt, r, g, tpw), B * (k + 1) * L)
-    for spec in args.xor.split(","):
+    for spec in [x for x in args.xor.split(",") if x]:
         g, ipt = [int(x) for x in spec.split(":")]
         cases["xor_encode_k%d g%d ipt%d" % (k, g, ipt)] = (xor(g, ipt), B * (k + 1) * L)
     cases["torch_copy_%dto%d" % (k, m)] = (lambda: cp_dst.copy_(cp_src[:cp_dst.numel()]), 2 * cp_dst.numel())
