@@ -127,14 +127,16 @@ def main():
     dev = torch.device("cuda", local)
     fec = importlib.import_module("0xfec_amd")
 
+    shard = importlib.import_module("0xfec_amd.shard")
     k, m, B = args.k, args.m, args.blocks
     n = k + m
+    g_lo, g_hi = shard.block_range(B * world, rank, world)   # this rank's slice of the global batch
     codec = fec.Codec(local)
     codec.prepare(k, m)
     codec.use_torch_stream()
     stream = torch.cuda.current_stream(dev)
 
-    data, parity, erased, masks, recovered = make_batch(torch, B, k, m, args.seed + 7919 * rank, dev)
+    data, parity, erased, masks, recovered = make_batch(torch, B, k, m, args.seed + g_lo, dev)
     torch.cuda.synchronize()
     dptr, pptr, optr = data.data_ptr(), parity.data_ptr(), recovered.data_ptr()
     dbs, pbs = k * SHARD_STRIDE, m * SHARD_STRIDE
@@ -225,8 +227,7 @@ def main():
     L = SHARD_LEN
     enc_bytes = B * (k + m) * L                  # read k shards, write m shards
     dec_bytes = B * (k + 1) * L                  # read first k present, write 1 erased data shard
-    payload_gib = world * B * k * PAYLOAD / 2**30
-    value = payload_gib / (step_ms / 1000.0)
+    value = shard.aggregate_gibps([B] * world, k, PAYLOAD, step_ms / 1000.0)
     enc_bw = enc_bytes / (enc_ms / 1000.0)
     dec_bw = dec_bytes / (dec_ms / 1000.0)
     dominant = "rs_encode_kernel" if enc_ms >= dec_ms else "rs_plan_kernel+rs_reconstruct_kernel (recover)"
@@ -245,7 +246,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (torch Philox bytes, seed 0x0FEC + 7919*rank)",
+            "data": "synthetic (torch Philox bytes, seed 0x0FEC + first global block of the rank)",
             "config": {"workload": "RS(k=%d,n=%d) encode + random single-data-erasure decode" % (k, n),
                        "blocks_per_gpu": B, "payload_bytes": PAYLOAD, "shard_len": L,
                        "shard_stride": SHARD_STRIDE, "layout": "data [B][k][1216] + parity [B][m][1216] buffers",
