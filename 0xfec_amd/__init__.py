@@ -169,6 +169,23 @@ class Codec:
     def sync(self):
         return _check(lib.fec_sync(self._h), "fec_sync")
 
+    # Kernel-selection knobs (diagnostics and tests; defaults are the measured best). Keys of
+    # the library's internal fec__set_tuning(); the setting is process-wide.
+    TUNING_KEYS = {"enc_nt": 0, "dec_nt": 1, "grid_mult": 2, "dec_max_rounds": 3, "pad_zero": 4,
+                   "items_per_thread": 5, "tiles_per_wg": 6, "rotate": 7, "xcd_swz": 8, "enc_wpc": 9,
+                   "dec_wpc": 10, "enc_fixed": 11, "dec_swz": 12, "gen_wpc": 13, "enc_queue": 14,
+                   "enc_qwpc": 15, "enc_qdepth": 16}
+
+    def set_tuning(self, **knobs):
+        """Set kernel-selection knobs; returns the previous values (pass them back to restore)."""
+        fn = lib.fec__set_tuning
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        fn.restype = ctypes.c_int
+        old = {}
+        for name, val in knobs.items():
+            old[name] = fn(self._h, self.TUNING_KEYS[name], int(val))
+        return old
+
     def prepare(self, k, m):
         return _check(lib.fec_rs_prepare(self._h, k, m), "fec_rs_prepare")
 

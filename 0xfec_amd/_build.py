@@ -36,7 +36,11 @@ def build(force=False, verbose=False):
     if not force and up_to_date():
         return LIB
     srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    # The atomic optimizer turns a single-lane atomicAdd (queue kernels' ticket draw) into a
+    # wave-aggregated one whose result is consumed on the spot, which makes the draw a full HBM
+    # round trip on the critical path; the tickets are consumed a stage later instead.
     cmd = [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
            "-I", os.path.join(os.path.dirname(HERE), "include"), "-o", LIB + ".tmp"] + srcs
     if verbose:
         print(" ".join(cmd))

@@ -45,6 +45,7 @@ struct fec_ctx {
     uint8_t* d_plans = nullptr;
     size_t plans_cap = 0;
     int* d_err = nullptr;    // [0] sticky device-path error, [1] host-path error
+    uint32_t* d_ctr = nullptr;   // ticket counters of the queue kernels (8 x kCtrStride words)
     uint8_t* h_stage = nullptr;
     uint8_t* d_stage = nullptr;
     size_t stage_cap = 0;
@@ -52,6 +53,7 @@ struct fec_ctx {
     int32_t* d_status = nullptr;
     size_t masks_cap = 0;
     int grid_cache[3][6] = {};
+    int ncu = 256;           // compute units of the device
 };
 
 #define HIP_TRY(expr)                      \
@@ -185,8 +187,14 @@ static int rs_encode_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks
             a.tabs = code->d_tabs + (size_t)r0 * k * 8;
             a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
             a.rot = fk::g_tune.rotate ? fk::line_rotation(ss, cps) : 0;
+            a.swz = (uint32_t)fk::g_tune.xcd_swz;
+            if (fk::fixed_encode_applies((uint32_t)k, (uint32_t)mr)) {
+                a.ctr = ctx->d_ctr;
+                HIP_TRY(fk::launch_rs_encode_fixed(a, ctx->ncu, ctx->stream));
+                continue;
+            }
             const size_t lds = (size_t)mr * k * sizeof(gf::PermTab);
-            int grid = grid_for(ctx, 0, (uint32_t)mr, lds <= 65536 ? lds : 0);
+            int grid = grid_for(ctx, 0, (uint32_t)mr, fk::occupancy_lds(fk::g_tune.gen_wpc, lds <= 65536 ? lds : 0));
             grid = flat_grid(grid, a.total);
             if (grid < 1) grid = 1;
             HIP_TRY(fk::launch_rs_encode(a, grid, ctx->stream));
@@ -242,13 +250,14 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         a.div_cps = fk::make_fastdiv(cps);
         a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
         a.rot = fk::g_tune.rotate ? fk::line_rotation(ss, cps) : 0;
+        a.swz = (uint32_t)fk::g_tune.dec_swz;
         a.out = out ? out + b0 * out_bs : nullptr;
         a.out_bs = out_bs;
         int grid;
         if (fk::g_tune.tiles_per_wg > 0)
             grid = (int)((a.ntiles + fk::g_tune.tiles_per_wg - 1) / fk::g_tune.tiles_per_wg);
         else
-            grid = grid_for(ctx, 1, maxe, lds);
+            grid = grid_for(ctx, 1, maxe, fk::occupancy_lds(fk::g_tune.dec_wpc, lds));
         grid = std::max(1, std::min<int>(grid, (int)a.ntiles));
         HIP_TRY(fk::launch_rs_reconstruct(a, grid, ctx->stream));
     }
@@ -274,7 +283,8 @@ static int xor_encode_device(fec_ctx* ctx, int k, size_t len, size_t nblocks, co
         a.div_cps = fk::make_fastdiv(cps);
         a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
         a.rot = fk::g_tune.rotate ? fk::line_rotation(ss, cps) : 0;
-        int grid = grid_for(ctx, 2, 1, 0);
+        a.swz = (uint32_t)fk::g_tune.xcd_swz;
+        int grid = grid_for(ctx, 2, 1, fk::occupancy_lds(fk::g_tune.gen_wpc, 0));
         grid = flat_grid(grid, a.total);
         if (grid < 1) grid = 1;
         HIP_TRY(fk::launch_xor_encode(a, grid, ctx->stream));
@@ -307,7 +317,8 @@ static int xor_reconstruct_device(fec_ctx* ctx, int k, size_t len, size_t nblock
         a.div_cps = fk::make_fastdiv(cps);
         a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
         a.rot = fk::g_tune.rotate ? fk::line_rotation(ss, cps) : 0;
-        int grid = grid_for(ctx, 2, 1, 0);
+        a.swz = (uint32_t)fk::g_tune.dec_swz;
+        int grid = grid_for(ctx, 2, 1, fk::occupancy_lds(fk::g_tune.dec_wpc, 0));
         grid = flat_grid(grid, a.total);
         if (grid < 1) grid = 1;
         HIP_TRY(fk::launch_xor_reconstruct(a, grid, ctx->stream));
@@ -433,12 +444,18 @@ int fec_ctx_create(int device, fec_ctx** out) {
     ctx->device = device;
     if (hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&ctx->d_err, 2 * sizeof(int)) != hipSuccess ||
+        hipMalloc(&ctx->d_ctr, 8 * fk::kCtrStride * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(ctx->d_err, 0, 2 * sizeof(int)) != hipSuccess) {
         (void)hipGetLastError();
         fec_ctx_destroy(ctx);
         return FEC_ERR_HIP;
     }
     ctx->stream = ctx->own;
+    if (hipDeviceGetAttribute(&ctx->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        ctx->ncu <= 0) {
+        (void)hipGetLastError();
+        ctx->ncu = 256;
+    }
     *out = ctx;
     return FEC_OK;
 }
@@ -453,6 +470,7 @@ void fec_ctx_destroy(fec_ctx* ctx) {
     }
     if (ctx->d_plans) (void)hipFree(ctx->d_plans);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
+    if (ctx->d_ctr) (void)hipFree(ctx->d_ctr);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
     if (ctx->d_masks) (void)hipFree(ctx->d_masks);
@@ -478,7 +496,12 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
     int* slot = key == 0 ? &fk::g_tune.enc_nt : key == 1 ? &fk::g_tune.dec_nt
               : key == 2 ? &fk::g_tune.grid_mult : key == 3 ? &fk::g_tune.dec_max_rounds
               : key == 4 ? &fk::g_tune.pad_zero : key == 5 ? &fk::g_tune.items_per_thread
-              : key == 6 ? &fk::g_tune.tiles_per_wg : key == 7 ? &fk::g_tune.rotate : nullptr;
+              : key == 6 ? &fk::g_tune.tiles_per_wg : key == 7 ? &fk::g_tune.rotate
+              : key == 8 ? &fk::g_tune.xcd_swz : key == 9 ? &fk::g_tune.enc_wpc
+              : key == 10 ? &fk::g_tune.dec_wpc : key == 11 ? &fk::g_tune.enc_fixed
+              : key == 12 ? &fk::g_tune.dec_swz : key == 13 ? &fk::g_tune.gen_wpc
+              : key == 14 ? &fk::g_tune.enc_queue : key == 15 ? &fk::g_tune.enc_qwpc
+              : key == 16 ? &fk::g_tune.enc_qdepth : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

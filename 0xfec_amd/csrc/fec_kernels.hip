@@ -16,6 +16,8 @@
 // (tools/kbench.py; DESIGN.md "Kernel tuning").
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "fec_kernels.hpp"
 #include "gf256.h"
 
@@ -53,6 +55,18 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
 // one wave on consecutive instructions, and the line is fetched from HBM once.
 __device__ __forceinline__ uint32_t rotate_chunk(uint32_t c, uint32_t cps, uint32_t rot) {
     return c < rot ? c + (cps - rot) : c - rot;
+}
+
+// Workgroup index in XCD-contiguous order. Dispatch deals workgroups round-robin over the 8
+// XCDs (MI355X_MICROARCH.md, workgroup dispatch); with swz the workgroups one XCD receives take
+// one contiguous eighth of the grid, so each XCD streams its own contiguous address range
+// (speed only: any bijection is correct). Workgroups past the last multiple of 8 keep their index.
+__device__ __forceinline__ uint32_t xcd_order(uint32_t swz) {
+    const uint32_t wg = blockIdx.x, G = gridDim.x;
+    if (!swz) return wg;
+    const uint32_t full = G & ~7u;
+    if (wg >= full) return wg;
+    return (wg & 7u) * (full >> 3) + (wg >> 3);
 }
 
 struct Idx {
@@ -134,15 +148,58 @@ __device__ __forceinline__ void store_chunk(uint8_t* p, const uint4& v, uint32_t
         st_partial(p, v, nb);
 }
 
-// acc ^= c * x for one 16-byte chunk (c given by its PermTab, read from LDS).
-__device__ __forceinline__ void mac(uint4& acc, const Idx (&ix)[4], const gf::PermTab* t) {
-    const uint4 lo = *reinterpret_cast<const uint4*>(t);   // t0lo t0hi t1lo t1hi
-    const uint32_t t2 = t->t2;
-    acc.x ^= gmul(ix[0], lo.x, lo.y, lo.z, lo.w, t2);
-    acc.y ^= gmul(ix[1], lo.x, lo.y, lo.z, lo.w, t2);
-    acc.z ^= gmul(ix[2], lo.x, lo.y, lo.z, lo.w, t2);
-    acc.w ^= gmul(ix[3], lo.x, lo.y, lo.z, lo.w, t2);
+// a ^ b ^ c in one VALU op. gfx950 has no v_xor3_b32; v_bitop3_b32 with truth table 0x96 is
+// the three-input XOR. As inline asm it also pins the accumulation order: left to the compiler,
+// long XOR chains are reassociated into trees that keep every product live at once.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
 }
+
+// The three v_perm products of c * x (x one packed dword, c by its PermTab words).
+struct Prod3 {
+    uint32_t p0, p1, p2;
+};
+__device__ __forceinline__ Prod3 gprod(const Idx& i, const uint4& lo, uint32_t t2) {
+    return {__builtin_amdgcn_perm(lo.y, lo.x, i.a), __builtin_amdgcn_perm(lo.w, lo.z, i.b),
+            __builtin_amdgcn_perm(t2, t2, i.c)};
+}
+
+// acc ^= c_a * x_a ^ c_b * x_b for one 16-byte chunk of two inputs: six v_perm products per
+// dword folded with three 3-input XORs.
+__device__ __forceinline__ void mac2(uint32_t (&acc)[4], const Idx (&ia)[4], const Idx (&ib)[4],
+                                     const gf::PermTab* ta, const gf::PermTab* tb) {
+    const uint4 la = *reinterpret_cast<const uint4*>(ta);
+    const uint4 lb = *reinterpret_cast<const uint4*>(tb);
+    const uint32_t a2 = ta->t2, b2 = tb->t2;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const Prod3 p = gprod(ia[d], la, a2);
+        const Prod3 q = gprod(ib[d], lb, b2);
+        acc[d] = xor3(xor3(xor3(acc[d], p.p0, p.p1), p.p2, q.p0), q.p1, q.p2);
+    }
+}
+
+// acc ^= c * x for one 16-byte chunk of one input.
+__device__ __forceinline__ void mac1(uint32_t (&acc)[4], const Idx (&ia)[4], const gf::PermTab* ta) {
+    const uint4 la = *reinterpret_cast<const uint4*>(ta);
+    const uint32_t a2 = ta->t2;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const Prod3 p = gprod(ia[d], la, a2);
+        acc[d] = xor3(acc[d], p.p0, p.p1) ^ p.p2;
+    }
+}
+
+__device__ __forceinline__ void split4(Idx (&ix)[4], const uint4& x) {
+    ix[0] = split(x.x);
+    ix[1] = split(x.y);
+    ix[2] = split(x.z);
+    ix[3] = split(x.w);
+}
+
+__device__ __forceinline__ uint4 as_uint4(const uint32_t (&v)[4]) { return make_uint4(v[0], v[1], v[2], v[3]); }
 
 // ------------------------------------------------------------------ RS encode
 // One lane = one 16-byte column chunk of one block; all m parities accumulate in VGPRs.
@@ -165,24 +222,33 @@ __global__ __launch_bounds__(kThreads) void rs_encode_kernel(EncodeArgs a) {
     }
     const uint32_t k = a.k, m = a.m;
     const uint32_t stride = gridDim.x * kThreads;
-    for (uint32_t item = blockIdx.x * kThreads + threadIdx.x; item < a.total; item += stride) {
+    for (uint32_t item = xcd_order(a.swz) * kThreads + threadIdx.x; item < a.total; item += stride) {
         const uint32_t b = fdiv(item, a.div_cps);
         const uint32_t c = rotate_chunk(item - b * a.cps, a.cps, a.rot);
         const uint8_t* src = a.in + (uint64_t)b * a.in_bs + (uint64_t)c * kChunk;
-        uint4 acc[MAXM];
+        uint32_t acc[MAXM][4];
 #pragma unroll
-        for (int r = 0; r < MAXM; ++r) acc[r] = make_uint4(0, 0, 0, 0);
+        for (int r = 0; r < MAXM; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0;
         for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
             uint4 x[kInGroup];
 #pragma unroll
             for (int jj = 0; jj < kInGroup; ++jj) x[jj] = ld16<NTL>(src + (uint64_t)min(j0 + jj, k - 1) * a.ss);
 #pragma unroll
-            for (int jj = 0; jj < kInGroup; ++jj) {
-                if (j0 + jj < k) {
-                    const Idx ix[4] = {split(x[jj].x), split(x[jj].y), split(x[jj].z), split(x[jj].w)};
+            for (int jj = 0; jj < kInGroup; jj += 2) {
+                const uint32_t j = j0 + jj;
+                if (j + 1 < k) {
+                    Idx ia[4], ib[4];
+                    split4(ia, x[jj]);
+                    split4(ib, x[jj + 1]);
 #pragma unroll
                     for (int r = 0; r < MAXM; ++r)
-                        if (r < (int)m) mac(acc[r], ix, tabs + r * k + j0 + jj);
+                        if (r < (int)m) mac2(acc[r], ia, ib, tabs + r * k + j, tabs + r * k + j + 1);
+                } else if (j < k) {
+                    Idx ia[4];
+                    split4(ia, x[jj]);
+#pragma unroll
+                    for (int r = 0; r < MAXM; ++r)
+                        if (r < (int)m) mac1(acc[r], ia, tabs + r * k + j);
                 }
             }
         }
@@ -190,7 +256,144 @@ __global__ __launch_bounds__(kThreads) void rs_encode_kernel(EncodeArgs a) {
         const uint32_t nb = a.len - c * kChunk;
 #pragma unroll
         for (int r = 0; r < MAXM; ++r)
-            if (r < (int)m) store_chunk<NTS>(dst + (uint64_t)r * a.ss, acc[r], nb, a.pad_zero);
+            if (r < (int)m) store_chunk<NTS>(dst + (uint64_t)r * a.ss, as_uint4(acc[r]), nb, a.pad_zero);
+    }
+}
+
+// ------------------------------------------------------------------ RS encode, fixed shape
+// The code shapes the reference benchmarks, with K and M compile-time: one lane = one 16-byte
+// column chunk, the K loads issued back to back, inputs folded in pairs (mac2), no runtime
+// guards. Tail chunks are stored whole with the pad bytes zeroed.
+template <int K, int M, int POL>
+struct FixedEncode {
+    static constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
+    const EncodeArgs& a;
+    const gf::PermTab* T;
+
+    __device__ __forceinline__ void load(uint4 (&x)[K], uint32_t it) const {
+        const uint32_t b = fdiv(it, a.div_cps);
+        const uint32_t c = it - b * a.cps;
+        const uint8_t* src = a.in + (uint64_t)b * a.in_bs + (uint64_t)c * kChunk;
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[j] = ld16<NTL>(src + (uint64_t)j * a.ss);
+    }
+
+    __device__ __forceinline__ void compute_store(const uint4 (&x)[K], uint32_t it) const {
+        // opaque zero: keeps the table reads next to their use (hoisted out of a loop they
+        // would hold 5*M*K VGPRs)
+        uint32_t toff = 0;
+        asm volatile("" : "+s"(toff));
+        const gf::PermTab* t = T + toff;
+        uint32_t acc[M][4];
+#pragma unroll
+        for (int r = 0; r < M; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0;
+#pragma unroll
+        for (int j = 0; j < K; j += 2) {
+            Idx ia[4], ib[4];
+            split4(ia, x[j]);
+            if (j + 1 < K) split4(ib, x[j + 1 < K ? j + 1 : j]);
+#pragma unroll
+            for (int r = 0; r < M; ++r) {
+                if (j + 1 < K) mac2(acc[r], ia, ib, t + r * K + j, t + r * K + j + 1);
+                else mac1(acc[r], ia, t + r * K + j);
+            }
+        }
+        const uint32_t b = fdiv(it, a.div_cps);
+        const uint32_t c = it - b * a.cps;
+        uint8_t* dst = a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk;
+        const uint32_t nb = min(a.len - c * kChunk, (uint32_t)kChunk);
+#pragma unroll
+        for (int r = 0; r < M; ++r) st16<NTS>(dst + (uint64_t)r * a.ss, keep_bytes(as_uint4(acc[r]), nb));
+    }
+};
+
+template <int K, int M>
+__device__ __forceinline__ const gf::PermTab* stage_tabs(uint8_t* smem, const uint32_t* tabs) {
+    uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(M * K * 8); i += kThreads) dst[i] = tabs[i];
+    __syncthreads();
+    return reinterpret_cast<const gf::PermTab*>(smem);
+}
+
+// Flat launch: one item per lane, XCD-contiguous workgroup order.
+template <int K, int M, int POL>
+__global__ __launch_bounds__(kThreads) void rs_encode_fixed_kernel(EncodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const FixedEncode<K, M, POL> f{a, stage_tabs<K, M>(smem, a.tabs)};
+    const uint32_t it = xcd_order(a.swz) * kThreads + threadIdx.x;
+    if (it >= a.total) return;
+    uint4 x[K];
+    f.load(x, it);
+    f.compute_store(x, it);
+}
+
+// Persistent ticket-queue launch (the default for the fixed shapes). The items are split into
+// 8 contiguous ranges; the workgroups with blockIdx % 8 == x own range x (the grid is a multiple
+// of 8, so every range has owners: correctness never depends on placement) and draw 256-item
+// chunks of it in order from ticket counter x. Round-robin dispatch puts those workgroups on one
+// XCD, so each XCD streams one compact window of addresses: measured as fast as a flat grid for
+// pure traffic, where a static persistent sweep lets the windows drift apart and loses ~20 %
+// (tools/mix_probe.py persist). Each lane loads its next chunk's K inputs and draws the ticket
+// after it before it computes and stores the current chunk (ping-pong register sets), so two
+// resident workgroups per CU keep HBM busy while the field arithmetic runs.
+template <int K, int M, int POL, int D>
+__global__ __launch_bounds__(kThreads) void rs_encode_queue_kernel(EncodeArgs a) {
+    static_assert(D == 1 || D == 2, "prefetch depth");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    // tk[2..2+D]: the first D+1 tickets (never rewritten); tk[t & 1]: the ticket drawn in stage
+    // t, read after that stage's barrier and rewritten two stages later, after a barrier every
+    // reader has passed
+    __shared__ uint32_t tk[2 + D + 1];
+    uint32_t* ctr = a.ctr + (blockIdx.x & 7u) * kCtrStride;
+    if (threadIdx.x == 0)
+        for (int i = 0; i <= D; ++i) tk[2 + i] = atomicAdd(ctr, 1u);
+    const FixedEncode<K, M, POL> f{a, stage_tabs<K, M>(smem, a.tabs)};   // barrier inside
+    const uint32_t lo = (blockIdx.x & 7u) * a.per_xcd;
+    const uint32_t hi = min(a.total, lo + a.per_xcd);
+    // chunk bases in flight (uniform over the workgroup): q[0] is computed, q[D] is loaded next
+    uint32_t q[D + 1];
+#pragma unroll
+    for (int i = 0; i <= D; ++i) q[i] = lo + tk[2 + i] * kThreads;
+    const uint32_t last = hi - 1;           // loads clamp to the range's last item
+    const uint32_t lane = threadIdx.x;
+    uint4 xs[D + 1][K];
+    // one stage: draw the ticket D+1 chunks ahead, issue the loads of chunk q[D], compute and
+    // store chunk q[0], publish the ticket. The barrier waits for LDS only (HIP's __syncthreads
+    // would also drain vmcnt, i.e. wait for the prefetched loads).
+    auto stage = [&](uint4 (&now)[K], uint4 (&fill)[K], uint32_t slot) {
+        uint32_t drawn = 0;
+        if (lane == 0) drawn = atomicAdd(ctr, 1u);
+        f.load(fill, min(q[D] + lane, last));   // clamped: unconditional, no merge of old values
+        if (q[0] + lane < hi) f.compute_store(now, q[0] + lane);
+        if (lane == 0) tk[slot] = drawn;
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < D; ++i) q[i] = q[i + 1];
+        q[D] = lo + tk[slot] * kThreads;
+    };
+    if (q[0] >= hi) return;
+#pragma unroll
+    for (int i = 0; i < D; ++i) f.load(xs[i], min(q[i] + lane, last));
+    if constexpr (D == 1) {
+        while (q[0] < hi) {
+            stage(xs[0], xs[1], 0);
+            if (q[0] >= hi) break;
+            stage(xs[1], xs[0], 1);
+        }
+    } else {
+        while (q[0] < hi) {
+            stage(xs[0], xs[2], 0);
+            if (q[0] >= hi) break;
+            stage(xs[1], xs[0], 1);
+            if (q[0] >= hi) break;
+            stage(xs[2], xs[1], 0);
+            if (q[0] >= hi) break;
+            stage(xs[0], xs[2], 1);
+            if (q[0] >= hi) break;
+            stage(xs[1], xs[0], 0);
+            if (q[0] >= hi) break;
+            stage(xs[2], xs[1], 1);
+        }
     }
 }
 
@@ -322,7 +525,7 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
     const PlanLayout lay = a.lay;
     gf::PermTab* tabs = reinterpret_cast<gf::PermTab*>(smem);                // G*maxe*k
     uint8_t* plans = smem + (size_t)G * maxe * k * sizeof(gf::PermTab);      // G*stride
-    for (uint32_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    for (uint32_t tile = xcd_order(a.swz); tile < a.ntiles; tile += gridDim.x) {
         const uint32_t b0 = tile * G;
         const uint32_t gt = min(G, a.nblocks - b0);
         __syncthreads();   // previous tile fully consumed
@@ -361,9 +564,9 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
             const gf::PermTab* T = tabs + g * maxe * k;
             uint8_t* dblk = a.data + (uint64_t)(b0 + g) * a.dbs + (uint64_t)c * kChunk;
             const uint8_t* pblk = a.parity + (uint64_t)(b0 + g) * a.pbs + (uint64_t)c * kChunk;
-            uint4 acc[MAXE];
+            uint32_t acc[MAXE][4];
 #pragma unroll
-            for (int r = 0; r < MAXE; ++r) acc[r] = make_uint4(0, 0, 0, 0);
+            for (int r = 0; r < MAXE; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0;
             for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
                 // the 8 input slots of this group, one ds_read_b64
                 const uint2 sl = *reinterpret_cast<const uint2*>(P + lay.in_off + j0);
@@ -376,12 +579,21 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
                     x[jj] = ld16<NTL>(slot < k ? dblk + (uint64_t)slot * a.ss : pblk + (uint64_t)(slot - k) * a.ss);
                 }
 #pragma unroll
-                for (int jj = 0; jj < kInGroup; ++jj) {
-                    if (j0 + jj < k) {
-                        const Idx ix[4] = {split(x[jj].x), split(x[jj].y), split(x[jj].z), split(x[jj].w)};
+                for (int jj = 0; jj < kInGroup; jj += 2) {
+                    const uint32_t j = j0 + jj;
+                    if (j + 1 < k) {
+                        Idx ia[4], ib[4];
+                        split4(ia, x[jj]);
+                        split4(ib, x[jj + 1]);
 #pragma unroll
                         for (int r = 0; r < MAXE; ++r)
-                            if (r < (int)rows) mac(acc[r], ix, T + r * k + j0 + jj);
+                            if (r < (int)rows) mac2(acc[r], ia, ib, T + r * k + j, T + r * k + j + 1);
+                    } else if (j < k) {
+                        Idx ia[4];
+                        split4(ia, x[jj]);
+#pragma unroll
+                        for (int r = 0; r < MAXE; ++r)
+                            if (r < (int)rows) mac1(acc[r], ia, T + r * k + j);
                     }
                 }
             }
@@ -391,8 +603,8 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
 #pragma unroll
             for (int r = 0; r < MAXE; ++r)
                 if (r < (int)nout)
-                    store_chunk<NTS>(oblk ? oblk + (uint64_t)r * a.ss : dblk + (uint64_t)out_idx[r] * a.ss, acc[r],
-                                    nb, a.pad_zero);
+                    store_chunk<NTS>(oblk ? oblk + (uint64_t)r * a.ss : dblk + (uint64_t)out_idx[r] * a.ss,
+                                     as_uint4(acc[r]), nb, a.pad_zero);
         }
     }
 }
@@ -403,7 +615,7 @@ __global__ __launch_bounds__(kThreads) void xor_encode_kernel(XorArgs a) {
     constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     const uint32_t k = a.k;
     const uint32_t stride = gridDim.x * kThreads;
-    for (uint32_t item = blockIdx.x * kThreads + threadIdx.x; item < a.total; item += stride) {
+    for (uint32_t item = xcd_order(a.swz) * kThreads + threadIdx.x; item < a.total; item += stride) {
         const uint32_t b = fdiv(item, a.div_cps);
         const uint32_t c = rotate_chunk(item - b * a.cps, a.cps, a.rot);
         const uint8_t* src = a.in + (uint64_t)b * a.in_bs + (uint64_t)c * kChunk;
@@ -431,7 +643,7 @@ __global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
     const uint32_t k = a.k, n = k + 1;
     const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
     const uint32_t stride = gridDim.x * kThreads;
-    for (uint32_t item = blockIdx.x * kThreads + threadIdx.x; item < a.total; item += stride) {
+    for (uint32_t item = xcd_order(a.swz) * kThreads + threadIdx.x; item < a.total; item += stride) {
         const uint32_t b = fdiv(item, a.div_cps);
         const uint32_t c = rotate_chunk(item - b * a.cps, a.cps, a.rot);
         const uint32_t miss = ~a.masks[b] & all;
@@ -473,10 +685,11 @@ template <int MAXM, int POL>
 static hipError_t enc_dispatch2(const EncodeArgs& a, int grid, hipStream_t s) {
     const bool lds_tabs = a.m * a.k <= (uint32_t)kMaxLdsTabs;
     if (lds_tabs) {
-        const size_t lds = (size_t)a.m * a.k * sizeof(gf::PermTab);
+        const size_t lds = occupancy_lds(g_tune.gen_wpc, (size_t)a.m * a.k * sizeof(gf::PermTab));
         hipLaunchKernelGGL((rs_encode_kernel<MAXM, true, POL>), dim3(grid), dim3(kThreads), lds, s, a);
     } else {
-        hipLaunchKernelGGL((rs_encode_kernel<MAXM, false, POL>), dim3(grid), dim3(kThreads), 0, s, a);
+        const size_t lds = occupancy_lds(g_tune.gen_wpc, 0);
+        hipLaunchKernelGGL((rs_encode_kernel<MAXM, false, POL>), dim3(grid), dim3(kThreads), lds, s, a);
     }
     return hipGetLastError();
 }
@@ -499,6 +712,53 @@ hipError_t launch_rs_encode(const EncodeArgs& a, int grid, hipStream_t s) {
     return enc_dispatch<16>(a, grid, s);   // caller splits m > 16
 }
 
+// (k, m) shapes with a fixed-shape encode instance: the reference's benchmark codes RS(2,3),
+// RS(8,12), RS(16,24). Any other shape runs the generic kernel.
+bool fixed_encode_applies(uint32_t k, uint32_t m) {
+    if (!g_tune.enc_fixed) return false;
+    return (k == 2 && m == 1) || (k == 8 && m == 4) || (k == 16 && m == 8);
+}
+
+template <int K, int M>
+static hipError_t enc_fixed_dispatch(const EncodeArgs& a, int grid, size_t lds, bool queue, hipStream_t s) {
+    if (queue) {
+        if (g_tune.enc_qdepth >= 2 && K <= 8)   // K = 16 at depth 2 exceeds the register file
+            hipLaunchKernelGGL((rs_encode_queue_kernel<K, M, 3, (K <= 8 ? 2 : 1)>), dim3(grid), dim3(kThreads), lds, s, a);
+        else
+            hipLaunchKernelGGL((rs_encode_queue_kernel<K, M, 3, 1>), dim3(grid), dim3(kThreads), lds, s, a);
+    } else {
+        if (g_tune.enc_nt & 1)
+            hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 3>), dim3(grid), dim3(kThreads), lds, s, a);
+        else
+            hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 2>), dim3(grid), dim3(kThreads), lds, s, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_rs_encode_fixed(EncodeArgs a, int ncu, hipStream_t s) {
+    const uint32_t chunks = (a.total + kThreads - 1) / kThreads;
+    if (chunks == 0) return hipSuccess;
+    const bool queue = g_tune.enc_queue && a.ctr != nullptr;
+    int grid = (int)chunks;
+    int wpc = g_tune.enc_wpc;
+    if (queue) {
+        wpc = g_tune.enc_qwpc > 0 ? g_tune.enc_qwpc : 2;
+        grid = ncu * wpc;
+        // no more owners per range than the range has chunks; a multiple of 8 (every range owned)
+        const int per_range = (int)((chunks + 7) / 8);
+        grid = std::min(grid / 8, per_range) * 8;
+        if (grid < 8) grid = 8;
+        a.per_xcd = ((a.total + 7) / 8 + kThreads - 1) / kThreads * kThreads;
+        const hipError_t e = hipMemsetAsync(a.ctr, 0, 8 * kCtrStride * sizeof(uint32_t), s);
+        if (e != hipSuccess) return e;
+    }
+    const size_t lds = occupancy_lds(wpc, (size_t)a.m * a.k * sizeof(gf::PermTab));
+    if (a.k == 2 && a.m == 1) return enc_fixed_dispatch<2, 1>(a, grid, lds, queue, s);
+    if (a.k == 8 && a.m == 4) return enc_fixed_dispatch<8, 4>(a, grid, lds, queue, s);
+    if (a.k == 16 && a.m == 8) return enc_fixed_dispatch<16, 8>(a, grid, lds, queue, s);
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_rs_plan(const PlanArgs& a, hipStream_t s) {
     const int grid = (int)((a.nblocks + kPlanThreads - 1) / kPlanThreads);
     if (grid == 0) return hipSuccess;
@@ -518,7 +778,7 @@ size_t recon_lds_bytes(uint32_t g, uint32_t k, uint32_t maxe, const PlanLayout& 
 
 template <int POL>
 static hipError_t recon_dispatch(const ReconArgs& a, int grid, hipStream_t s) {
-    const size_t lds = recon_lds_bytes(a.g, a.k, a.maxe, a.lay);
+    const size_t lds = occupancy_lds(g_tune.dec_wpc, recon_lds_bytes(a.g, a.k, a.maxe, a.lay));
     if (a.maxe <= 1) hipLaunchKernelGGL((rs_reconstruct_kernel<1, POL>), dim3(grid), dim3(kThreads), lds, s, a);
     else if (a.maxe <= 2) hipLaunchKernelGGL((rs_reconstruct_kernel<2, POL>), dim3(grid), dim3(kThreads), lds, s, a);
     else if (a.maxe <= 4) hipLaunchKernelGGL((rs_reconstruct_kernel<4, POL>), dim3(grid), dim3(kThreads), lds, s, a);
@@ -537,14 +797,16 @@ hipError_t launch_rs_reconstruct(const ReconArgs& a, int grid, hipStream_t s) {
 }
 
 hipError_t launch_xor_encode(const XorArgs& a, int grid, hipStream_t s) {
-    if (g_tune.enc_nt & 3) hipLaunchKernelGGL(xor_encode_kernel<3>, dim3(grid), dim3(kThreads), 0, s, a);
-    else hipLaunchKernelGGL(xor_encode_kernel<0>, dim3(grid), dim3(kThreads), 0, s, a);
+    const size_t lds = occupancy_lds(g_tune.gen_wpc, 0);
+    if (g_tune.enc_nt & 3) hipLaunchKernelGGL(xor_encode_kernel<3>, dim3(grid), dim3(kThreads), lds, s, a);
+    else hipLaunchKernelGGL(xor_encode_kernel<0>, dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_xor_reconstruct(const XorArgs& a, int grid, hipStream_t s) {
-    if (g_tune.dec_nt & 3) hipLaunchKernelGGL(xor_reconstruct_kernel<3>, dim3(grid), dim3(kThreads), 0, s, a);
-    else hipLaunchKernelGGL(xor_reconstruct_kernel<0>, dim3(grid), dim3(kThreads), 0, s, a);
+    const size_t lds = occupancy_lds(g_tune.dec_wpc, 0);
+    if (g_tune.dec_nt & 3) hipLaunchKernelGGL(xor_reconstruct_kernel<3>, dim3(grid), dim3(kThreads), lds, s, a);
+    else hipLaunchKernelGGL(xor_reconstruct_kernel<0>, dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 

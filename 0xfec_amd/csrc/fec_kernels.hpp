@@ -30,7 +30,12 @@ struct EncodeArgs {
     const uint32_t* tabs;      // m * k PermTabs (8 dwords each), device memory
     uint32_t pad_zero;         // tail chunk: full 16-B store, bytes past len zeroed
     uint32_t rot;              // chunk rotation inside a block (line_rotation())
+    uint32_t swz;              // XCD-contiguous workgroup order (xcd_order())
+    uint32_t* ctr;             // queue kernel: 8 zeroed ticket counters, kCtrStride words apart
+    uint32_t per_xcd;          // queue kernel: items per XCD range
 };
+
+constexpr int kCtrStride = 32;      // one 128-byte line per ticket counter
 
 // Decode plan, one record of `stride` bytes per block (offsets from plan_layout()):
 //   [in_off,   +rup8(k))  input shard slots = the first k present shards, in index order
@@ -67,6 +72,7 @@ struct ReconArgs {
     uint32_t rot;
     uint8_t* out;              // recover: rebuilt shard r of block b at out + b*out_bs + r*ss
     uint64_t out_bs;           //          (nullptr: rebuild in place into the data region)
+    uint32_t swz;
 };
 
 struct XorArgs {
@@ -82,6 +88,7 @@ struct XorArgs {
     FastDiv div_cps;
     uint32_t pad_zero;
     uint32_t rot;
+    uint32_t swz;
 };
 
 // Kernel-selection knobs. Defaults are the measured best (tools/kbench.py A/Bs them through
@@ -95,7 +102,26 @@ struct Tuning {
     int items_per_thread = 1; // >0: flat grids = total / (256 * items_per_thread); 0: persistent
     int tiles_per_wg = 1;     // >0: decode grid = ntiles / tiles_per_wg; 0: persistent
     int rotate = 0;           // rotate chunk order so shard boundaries share a wave (measured: no gain)
+    int xcd_swz = 1;          // encode / XOR: workgroups of one XCD take one contiguous range of the grid
+    int dec_swz = 0;          // same for reconstruct
+    int enc_wpc = 3;          // resident workgroups per CU, fixed-shape encode (0: as many as fit)
+    int gen_wpc = 0;          // same for the generic encode and XOR encode
+    int dec_wpc = 0;          // same for reconstruct
+    int enc_fixed = 1;        // compile-time-shape encode for RS(2,3), RS(8,12), RS(16,24)
+    int enc_queue = 1;        // ... as the persistent ticket-queue kernel (0: flat grid)
+    int enc_qwpc = 2;         // resident workgroups per CU of the queue kernel
+    int enc_qdepth = 1;       // chunks the queue kernel loads ahead of the one it computes
 };
+
+// Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):
+// halfway between 160K/(wpc+1) and 160K/wpc, never below what the kernel itself needs.
+inline size_t occupancy_lds(int wpc, size_t own) {
+    if (wpc <= 0) return own;
+    const size_t cu = 160u * 1024u;
+    size_t pad = (cu / (size_t)wpc + cu / (size_t)(wpc + 1)) / 2;
+    pad &= ~(size_t)255;
+    return own > pad ? own : pad;
+}
 
 // Chunks to rotate for shard stride ss: the chunks after the last 128-byte line boundary of a
 // line-aligned shard, when they fit in the shard's chunk range.
@@ -106,6 +132,9 @@ inline uint32_t line_rotation(uint64_t ss, uint32_t cps) {
 extern Tuning g_tune;
 
 hipError_t launch_rs_encode(const EncodeArgs& a, int grid, hipStream_t s);
+// Fixed-shape encode (flat grid, one item per lane) for the shapes it is instantiated for.
+bool fixed_encode_applies(uint32_t k, uint32_t m);
+hipError_t launch_rs_encode_fixed(EncodeArgs a, int ncu, hipStream_t s);
 hipError_t launch_rs_plan(const PlanArgs& a, hipStream_t s);
 hipError_t launch_rs_reconstruct(const ReconArgs& a, int grid, hipStream_t s);
 hipError_t launch_xor_encode(const XorArgs& a, int grid, hipStream_t s);

@@ -33,6 +33,30 @@ PAYLOAD = 1200
 SHARD_LEN = PAYLOAD + 2          # + big-endian uint16 length trailer
 SHARD_STRIDE = 1216              # 16-byte aligned device slot per shard
 HBM_PEAK = 8.0e12                # MI355X HBM3E spec, bytes/s (MI355X_MICROARCH.md)
+# rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of this bench (separate passes, tools/pmc_traffic.py,
+# gfx950 FETCH_SIZE x2 correction): HBM bytes per launch of each codec kernel
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "pmc_traffic_v5.json")
+
+
+def encode_kernel_name(k, m):
+    """The kernel fec_rs_encode_batch runs for (k, m) at the library's default tuning
+    (fec_kernels.hpp Tuning: fixed shapes run the ticket-queue kernel)."""
+    if (k, m) in ((2, 1), (8, 4), (16, 8)):
+        return "rs_encode_queue_kernel<%d, %d" % (k, m)
+    return "rs_encode_kernel<"
+
+
+def committed_traffic(kernel_prefix):
+    """HBM bytes per launch of the kernel from the committed PMC profile, or None."""
+    try:
+        with open(TRAFFIC_JSON) as fh:
+            prof = json.load(fh)
+    except (OSError, ValueError):
+        return None, None
+    for name, rec in prof.items():
+        if kernel_prefix in name and rec.get("traffic_bytes"):
+            return rec["traffic_bytes"], os.path.relpath(TRAFFIC_JSON, ROOT)
+    return None, None
 
 
 def parse():
@@ -230,8 +254,13 @@ def main():
     value = shard.aggregate_gibps([B] * world, k, PAYLOAD, step_ms / 1000.0)
     enc_bw = enc_bytes / (enc_ms / 1000.0)
     dec_bw = dec_bytes / (dec_ms / 1000.0)
-    dominant = "rs_encode_kernel" if enc_ms >= dec_ms else "rs_plan_kernel+rs_reconstruct_kernel (recover)"
-    dom_bw, dom_bytes = (enc_bw, enc_bytes) if enc_ms >= dec_ms else (dec_bw, dec_bytes)
+    enc_kernel = encode_kernel_name(k, m)
+    if enc_ms >= dec_ms:
+        dominant, dom_bw, dom_bytes = enc_kernel + ">", enc_bw, enc_bytes
+        traffic, traffic_src = committed_traffic(enc_kernel)
+    else:
+        dominant, dom_bw, dom_bytes = "rs_plan_kernel+rs_reconstruct_kernel (recover)", dec_bw, dec_bytes
+        traffic, traffic_src = committed_traffic("rs_reconstruct_kernel")
 
     if rank == 0:
         out = {
@@ -252,7 +281,9 @@ def main():
                        "shard_stride": SHARD_STRIDE, "layout": "data [B][k][1216] + parity [B][m][1216] buffers",
                        "parallelism": "independent block ranges per GPU"},
             "roofline": {"bound": "hbm", "achieved": round(dom_bw / 1e9, 1), "peak": HBM_PEAK / 1e9,
-                         "unit": "GB/s", "frac": round(dom_bw / HBM_PEAK, 4), "traffic": None,
+                         "unit": "GB/s", "frac": round(dom_bw / HBM_PEAK, 4),
+                         "traffic": None if traffic is None else round(traffic / 1e9, 3),
+                         "traffic_unit": "GB per launch", "traffic_source": traffic_src,
                          "kernel": dominant, "algorithmic_bytes_per_launch": dom_bytes},
             "kernels": {
                 "encode": {"ms": round(enc_ms, 4), "GB/s": round(enc_bw / 1e9, 1), "bytes": enc_bytes,

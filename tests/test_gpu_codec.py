@@ -284,3 +284,40 @@ def test_rs_recover_out_of_place(codec, oracle, torch, fec, k, m, slots):
         for r, i in enumerate(miss):
             assert np.array_equal(got[b, r, :L], sh[b, i, :L])
     assert saw_over == over
+
+
+# Every RS encode kernel form (fixed-shape flat grid, ticket-queue at prefetch depth 1 and 2,
+# generic runtime-shape kernel) against the oracle, at batch sizes that leave the 8 queue
+# ranges empty, partial and ragged (B * ceil(L/16) items vs 8 ranges of 256-item chunks).
+ENC_VARIANTS = {
+    "generic": dict(enc_fixed=0),
+    "fixed_flat": dict(enc_fixed=1, enc_queue=0, enc_wpc=3),
+    "queue_d1": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=1),
+    "queue_d2": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=2),
+    "queue_d1_1wg": dict(enc_fixed=1, enc_queue=1, enc_qwpc=1, enc_qdepth=1),
+}
+
+
+@pytest.mark.parametrize("variant", sorted(ENC_VARIANTS))
+@pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8)])
+@pytest.mark.parametrize("B,L", [(1, 1), (3, 17), (37, 1202), (1000, 1202), (4099, 1436), (20000, 33)])
+def test_rs_encode_kernel_variants_match_oracle(codec, oracle, torch, variant, k, m, B, L):
+    rng = np.random.default_rng(B * 31 + L * 7 + k)
+    n = k + m
+    S = (L + 15) // 16 * 16
+    data = rng.integers(0, 256, (B, k, S), dtype=np.uint8)
+    data[:, :, L:] = 0
+    ref = np.zeros((B, n, S), dtype=np.uint8)
+    ref[:, :k] = data
+    oracle.rs_encode(k, m, ref)
+    d = torch.from_numpy(data).cuda()
+    p = torch.full((B, m, S), 0xA5, dtype=torch.uint8, device="cuda")
+    old = codec.set_tuning(**ENC_VARIANTS[variant])
+    try:
+        codec.rs_encode_split(k, m, d, p, shard_len=L)
+        codec.sync()
+    finally:
+        codec.set_tuning(**old)
+    got = p.cpu().numpy()
+    assert np.array_equal(got[:, :, :L], ref[:, k:, :L])
+    assert not got[:, :, L:].any()               # pad to the 16-byte boundary written as zeros

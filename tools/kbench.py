@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--dec", default="3:8:0:1,2:8:0:1",
                     help="decode nt:rounds:grid_mult:tiles_per_wg")
     ap.add_argument("--xor", default="0:1", help="xor grid_mult:items_per_thread")
+    ap.add_argument("--occ", default="",
+                    help="swz:enc_wpc:dec_wpc triples; when given, only the split-layout encode and "
+                         "recover (the bench.py step) are timed, once per triple")
     args = ap.parse_args()
     import torch
     fec = importlib.import_module("0xfec_amd")
@@ -52,7 +55,9 @@ def main():
 
     def tune(**kv):
         keys = {"enc_nt": 0, "dec_nt": 1, "grid_mult": 2, "dec_max_rounds": 3, "pad_zero": 4,
-                "items_per_thread": 5, "tiles_per_wg": 6, "rotate": 7}
+                "items_per_thread": 5, "tiles_per_wg": 6, "rotate": 7, "xcd_swz": 8, "enc_wpc": 9,
+                "dec_wpc": 10, "enc_fixed": 11, "dec_swz": 12, "gen_wpc": 13,
+                "enc_queue": 14, "enc_qwpc": 15, "enc_qdepth": 16}
         for key, val in kv.items():
             fec.lib.fec__set_tuning(codec.handle, keys[key], val)
 
@@ -101,21 +106,53 @@ def main():
         return f
 
     cases = {}
-    for rot in (1, 0):
+    if args.occ:
+        # spec = swz:enc_wpc:dec_swz:dec_wpc:enc_fixed[:queue_wpc[:depth]]  (queue_wpc 0: flat grid)
+        for spec in args.occ.split(","):
+            v = [int(x) for x in spec.split(":")] + [0, 1]
+            swz, ew, dsw, dw, fx, qw, qd = v[:7]
+
+            def occ(fn, swz=swz, ew=ew, dsw=dsw, dw=dw, fx=fx, qw=qw, qd=qd):
+                def f():
+                    tune(xcd_swz=swz, enc_wpc=ew, dec_swz=dsw, dec_wpc=dw, enc_fixed=fx,
+                         enc_queue=1 if qw else 0, enc_qwpc=max(qw, 1), enc_qdepth=qd)
+                    fn()
+                return f
+            cases["rs_encode split fixed%d swz%d wpc%d queue%d d%d" % (fx, swz, ew, qw, qd)] = (
+                occ(enc_split(3, 0)), B * n * L)
+            if not qw:
+                cases["rs_recover split swz%d wpc%d" % (dsw, dw)] = (occ(rec_split(3, 0)), B * (k + 1) * L)
+    for rot in (1, 0) if not args.occ else ():
         cases["rs_recover split rot%d" % rot] = (rec_split(3, rot), B * (k + 1) * L)
         cases["rs_encode split rot%d" % rot] = (enc_split(3, rot), B * n * L)
-    cases["rs_reconstruct split pol3"] = (dec_split(3), B * (k + 1) * L)
-    for spec in [x for x in args.enc.split(",") if x]:
+    if not args.occ:
+        cases["rs_reconstruct split pol3"] = (dec_split(3), B * (k + 1) * L)
+    for spec in [x for x in args.enc.split(",") if x and not args.occ]:
         v, g, ipt = [int(x) for x in spec.split(":")]
         cases["rs_encode nt%d g%d ipt%d" % (v, g, ipt)] = (enc(v, g, ipt), B * n * L)
-    for spec in [x for x in args.dec.split(",") if x]:
+    for spec in [x for x in args.dec.split(",") if x and not args.occ]:
         nt, r, g, tpw = [int(x) for x in spec.split(":")]
         cases["rs_reconstruct nt%d r%d g%d tpw%d" % (nt, r, g, tpw)] = (dec(nt, r, g, tpw), B * (k + 1) * L)
-    for spec in [x for x in args.xor.split(",") if x]:
+    for spec in [x for x in args.xor.split(",") if x and not args.occ]:
         g, ipt = [int(x) for x in spec.split(":")]
         cases["xor_encode_k%d g%d ipt%d" % (k, g, ipt)] = (xor(g, ipt), B * (k + 1) * L)
     cases["torch_copy_%dto%d" % (k, m)] = (lambda: cp_dst.copy_(cp_src[:cp_dst.numel()]), 2 * cp_dst.numel())
     cases["torch_sum_read"] = (lambda: rd.sum(), rd.numel() * 4)
+    if args.occ:
+        # the fixed-shape encode must equal the generic one byte for byte
+        tune(enc_fixed=0, enc_queue=0)
+        enc_split(3, 0)()
+        torch.cuda.synchronize()
+        ref = psplit.clone()
+        psplit.zero_()
+        for q, d in ((0, 1), (1, 1), (1, 2)):
+            psplit.zero_()
+            tune(enc_fixed=1, enc_queue=q, enc_qwpc=2, enc_qdepth=d)
+            enc_split(3, 0)()
+            torch.cuda.synchronize()
+            print("fixed encode (queue=%d depth=%d) == generic encode:" % (q, d),
+                  bool(torch.equal(ref[:, :, :L], psplit[:, :, :L])), flush=True)
+        del ref
     res = {name: [] for name in cases}
     for _ in range(args.rounds):
         for name, (fn, nbytes) in cases.items():
