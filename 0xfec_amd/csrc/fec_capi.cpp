@@ -45,7 +45,7 @@ struct fec_ctx {
     uint8_t* d_plans = nullptr;
     size_t plans_cap = 0;
     int* d_err = nullptr;    // [0] sticky device-path error, [1] host-path error
-    uint32_t* d_ctr = nullptr;   // ticket counters of the queue kernels (8 x kCtrStride words)
+    uint32_t* d_ctr = nullptr;   // ticket counters of the queue kernels (fk::kCtrWords words)
     uint8_t* h_stage = nullptr;
     uint8_t* d_stage = nullptr;
     size_t stage_cap = 0;
@@ -444,7 +444,8 @@ int fec_ctx_create(int device, fec_ctx** out) {
     ctx->device = device;
     if (hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&ctx->d_err, 2 * sizeof(int)) != hipSuccess ||
-        hipMalloc(&ctx->d_ctr, 8 * fk::kCtrStride * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&ctx->d_ctr, fk::kCtrWords * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(ctx->d_ctr, 0, fk::kCtrWords * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(ctx->d_err, 0, 2 * sizeof(int)) != hipSuccess) {
         (void)hipGetLastError();
         fec_ctx_destroy(ctx);

@@ -232,7 +232,8 @@ __global__ __launch_bounds__(kThreads) void rs_encode_kernel(EncodeArgs a) {
         for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
             uint4 x[kInGroup];
 #pragma unroll
-            for (int jj = 0; jj < kInGroup; ++jj) x[jj] = ld16<NTL>(src + (uint64_t)min(j0 + jj, k - 1) * a.ss);
+            for (int jj = 0; jj < kInGroup; ++jj)   // uniform predicate: no loads past shard k-1
+                x[jj] = j0 + jj < k ? ld16<NTL>(src + (uint64_t)(j0 + jj) * a.ss) : make_uint4(0, 0, 0, 0);
 #pragma unroll
             for (int jj = 0; jj < kInGroup; jj += 2) {
                 const uint32_t j = j0 + jj;
@@ -371,48 +372,74 @@ __global__ __launch_bounds__(kThreads) void rs_encode_queue_kernel(EncodeArgs a)
         for (int i = 0; i < D; ++i) q[i] = q[i + 1];
         q[D] = lo + tk[slot] * kThreads;
     };
-    if (q[0] >= hi) return;
+    if (q[0] < hi) {
 #pragma unroll
-    for (int i = 0; i < D; ++i) f.load(xs[i], min(q[i] + lane, last));
-    if constexpr (D == 1) {
-        while (q[0] < hi) {
-            stage(xs[0], xs[1], 0);
-            if (q[0] >= hi) break;
-            stage(xs[1], xs[0], 1);
+        for (int i = 0; i < D; ++i) f.load(xs[i], min(q[i] + lane, last));
+        if constexpr (D == 1) {
+            while (q[0] < hi) {
+                stage(xs[0], xs[1], 0);
+                if (q[0] >= hi) break;
+                stage(xs[1], xs[0], 1);
+            }
+        } else {
+            while (q[0] < hi) {
+                stage(xs[0], xs[2], 0);
+                if (q[0] >= hi) break;
+                stage(xs[1], xs[0], 1);
+                if (q[0] >= hi) break;
+                stage(xs[2], xs[1], 0);
+                if (q[0] >= hi) break;
+                stage(xs[0], xs[2], 1);
+                if (q[0] >= hi) break;
+                stage(xs[1], xs[0], 0);
+                if (q[0] >= hi) break;
+                stage(xs[2], xs[1], 1);
+            }
         }
-    } else {
-        while (q[0] < hi) {
-            stage(xs[0], xs[2], 0);
-            if (q[0] >= hi) break;
-            stage(xs[1], xs[0], 1);
-            if (q[0] >= hi) break;
-            stage(xs[2], xs[1], 0);
-            if (q[0] >= hi) break;
-            stage(xs[0], xs[2], 1);
-            if (q[0] >= hi) break;
-            stage(xs[1], xs[0], 0);
-            if (q[0] >= hi) break;
-            stage(xs[2], xs[1], 1);
+    }
+    // The last workgroup to finish rewinds the counters for the next launch on this stream
+    // (every workgroup's draws precede its arrival, released by the fence).
+    if (threadIdx.x == 0) {
+        __threadfence();
+        uint32_t* done = a.ctr + 8 * kCtrStride;
+        if (atomicAdd(done, 1u) == gridDim.x - 1) {
+            for (int x = 0; x < 8; ++x) atomicExch(a.ctr + x * kCtrStride, 0u);
+            atomicExch(done, 0u);
         }
     }
 }
 
 // ------------------------------------------------------------------ RS reconstruct plan
 // One thread per block, one wave per workgroup. From the present mask: E = erased data
-// shards (e of them), R = first e present parity shards; the first k present shards are
-// then exactly {present data} + R. Solve A[R][E] (e x e) and express each erased shard over
-// those k inputs. Each lane assembles its record in LDS (byte writes), then the wave copies
-// its 64 consecutive records to HBM with 16-byte stores.
+// shards (e of them); the inputs are the first k present shards in index order (as in
+// klauspost ReconstructData). One erasure: a single parity row solves it. Two or more: the
+// coefficients come from Lagrange interpolation over the shard indices (below). Each lane
+// assembles its record in LDS (byte writes), then the wave copies its 64 consecutive records
+// to HBM with 16-byte stores.
 constexpr int kPlanThreads = 64;
 
-template <int MAXE>
+// LDS of one plan workgroup: exp/log tables, the parity rows, the records.
+struct PlanLds {
+    size_t prows, recs, total;
+};
+__host__ __device__ inline PlanLds plan_lds(uint32_t m, uint32_t k, uint32_t stride) {
+    PlanLds l;
+    l.prows = 768;
+    l.recs = (l.prows + m * k + 15) & ~(size_t)15;
+    l.total = l.recs + (size_t)kPlanThreads * stride;
+    return l;
+}
+
 __global__ __launch_bounds__(kPlanThreads) void rs_plan_kernel(PlanArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const PlanLds L = plan_lds(a.m, a.k, a.lay.stride);
     uint8_t* s_exp = smem;                 // 512
     uint8_t* s_log = smem + 512;           // 256
-    uint8_t* recs = smem + 768;            // kPlanThreads * stride
+    uint8_t* s_prows = smem + L.prows;     // m x k
+    uint8_t* recs = smem + L.recs;         // kPlanThreads * stride
     for (int i = threadIdx.x; i < 512; i += kPlanThreads) s_exp[i] = gf::kTables.exp[i];
     for (int i = threadIdx.x; i < 256; i += kPlanThreads) s_log[i] = gf::kTables.log[i];
+    for (uint32_t i = threadIdx.x; i < a.m * a.k; i += kPlanThreads) s_prows[i] = a.prows[i];
     __syncthreads();
     auto mul = [&](uint32_t x, uint32_t y) -> uint32_t {
         return (x && y) ? s_exp[s_log[x] + s_log[y]] : 0u;
@@ -442,7 +469,7 @@ __global__ __launch_bounds__(kPlanThreads) void rs_plan_kernel(PlanArgs a) {
             // one erasure: x_E = inv(A[R0][E0]) * (p_R0 ^ sum_j A[R0][j] x_j)
             const uint32_t E0 = __ffs(~mask & kmask) - 1;
             const uint32_t R0 = __ffs(mask >> k) - 1;
-            const uint8_t* row = a.prows + R0 * k;
+            const uint8_t* row = s_prows + R0 * k;
             const uint32_t inv = s_exp[255 - s_log[row[E0]]];
             for (uint32_t j = 0, pos = 0; j < k; ++j) {
                 if (j == E0) continue;
@@ -455,51 +482,39 @@ __global__ __launch_bounds__(kPlanThreads) void rs_plan_kernel(PlanArgs a) {
             P[lay.out_off] = (uint8_t)E0;
             P[lay.nout_off] = 1;
         } else {
-            uint8_t E[MAXE], R[MAXE];
-            uint32_t ne = 0, nr = 0;
-            for (uint32_t i = 0; i < k; ++i)
-                if (!((mask >> i) & 1u)) E[ne++] = (uint8_t)i;
-            for (uint32_t p = 0; p < m && nr < e; ++p)
-                if ((mask >> (k + p)) & 1u) R[nr++] = (uint8_t)p;
-            // Gauss-Jordan on [A | I], A[t][i] = prows[R[t]][E[i]]
-            uint8_t A[MAXE][2 * MAXE];
-            for (uint32_t t = 0; t < e; ++t)
-                for (uint32_t i = 0; i < 2 * e; ++i)
-                    A[t][i] = i < e ? a.prows[R[t] * k + E[i]] : (uint8_t)(i - e == t);
-            for (uint32_t col = 0; col < e; ++col) {
-                uint32_t piv = col;
-                while (piv < e && A[piv][col] == 0) ++piv;
-                if (piv != col)
-                    for (uint32_t i = 0; i < 2 * e; ++i) {
-                        const uint8_t tmp = A[piv][i];
-                        A[piv][i] = A[col][i];
-                        A[col][i] = tmp;
-                    }
-                const uint32_t inv = s_exp[255 - s_log[A[col][col]]];
-                for (uint32_t i = 0; i < 2 * e; ++i) A[col][i] = (uint8_t)mul(inv, A[col][i]);
-                for (uint32_t r = 0; r < e; ++r) {
-                    if (r == col) continue;
-                    const uint32_t f = A[r][col];
-                    if (!f) continue;
-                    for (uint32_t i = 0; i < 2 * e; ++i) A[r][i] ^= (uint8_t)mul(f, A[col][i]);
-                }
-            }
+            // e >= 2, by Lagrange interpolation instead of inverting the e x e system. The
+            // systematic matrix is M = V inv(V_top) with V[r][c] = r^c (klauspost buildMatrix),
+            // so every shard is y_r = p(r) for one polynomial p of degree < k, and an erased
+            // data shard is x_i = p(i) = sum over the first k present shards s of
+            //   y_s * prod_{t != s} (i ^ t) / (s ^ t)
+            // (nodes are the shard indices as field elements, all distinct). This is the same
+            // unique solution ReconstructData computes; in the log domain it is sums of table
+            // lookups with no serial dependence: k^2 + 3ek lookups per block.
+            uint8_t* S = P + lay.in_off;
+            uint8_t* C = P + lay.coef_off;
             uint32_t pos = 0;
-            for (uint32_t j = 0; j < k; ++j) {
-                if (!((mask >> j) & 1u)) continue;
-                P[lay.in_off + pos] = (uint8_t)j;
-                for (uint32_t i = 0; i < e; ++i) {
-                    uint32_t c = 0;
-                    for (uint32_t t = 0; t < e; ++t) c ^= mul(A[i][e + t], a.prows[R[t] * k + j]);
-                    P[lay.coef_off + i * k + pos] = (uint8_t)c;
+            for (uint32_t idx = 0; idx < n && pos < k; ++idx)
+                if ((mask >> idx) & 1u) S[pos++] = (uint8_t)idx;
+            for (uint32_t i = 0, r = 0; i < k; ++i)
+                if (!((mask >> i) & 1u)) P[lay.out_off + r++] = (uint8_t)i;
+            // D_p = sum_{q != p} log(s_p ^ s_q) mod 255, kept in row 0 of the coefficients
+            for (uint32_t p = 0; p < k; ++p) {
+                const uint32_t sp = S[p];
+                uint32_t d = 0;
+                for (uint32_t q = 0; q < k; ++q)
+                    if (q != p) d += s_log[sp ^ S[q]];
+                C[p] = (uint8_t)(d % 255u);
+            }
+            // rows high to low: row 0 overwrites each D_p right after reading it
+            for (uint32_t r = e; r-- > 0;) {
+                const uint32_t i = P[lay.out_off + r];
+                uint32_t nsum = 0;
+                for (uint32_t q = 0; q < k; ++q) nsum += s_log[i ^ S[q]];
+                for (uint32_t p = 0; p < k; ++p) {
+                    const uint32_t v = nsum + 2u * 255u - s_log[i ^ S[p]] - C[p];
+                    C[r * k + p] = s_exp[v % 255u];
                 }
-                ++pos;
             }
-            for (uint32_t t = 0; t < e; ++t, ++pos) {
-                P[lay.in_off + pos] = (uint8_t)(k + R[t]);
-                for (uint32_t i = 0; i < e; ++i) P[lay.coef_off + i * k + pos] = A[i][e + t];
-            }
-            for (uint32_t i = 0; i < e; ++i) P[lay.out_off + i] = E[i];
             P[lay.nout_off] = (uint8_t)e;
         }
         if (a.status) a.status[b] = st;
@@ -610,7 +625,22 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
 }
 
 // ------------------------------------------------------------------ XOR
-template <int POL>
+// KG = inputs loaded back to back per group (2, 4 or 8, the smallest that covers k, or 8 for
+// k > 8): a group issues exactly the loads it uses except for clamped repeats in the last
+// group, so XOR(2,1) issues 2 loads per item, not 8.
+template <int KG>
+__device__ __forceinline__ void xor_fold(uint4& acc, const uint4 (&x)[KG], uint32_t valid) {
+#pragma unroll
+    for (int jj = 0; jj < KG; ++jj)
+        if ((uint32_t)jj < valid) {
+            acc.x ^= x[jj].x;
+            acc.y ^= x[jj].y;
+            acc.z ^= x[jj].z;
+            acc.w ^= x[jj].w;
+        }
+}
+
+template <int POL, int KG>
 __global__ __launch_bounds__(kThreads) void xor_encode_kernel(XorArgs a) {
     constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     const uint32_t k = a.k;
@@ -620,24 +650,17 @@ __global__ __launch_bounds__(kThreads) void xor_encode_kernel(XorArgs a) {
         const uint32_t c = rotate_chunk(item - b * a.cps, a.cps, a.rot);
         const uint8_t* src = a.in + (uint64_t)b * a.in_bs + (uint64_t)c * kChunk;
         uint4 acc = make_uint4(0, 0, 0, 0);
-        for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
-            uint4 x[kInGroup];
+        for (uint32_t j0 = 0; j0 < k; j0 += KG) {
+            uint4 x[KG];
 #pragma unroll
-            for (int jj = 0; jj < kInGroup; ++jj) x[jj] = ld16<NTL>(src + (uint64_t)min(j0 + jj, k - 1) * a.ss);
-#pragma unroll
-            for (int jj = 0; jj < kInGroup; ++jj)
-                if (j0 + jj < k) {
-                    acc.x ^= x[jj].x;
-                    acc.y ^= x[jj].y;
-                    acc.z ^= x[jj].z;
-                    acc.w ^= x[jj].w;
-                }
+            for (int jj = 0; jj < KG; ++jj) x[jj] = ld16<NTL>(src + (uint64_t)min(j0 + jj, k - 1) * a.ss);
+            xor_fold<KG>(acc, x, k - j0);
         }
         store_chunk<NTS>(a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk, acc, a.len - c * kChunk, a.pad_zero);
     }
 }
 
-template <int POL>
+template <int POL, int KG>
 __global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
     constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     const uint32_t k = a.k, n = k + 1;
@@ -659,22 +682,15 @@ __global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
         uint8_t* blk = a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk;
         const uint8_t* par = a.parity + (uint64_t)b * a.par_bs + (uint64_t)c * kChunk;
         uint4 acc = make_uint4(0, 0, 0, 0);
-        for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
-            uint4 x[kInGroup];
+        for (uint32_t j0 = 0; j0 < k; j0 += KG) {
+            uint4 x[KG];
 #pragma unroll
-            for (int jj = 0; jj < kInGroup; ++jj) {
+            for (int jj = 0; jj < KG; ++jj) {
                 const uint32_t j = min(j0 + jj, k - 1);
                 const uint32_t s = j + (j >= mi);     // the k shards other than the missing one
                 x[jj] = ld16<NTL>(s < k ? blk + (uint64_t)s * a.ss : par);
             }
-#pragma unroll
-            for (int jj = 0; jj < kInGroup; ++jj)
-                if (j0 + jj < k) {
-                    acc.x ^= x[jj].x;
-                    acc.y ^= x[jj].y;
-                    acc.z ^= x[jj].z;
-                    acc.w ^= x[jj].w;
-                }
+            xor_fold<KG>(acc, x, k - j0);
         }
         store_chunk<NTS>(blk + (uint64_t)mi * a.ss, acc, a.len - c * kChunk, a.pad_zero);
     }
@@ -738,9 +754,12 @@ static hipError_t enc_fixed_dispatch(const EncodeArgs& a, int grid, size_t lds, 
 hipError_t launch_rs_encode_fixed(EncodeArgs a, int ncu, hipStream_t s) {
     const uint32_t chunks = (a.total + kThreads - 1) / kThreads;
     if (chunks == 0) return hipSuccess;
-    const bool queue = g_tune.enc_queue && a.ctr != nullptr;
+    // Per shape (measured): RS(8,12) runs the ticket queue at 2 workgroups/CU;
+    // RS(2,3) (2 loads per lane: little in flight per wave) the flat grid at full residency;
+    // RS(16,24) (VALU-heavy: 128 coefficients) the flat grid at 4 workgroups/CU.
+    const bool queue = g_tune.enc_queue && a.ctr != nullptr && a.k == 8;
     int grid = (int)chunks;
-    int wpc = g_tune.enc_wpc;
+    int wpc = a.k == 2 ? 0 : a.k == 16 ? 4 : g_tune.enc_wpc;
     if (queue) {
         wpc = g_tune.enc_qwpc > 0 ? g_tune.enc_qwpc : 2;
         grid = ncu * wpc;
@@ -749,8 +768,6 @@ hipError_t launch_rs_encode_fixed(EncodeArgs a, int ncu, hipStream_t s) {
         grid = std::min(grid / 8, per_range) * 8;
         if (grid < 8) grid = 8;
         a.per_xcd = ((a.total + 7) / 8 + kThreads - 1) / kThreads * kThreads;
-        const hipError_t e = hipMemsetAsync(a.ctr, 0, 8 * kCtrStride * sizeof(uint32_t), s);
-        if (e != hipSuccess) return e;
     }
     const size_t lds = occupancy_lds(wpc, (size_t)a.m * a.k * sizeof(gf::PermTab));
     if (a.k == 2 && a.m == 1) return enc_fixed_dispatch<2, 1>(a, grid, lds, queue, s);
@@ -762,13 +779,9 @@ hipError_t launch_rs_encode_fixed(EncodeArgs a, int ncu, hipStream_t s) {
 hipError_t launch_rs_plan(const PlanArgs& a, hipStream_t s) {
     const int grid = (int)((a.nblocks + kPlanThreads - 1) / kPlanThreads);
     if (grid == 0) return hipSuccess;
-    const size_t lds = 768 + (size_t)kPlanThreads * a.lay.stride;
+    const size_t lds = plan_lds(a.m, a.k, a.lay.stride).total;
     const dim3 g(grid), t(kPlanThreads);
-    if (a.maxe <= 1) hipLaunchKernelGGL(rs_plan_kernel<1>, g, t, lds, s, a);
-    else if (a.maxe <= 2) hipLaunchKernelGGL(rs_plan_kernel<2>, g, t, lds, s, a);
-    else if (a.maxe <= 4) hipLaunchKernelGGL(rs_plan_kernel<4>, g, t, lds, s, a);
-    else if (a.maxe <= 8) hipLaunchKernelGGL(rs_plan_kernel<8>, g, t, lds, s, a);
-    else hipLaunchKernelGGL(rs_plan_kernel<16>, g, t, lds, s, a);
+    hipLaunchKernelGGL(rs_plan_kernel, g, t, lds, s, a);
     return hipGetLastError();
 }
 
@@ -796,18 +809,30 @@ hipError_t launch_rs_reconstruct(const ReconArgs& a, int grid, hipStream_t s) {
     }
 }
 
-hipError_t launch_xor_encode(const XorArgs& a, int grid, hipStream_t s) {
-    const size_t lds = occupancy_lds(g_tune.gen_wpc, 0);
-    if (g_tune.enc_nt & 3) hipLaunchKernelGGL(xor_encode_kernel<3>, dim3(grid), dim3(kThreads), lds, s, a);
-    else hipLaunchKernelGGL(xor_encode_kernel<0>, dim3(grid), dim3(kThreads), lds, s, a);
+template <int KG>
+static void xor_launch(const XorArgs& a, int grid, size_t lds, bool nt, bool encode, hipStream_t s) {
+    if (encode) {
+        if (nt) hipLaunchKernelGGL((xor_encode_kernel<3, KG>), dim3(grid), dim3(kThreads), lds, s, a);
+        else hipLaunchKernelGGL((xor_encode_kernel<0, KG>), dim3(grid), dim3(kThreads), lds, s, a);
+    } else {
+        if (nt) hipLaunchKernelGGL((xor_reconstruct_kernel<3, KG>), dim3(grid), dim3(kThreads), lds, s, a);
+        else hipLaunchKernelGGL((xor_reconstruct_kernel<0, KG>), dim3(grid), dim3(kThreads), lds, s, a);
+    }
+}
+
+static hipError_t xor_dispatch(const XorArgs& a, int grid, size_t lds, bool nt, bool encode, hipStream_t s) {
+    if (a.k <= 2) xor_launch<2>(a, grid, lds, nt, encode, s);
+    else if (a.k <= 4) xor_launch<4>(a, grid, lds, nt, encode, s);
+    else xor_launch<8>(a, grid, lds, nt, encode, s);
     return hipGetLastError();
 }
 
+hipError_t launch_xor_encode(const XorArgs& a, int grid, hipStream_t s) {
+    return xor_dispatch(a, grid, occupancy_lds(g_tune.gen_wpc, 0), (g_tune.enc_nt & 3) != 0, true, s);
+}
+
 hipError_t launch_xor_reconstruct(const XorArgs& a, int grid, hipStream_t s) {
-    const size_t lds = occupancy_lds(g_tune.dec_wpc, 0);
-    if (g_tune.dec_nt & 3) hipLaunchKernelGGL(xor_reconstruct_kernel<3>, dim3(grid), dim3(kThreads), lds, s, a);
-    else hipLaunchKernelGGL(xor_reconstruct_kernel<0>, dim3(grid), dim3(kThreads), lds, s, a);
-    return hipGetLastError();
+    return xor_dispatch(a, grid, occupancy_lds(g_tune.dec_wpc, 0), (g_tune.dec_nt & 3) != 0, false, s);
 }
 
 uint32_t pick_tile_blocks(uint32_t cps, uint32_t k, uint32_t maxe, const PlanLayout& lay) {
@@ -851,7 +876,7 @@ int occupancy_grid(int device, int which, uint32_t sel, size_t lds) {
         else if (sel <= 8) fn = (const void*)rs_reconstruct_kernel<8, 3>;
         else fn = (const void*)rs_reconstruct_kernel<16, 3>;
     } else {
-        fn = (const void*)xor_encode_kernel<3>;
+        fn = (const void*)xor_encode_kernel<3, 8>;
     }
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kThreads, lds) != hipSuccess || per <= 0)
         per = 4;

@@ -31,11 +31,13 @@ struct EncodeArgs {
     uint32_t pad_zero;         // tail chunk: full 16-B store, bytes past len zeroed
     uint32_t rot;              // chunk rotation inside a block (line_rotation())
     uint32_t swz;              // XCD-contiguous workgroup order (xcd_order())
-    uint32_t* ctr;             // queue kernel: 8 zeroed ticket counters, kCtrStride words apart
+    uint32_t* ctr;             // queue kernel: 8 ticket counters kCtrStride words apart, then the
+                               // arrival counter; all zero at launch, rewound by the last workgroup
     uint32_t per_xcd;          // queue kernel: items per XCD range
 };
 
 constexpr int kCtrStride = 32;      // one 128-byte line per ticket counter
+constexpr int kCtrWords = 9 * kCtrStride;
 
 // Decode plan, one record of `stride` bytes per block (offsets from plan_layout()):
 //   [in_off,   +rup8(k))  input shard slots = the first k present shards, in index order

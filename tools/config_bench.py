@@ -1,0 +1,161 @@
+#!/usr/bin/env python3
+"""Device-resident encode + decode rates for every GPU configuration of BASELINE.json
+(diagnostics beside bench.py, which times only the headline RS(8,12) config).
+
+  RS(2,3)    65 536 blocks, one random erased data shard per block
+  RS(8,12)   2^20 blocks, one random erased data shard per block (bench.py's workload)
+  RS(16,24)  2^19 blocks, e ~ U{1..8} erasures per block, uniform over all 24 shards
+  XOR(2,1)   2^20 blocks (the reference's XOR factory code), one erased data shard
+
+Algorithmic bytes (L = 1202): encode k*L read + m*L written per block; decode (recover into an
+output buffer) (k + e_d)*L per block with e_d >= 1 erased data shards, nothing for blocks whose
+data shards all arrived. Prints one JSON line per config.
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+PAYLOAD, L, S = 1200, 1202, 1216
+
+
+def timed(torch, fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def make_data(torch, B, k, g):
+    data = torch.zeros((B, k, S), dtype=torch.uint8, device="cuda")
+    for b0 in range(0, B, 1 << 16):
+        b1 = min(B, b0 + (1 << 16))
+        data[b0:b1, :, :PAYLOAD] = torch.randint(0, 256, (b1 - b0, k, PAYLOAD), generator=g, device="cuda",
+                                                 dtype=torch.int16).to(torch.uint8)
+    data[:, :, PAYLOAD] = PAYLOAD >> 8
+    data[:, :, PAYLOAD + 1] = PAYLOAD & 0xFF
+    return data
+
+
+def run_rs(torch, fec, codec, k, m, B, multi, iters, seed):
+    n = k + m
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    data = make_data(torch, B, k, g)
+    parity = torch.zeros((B, m, S), dtype=torch.uint8, device="cuda")
+    if multi:
+        # e ~ U{1..multi} erasures per block, a uniform subset of the n shards
+        e = torch.randint(1, multi + 1, (B,), generator=g, device="cuda")
+        keys = torch.rand((B, n), generator=g, device="cuda")
+        rank = keys.argsort(dim=1).argsort(dim=1)
+        lost = rank < e[:, None]
+    else:
+        which = torch.randint(0, k, (B,), generator=g, device="cuda")
+        lost = torch.zeros((B, n), dtype=torch.bool, device="cuda")
+        lost[torch.arange(B, device="cuda"), which] = True
+    weights = torch.bitwise_left_shift(torch.ones(n, dtype=torch.int64, device="cuda"),
+                                       torch.arange(n, device="cuda"))
+    masks = (((~lost).to(torch.int64) * weights).sum(dim=1)).to(torch.int32)
+    e_d = lost[:, :k].sum(dim=1)
+    slots = int(e_d.max().item())
+    out = torch.zeros((B, max(slots, 1), S), dtype=torch.uint8, device="cuda")
+    status = torch.zeros((B,), dtype=torch.int32, device="cuda")
+
+    def enc():
+        codec.rs_encode_split(k, m, data, parity, shard_len=L)
+
+    def dec():
+        codec.rs_recover_split(k, m, data, parity, masks, out, status=status, shard_len=L)
+
+    enc()
+    dec()
+    codec.sync()
+    # full-size check: recovered slot r of block b == its r-th erased data shard
+    ok = bool((status == e_d.to(torch.int32)).all().item())
+    order = torch.where(lost[:, :k], torch.arange(k, device="cuda"), k).sort(dim=1).values
+    for r in range(slots):
+        rows = (e_d > r).nonzero().squeeze(1)
+        if rows.numel():
+            src = data[rows, order[rows, r], :L]
+            ok = ok and bool(torch.equal(out[rows, r, :L], src))
+    for _ in range(2):
+        enc()
+        dec()
+    torch.cuda.synchronize()
+    t_enc = timed(torch, enc, iters)
+    t_dec = timed(torch, dec, iters)
+    enc_bytes = B * n * L
+    dec_bytes = int(((k + e_d) * (e_d > 0)).sum().item()) * L
+    return {"config": "RS(%d,%d)" % (k, n), "blocks": B,
+            "erasures": ("U{1..%d} of %d shards" % (multi, n)) if multi else "1 data shard",
+            "mean_data_erasures": round(float(e_d.float().mean().item()), 3),
+            "encode_ms": round(t_enc, 4), "decode_ms": round(t_dec, 4),
+            "encode_TB/s": round(enc_bytes / t_enc / 1e9, 3), "decode_TB/s": round(dec_bytes / t_dec / 1e9, 3),
+            "payload_GiB/s": round(B * k * PAYLOAD / 2**30 / ((t_enc + t_dec) / 1e3), 1),
+            "step_frac": round((enc_bytes + dec_bytes) / ((t_enc + t_dec) / 1e3) / 8e12, 4),
+            "check": ok}
+
+
+def run_xor(torch, fec, codec, k, B, iters, seed):
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    sh = torch.zeros((B, k + 1, S), dtype=torch.uint8, device="cuda")
+    sh[:, :k] = make_data(torch, B, k, g)
+    which = torch.randint(0, k, (B,), generator=g, device="cuda")
+    masks = (((1 << (k + 1)) - 1) - torch.bitwise_left_shift(torch.ones_like(which), which)).to(torch.int32)
+    ref = None
+
+    def enc():
+        codec.xor_encode(k, sh, shard_len=L)
+
+    def dec():
+        codec.xor_reconstruct(k, sh, masks, shard_len=L)
+
+    enc()
+    codec.sync()
+    ref = sh[:, :k, :L].clone()
+    sh[torch.arange(B, device="cuda"), which] = 0
+    dec()
+    codec.sync()
+    ok = bool(torch.equal(sh[:, :k, :L], ref))
+    del ref
+    t_enc = timed(torch, enc, iters)
+    t_dec = timed(torch, dec, iters)
+    enc_bytes = B * (k + 1) * L
+    dec_bytes = B * (k + 1) * L
+    return {"config": "XOR(%d,1)" % k, "blocks": B, "erasures": "1 data shard",
+            "encode_ms": round(t_enc, 4), "decode_ms": round(t_dec, 4),
+            "encode_TB/s": round(enc_bytes / t_enc / 1e9, 3), "decode_TB/s": round(dec_bytes / t_dec / 1e9, 3),
+            "payload_GiB/s": round(B * k * PAYLOAD / 2**30 / ((t_enc + t_dec) / 1e3), 1),
+            "step_frac": round((enc_bytes + dec_bytes) / ((t_enc + t_dec) / 1e3) / 8e12, 4),
+            "check": ok}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    import torch
+    fec = importlib.import_module("0xfec_amd")
+    codec = fec.Codec(0).use_torch_stream()
+    cases = [("rs23", lambda: run_rs(torch, fec, codec, 2, 1, 65536, 0, max(args.iters, 100), 0x0FEC)),
+             ("rs812", lambda: run_rs(torch, fec, codec, 8, 4, 1 << 20, 0, args.iters, 0x0FEC)),
+             ("rs1624", lambda: run_rs(torch, fec, codec, 16, 8, 1 << 19, 8, args.iters, 0x0FEC)),
+             ("xor21", lambda: run_xor(torch, fec, codec, 2, 1 << 20, args.iters, 0x0FEC))]
+    for name, fn in cases:
+        if args.only and name not in args.only.split(","):
+            continue
+        print(json.dumps(fn()), flush=True)
+        torch.cuda.empty_cache()
+    codec.close()
+
+
+if __name__ == "__main__":
+    main()
