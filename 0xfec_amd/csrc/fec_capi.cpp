@@ -253,6 +253,10 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         a.swz = (uint32_t)fk::g_tune.dec_swz;
         a.out = out ? out + b0 * out_bs : nullptr;
         a.out_bs = out_bs;
+        if (fk::wave_recon_applies(cps, k, maxe, lay.stride)) {
+            HIP_TRY(fk::launch_rs_reconstruct_wave(a, ctx->stream));
+            continue;
+        }
         int grid;
         if (fk::g_tune.tiles_per_wg > 0)
             grid = (int)((a.ntiles + fk::g_tune.tiles_per_wg - 1) / fk::g_tune.tiles_per_wg);
@@ -502,7 +506,7 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 10 ? &fk::g_tune.dec_wpc : key == 11 ? &fk::g_tune.enc_fixed
               : key == 12 ? &fk::g_tune.dec_swz : key == 13 ? &fk::g_tune.gen_wpc
               : key == 14 ? &fk::g_tune.enc_queue : key == 15 ? &fk::g_tune.enc_qwpc
-              : key == 16 ? &fk::g_tune.enc_qdepth : nullptr;
+              : key == 16 ? &fk::g_tune.enc_qdepth : key == 17 ? &fk::g_tune.dec_wave : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

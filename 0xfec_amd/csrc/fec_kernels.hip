@@ -528,10 +528,74 @@ __global__ __launch_bounds__(kPlanThreads) void rs_plan_kernel(PlanArgs a) {
 }
 
 // ------------------------------------------------------------------ RS reconstruct
-// A workgroup takes tiles of G consecutive blocks: it stages their plans in LDS, expands
-// every coefficient to its PermTab once, then lanes sweep the G*cps (block, chunk) items.
-// Rows beyond a block's own erasure count carry zero tables, and each item loops only to
-// the wave's largest erasure count (ballot), so one-erasure batches do one row of work.
+// One (block, chunk) item: load the k input shards named by the plan record P, fold them with
+// the block's PermTabs T (row r = erased shard r), store the rebuilt chunks. `rows` is
+// wave-uniform (the wave's largest erasure count), so the loop bounds never diverge.
+template <int MAXE, bool NTL, bool NTS>
+__device__ __forceinline__ void recon_item(const ReconArgs& a, const uint8_t* P, const gf::PermTab* T,
+                                           uint32_t blk, uint32_t c, uint32_t rows, uint32_t nout) {
+    const uint32_t k = a.k;
+    const PlanLayout& lay = a.lay;
+    uint8_t* dblk = a.data + (uint64_t)blk * a.dbs + (uint64_t)c * kChunk;
+    const uint8_t* pblk = a.parity + (uint64_t)blk * a.pbs + (uint64_t)c * kChunk;
+    uint32_t acc[MAXE][4];
+#pragma unroll
+    for (int r = 0; r < MAXE; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0;
+    for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
+        // the 8 input slots of this group, one ds_read_b64
+        const uint2 sl = *reinterpret_cast<const uint2*>(P + lay.in_off + j0);
+        uint4 x[kInGroup];
+#pragma unroll
+        for (int jj = 0; jj < kInGroup; ++jj) {
+            const uint32_t w = jj < 4 ? sl.x : sl.y;
+            const uint32_t slot = (w >> (8 * (jj & 3))) & 0xFFu;
+            x[jj] = j0 + jj < k   // uniform predicate: no loads past input k-1
+                        ? ld16<NTL>(slot < k ? dblk + (uint64_t)slot * a.ss : pblk + (uint64_t)(slot - k) * a.ss)
+                        : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int jj = 0; jj < kInGroup; jj += 2) {
+            const uint32_t j = j0 + jj;
+            if (j + 1 < k) {
+                Idx ia[4], ib[4];
+                split4(ia, x[jj]);
+                split4(ib, x[jj + 1]);
+#pragma unroll
+                for (int r = 0; r < MAXE; ++r)
+                    if (r < (int)rows) mac2(acc[r], ia, ib, T + r * k + j, T + r * k + j + 1);
+            } else if (j < k) {
+                Idx ia[4];
+                split4(ia, x[jj]);
+#pragma unroll
+                for (int r = 0; r < MAXE; ++r)
+                    if (r < (int)rows) mac1(acc[r], ia, T + r * k + j);
+            }
+        }
+    }
+    const uint32_t nb = a.len - c * kChunk;
+    const uint8_t* out_idx = P + lay.out_off;
+    uint8_t* oblk = a.out ? a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk : nullptr;
+#pragma unroll
+    for (int r = 0; r < MAXE; ++r)
+        if (r < (int)nout)
+            store_chunk<NTS>(oblk ? oblk + (uint64_t)r * a.ss : dblk + (uint64_t)out_idx[r] * a.ss, as_uint4(acc[r]),
+                             nb, a.pad_zero);
+}
+
+template <int MAXE>
+__device__ __forceinline__ uint32_t wave_rows(uint32_t nout) {
+    uint32_t rows = 0;
+#pragma unroll
+    for (int r = 0; r < MAXE; ++r)
+        if (__any((int)nout > r)) rows = r + 1;
+    return rows;
+}
+
+// Tile form: a workgroup takes tiles of G consecutive blocks: it stages their plans in LDS,
+// expands every coefficient to its PermTab once, then lanes sweep the G*cps (block, chunk)
+// items. Rows beyond a block's own erasure count carry zero tables, and each item loops only
+// to the wave's largest erasure count (ballot), so one-erasure batches do one row of work.
+// Used for short shards (fewer than 32 chunks: many blocks per wave).
 template <int MAXE, int POL>
 __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
     constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
@@ -571,57 +635,69 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
             const uint32_t c = rotate_chunk(t - g * a.cps, a.cps, a.rot);
             const uint8_t* P = plans + g * lay.stride;
             const uint32_t nout = inr ? P[lay.nout_off] : 0;
-            uint32_t rows = 0;
-#pragma unroll
-            for (int r = 0; r < MAXE; ++r)
-                if (__any((int)nout > r)) rows = r + 1;
+            const uint32_t rows = wave_rows<MAXE>(nout);
             if (nout == 0) continue;
-            const gf::PermTab* T = tabs + g * maxe * k;
-            uint8_t* dblk = a.data + (uint64_t)(b0 + g) * a.dbs + (uint64_t)c * kChunk;
-            const uint8_t* pblk = a.parity + (uint64_t)(b0 + g) * a.pbs + (uint64_t)c * kChunk;
-            uint32_t acc[MAXE][4];
-#pragma unroll
-            for (int r = 0; r < MAXE; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0;
-            for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
-                // the 8 input slots of this group, one ds_read_b64
-                const uint2 sl = *reinterpret_cast<const uint2*>(P + lay.in_off + j0);
-                uint4 x[kInGroup];
-#pragma unroll
-                for (int jj = 0; jj < kInGroup; ++jj) {
-                    const uint32_t w = jj < 4 ? sl.x : sl.y;
-                    uint32_t slot = (w >> (8 * (jj & 3))) & 0xFFu;
-                    if (j0 + jj >= k) slot = (sl.x & 0xFFu);   // clamp to a valid shard
-                    x[jj] = ld16<NTL>(slot < k ? dblk + (uint64_t)slot * a.ss : pblk + (uint64_t)(slot - k) * a.ss);
-                }
-#pragma unroll
-                for (int jj = 0; jj < kInGroup; jj += 2) {
-                    const uint32_t j = j0 + jj;
-                    if (j + 1 < k) {
-                        Idx ia[4], ib[4];
-                        split4(ia, x[jj]);
-                        split4(ib, x[jj + 1]);
-#pragma unroll
-                        for (int r = 0; r < MAXE; ++r)
-                            if (r < (int)rows) mac2(acc[r], ia, ib, T + r * k + j, T + r * k + j + 1);
-                    } else if (j < k) {
-                        Idx ia[4];
-                        split4(ia, x[jj]);
-#pragma unroll
-                        for (int r = 0; r < MAXE; ++r)
-                            if (r < (int)rows) mac1(acc[r], ia, T + r * k + j);
-                    }
-                }
-            }
-            const uint32_t nb = a.len - c * kChunk;
-            const uint8_t* out_idx = P + lay.out_off;
-            uint8_t* oblk = a.out ? a.out + (uint64_t)(b0 + g) * a.out_bs + (uint64_t)c * kChunk : nullptr;
-#pragma unroll
-            for (int r = 0; r < MAXE; ++r)
-                if (r < (int)nout)
-                    store_chunk<NTS>(oblk ? oblk + (uint64_t)r * a.ss : dblk + (uint64_t)out_idx[r] * a.ss,
-                                     as_uint4(acc[r]), nb, a.pad_zero);
+            recon_item<MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, b0 + g, c, rows, nout);
         }
     }
+}
+
+// Wave form (shards of 32+ chunks, i.e. at most 3 blocks per wave): flat grid, one item per
+// lane; each wave stages the plan records of its own blocks and expands only the PermTabs of
+// rows those blocks rebuild, in a wave-private LDS slice, so no workgroup barrier stands
+// between a wave's plan load and its data loads.
+constexpr uint32_t kWaveBlocks = 3;
+
+__host__ __device__ inline size_t wave_slice_bytes(uint32_t k, uint32_t maxe, uint32_t stride) {
+    return (size_t)kWaveBlocks * maxe * k * 32 + (size_t)kWaveBlocks * stride;
+}
+
+template <int MAXE, int POL>
+__global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs a) {
+    constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t k = a.k, maxe = a.maxe;
+    const PlanLayout lay = a.lay;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint8_t* slice = smem + (size_t)wave * wave_slice_bytes(k, maxe, lay.stride);
+    gf::PermTab* tabs = reinterpret_cast<gf::PermTab*>(slice);                      // 3*maxe*k
+    uint8_t* plans = slice + (size_t)kWaveBlocks * maxe * k * sizeof(gf::PermTab);  // 3*stride
+    const uint32_t total = a.nblocks * a.cps;
+    const uint32_t i0 = (xcd_order(a.swz) * kThreads) + (wave << 6);
+    if (i0 >= total) return;
+    const uint32_t bfirst = fdiv(i0, a.div_cps);
+    const uint32_t nb = fdiv(min(i0 + 63u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
+    {
+        const uint32_t nw = nb * lay.stride / 16;
+        const uint4* src = reinterpret_cast<const uint4*>(a.plans + (uint64_t)bfirst * lay.stride);
+        if (lane < nw) reinterpret_cast<uint4*>(plans)[lane] = src[lane];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    {
+        const uint32_t ne = nb * maxe * k;
+        for (uint32_t i = lane; i < ne; i += 64) {
+            const uint32_t g = i / (maxe * k);
+            const uint32_t rem = i - g * maxe * k;
+            const uint32_t r = rem / k, j = rem - r * k;
+            const uint8_t* P = plans + g * lay.stride;
+            if (r < P[lay.nout_off]) tabs[i] = gf::make_permtab(P[lay.coef_off + r * k + j]);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t item = i0 + lane;
+    const bool inr = item < total;
+    const uint32_t blk = inr ? fdiv(item, a.div_cps) : bfirst;
+    const uint32_t g = blk - bfirst;
+    const uint32_t c = item - blk * a.cps;
+    const uint8_t* P = plans + g * lay.stride;
+    const uint32_t nout = inr ? P[lay.nout_off] : 0;
+    const uint32_t rows = wave_rows<MAXE>(nout);
+    if (nout == 0) return;
+    recon_item<MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, blk, c, rows, nout);
 }
 
 // ------------------------------------------------------------------ XOR
@@ -798,6 +874,34 @@ static hipError_t recon_dispatch(const ReconArgs& a, int grid, hipStream_t s) {
     else if (a.maxe <= 8) hipLaunchKernelGGL((rs_reconstruct_kernel<8, POL>), dim3(grid), dim3(kThreads), lds, s, a);
     else hipLaunchKernelGGL((rs_reconstruct_kernel<16, POL>), dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
+}
+
+// The wave form applies to shards of 32+ chunks (at most 3 blocks per wave) while its LDS
+// (4 wave slices per workgroup) stays within 64 KiB.
+bool wave_recon_applies(uint32_t cps, uint32_t k, uint32_t maxe, uint32_t stride) {
+    return g_tune.dec_wave && cps >= 32 && 4 * wave_slice_bytes(k, maxe, stride) <= 65536;
+}
+
+template <int POL>
+static hipError_t recon_wave_dispatch(const ReconArgs& a, hipStream_t s) {
+    const int grid = (int)(((uint64_t)a.nblocks * a.cps + kThreads - 1) / kThreads);
+    if (grid == 0) return hipSuccess;
+    const size_t lds = occupancy_lds(g_tune.dec_wpc, 4 * wave_slice_bytes(a.k, a.maxe, a.lay.stride));
+    if (a.maxe <= 1) hipLaunchKernelGGL((rs_reconstruct_wave_kernel<1, POL>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (a.maxe <= 2) hipLaunchKernelGGL((rs_reconstruct_wave_kernel<2, POL>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (a.maxe <= 4) hipLaunchKernelGGL((rs_reconstruct_wave_kernel<4, POL>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (a.maxe <= 8) hipLaunchKernelGGL((rs_reconstruct_wave_kernel<8, POL>), dim3(grid), dim3(kThreads), lds, s, a);
+    else hipLaunchKernelGGL((rs_reconstruct_wave_kernel<16, POL>), dim3(grid), dim3(kThreads), lds, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_rs_reconstruct_wave(const ReconArgs& a, hipStream_t s) {
+    switch (g_tune.dec_nt & 3) {
+        case 0: return recon_wave_dispatch<0>(a, s);
+        case 1: return recon_wave_dispatch<1>(a, s);
+        case 2: return recon_wave_dispatch<2>(a, s);
+        default: return recon_wave_dispatch<3>(a, s);
+    }
 }
 
 hipError_t launch_rs_reconstruct(const ReconArgs& a, int grid, hipStream_t s) {

@@ -113,6 +113,7 @@ struct Tuning {
     int enc_queue = 1;        // ... as the persistent ticket-queue kernel (0: flat grid)
     int enc_qwpc = 2;         // resident workgroups per CU of the queue kernel
     int enc_qdepth = 1;       // chunks the queue kernel loads ahead of the one it computes
+    int dec_wave = 1;         // reconstruct: wave-private plan staging (shards of 32+ chunks)
 };
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):
@@ -139,6 +140,8 @@ bool fixed_encode_applies(uint32_t k, uint32_t m);
 hipError_t launch_rs_encode_fixed(EncodeArgs a, int ncu, hipStream_t s);
 hipError_t launch_rs_plan(const PlanArgs& a, hipStream_t s);
 hipError_t launch_rs_reconstruct(const ReconArgs& a, int grid, hipStream_t s);
+bool wave_recon_applies(uint32_t cps, uint32_t k, uint32_t maxe, uint32_t stride);
+hipError_t launch_rs_reconstruct_wave(const ReconArgs& a, hipStream_t s);
 hipError_t launch_xor_encode(const XorArgs& a, int grid, hipStream_t s);
 hipError_t launch_xor_reconstruct(const XorArgs& a, int grid, hipStream_t s);
 

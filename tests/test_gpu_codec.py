@@ -321,3 +321,40 @@ def test_rs_encode_kernel_variants_match_oracle(codec, oracle, torch, variant, k
     got = p.cpu().numpy()
     assert np.array_equal(got[:, :, :L], ref[:, k:, :L])
     assert not got[:, :, L:].any()               # pad to the 16-byte boundary written as zeros
+
+
+# Both reconstruct kernel forms (workgroup tiles; wave-private plans for shards of 32+ chunks)
+# in place and out of place, against the oracle, with the erasure counts mixed inside waves.
+@pytest.mark.parametrize("wave", [0, 1])
+@pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10)])
+@pytest.mark.parametrize("L", [513, 1202, 1436])
+def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, wave, k, m, L):
+    rng = np.random.default_rng(11 * k + L + wave)
+    n, B = k + m, 389
+    S = (L + 15) // 16 * 16
+    sh = _rand_shards(rng, B, n, S, L)
+    oracle.rs_encode(k, m, sh)
+    masks = _random_masks(rng, B, k, m)
+    data_np = np.ascontiguousarray(sh[:, :k]).copy()
+    for b in range(B):
+        for i in range(k):
+            if not (masks[b] >> i) & 1:
+                data_np[b, i] = 0x3C
+    par = torch.from_numpy(np.ascontiguousarray(sh[:, k:])).cuda()
+    dm = torch.from_numpy(masks.view(np.int32)).cuda()
+    old = codec.set_tuning(dec_wave=wave)
+    try:
+        out = torch.full((B, m, S), 0xEE, dtype=torch.uint8, device="cuda")
+        data = torch.from_numpy(data_np).cuda()
+        codec.rs_recover_split(k, m, data, par, dm, out, shard_len=L)
+        codec.sync()
+        got = out.cpu().numpy()
+        for b in range(B):
+            miss = [i for i in range(k) if not (masks[b] >> i) & 1]
+            for r, i in enumerate(miss):
+                assert np.array_equal(got[b, r, :L], sh[b, i, :L]), (b, r, i)
+        codec.rs_reconstruct_split(k, m, data, par, dm, shard_len=L)
+        codec.sync()
+        assert np.array_equal(data.cpu().numpy()[:, :, :L], sh[:, :k, :L])
+    finally:
+        codec.set_tuning(**old)

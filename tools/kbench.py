@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--occ", default="",
                     help="swz:enc_wpc:dec_wpc triples; when given, only the split-layout encode and "
                          "recover (the bench.py step) are timed, once per triple")
+    ap.add_argument("--dsweep", default="",
+                    help="wave:dec_swz:dec_wpc triples; when given, only the split-layout recover "
+                         "(the bench.py decode) is timed, once per triple")
     args = ap.parse_args()
     import torch
     fec = importlib.import_module("0xfec_amd")
@@ -57,7 +60,7 @@ def main():
         keys = {"enc_nt": 0, "dec_nt": 1, "grid_mult": 2, "dec_max_rounds": 3, "pad_zero": 4,
                 "items_per_thread": 5, "tiles_per_wg": 6, "rotate": 7, "xcd_swz": 8, "enc_wpc": 9,
                 "dec_wpc": 10, "enc_fixed": 11, "dec_swz": 12, "gen_wpc": 13,
-                "enc_queue": 14, "enc_qwpc": 15, "enc_qdepth": 16}
+                "enc_queue": 14, "enc_qwpc": 15, "enc_qdepth": 16, "dec_wave": 17}
         for key, val in kv.items():
             fec.lib.fec__set_tuning(codec.handle, keys[key], val)
 
@@ -106,6 +109,17 @@ def main():
         return f
 
     cases = {}
+    if args.dsweep:
+        args.occ = ""
+        for spec in args.dsweep.split(","):
+            wv, dsw, dw = [int(x) for x in spec.split(":")]
+
+            def dsw_case(fn, wv=wv, dsw=dsw, dw=dw):
+                def f():
+                    tune(dec_wave=wv, dec_swz=dsw, dec_wpc=dw)
+                    fn()
+                return f
+            cases["rs_recover split wave%d swz%d wpc%d" % (wv, dsw, dw)] = (dsw_case(rec_split(3, 0)), B * (k + 1) * L)
     if args.occ:
         # spec = swz:enc_wpc:dec_swz:dec_wpc:enc_fixed[:queue_wpc[:depth]]  (queue_wpc 0: flat grid)
         for spec in args.occ.split(","):
@@ -122,18 +136,18 @@ def main():
                 occ(enc_split(3, 0)), B * n * L)
             if not qw:
                 cases["rs_recover split swz%d wpc%d" % (dsw, dw)] = (occ(rec_split(3, 0)), B * (k + 1) * L)
-    for rot in (1, 0) if not args.occ else ():
+    for rot in (1, 0) if not (args.occ or args.dsweep) else ():
         cases["rs_recover split rot%d" % rot] = (rec_split(3, rot), B * (k + 1) * L)
         cases["rs_encode split rot%d" % rot] = (enc_split(3, rot), B * n * L)
-    if not args.occ:
+    if not (args.occ or args.dsweep):
         cases["rs_reconstruct split pol3"] = (dec_split(3), B * (k + 1) * L)
-    for spec in [x for x in args.enc.split(",") if x and not args.occ]:
+    for spec in [x for x in args.enc.split(",") if x and not (args.occ or args.dsweep)]:
         v, g, ipt = [int(x) for x in spec.split(":")]
         cases["rs_encode nt%d g%d ipt%d" % (v, g, ipt)] = (enc(v, g, ipt), B * n * L)
-    for spec in [x for x in args.dec.split(",") if x and not args.occ]:
+    for spec in [x for x in args.dec.split(",") if x and not (args.occ or args.dsweep)]:
         nt, r, g, tpw = [int(x) for x in spec.split(":")]
         cases["rs_reconstruct nt%d r%d g%d tpw%d" % (nt, r, g, tpw)] = (dec(nt, r, g, tpw), B * (k + 1) * L)
-    for spec in [x for x in args.xor.split(",") if x and not args.occ]:
+    for spec in [x for x in args.xor.split(",") if x and not (args.occ or args.dsweep)]:
         g, ipt = [int(x) for x in spec.split(":")]
         cases["xor_encode_k%d g%d ipt%d" % (k, g, ipt)] = (xor(g, ipt), B * (k + 1) * L)
     cases["torch_copy_%dto%d" % (k, m)] = (lambda: cp_dst.copy_(cp_src[:cp_dst.numel()]), 2 * cp_dst.numel())
