@@ -1,0 +1,256 @@
+// fec_batch.cpp — RepairQueue (repair_queue.go restated) and BatchEncoder (deferred, batched
+// repair-symbol generation on the GPU). Design and contracts: include/fec_batch.hpp.
+#include "../../include/fec_batch.hpp"
+
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "../../include/fec_hip.h"
+
+namespace fec {
+
+// ------------------------------------------------------------------ RepairQueue
+
+Error RepairQueue::Add(RepairFrame f) {   // repair_queue.go:40-69
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (closed_) return closeErr_.ok() ? Error::text("repair queue closed") : closeErr_;
+        // the reference panics("repair queue full") here (repair_queue.go:53)
+        if (q_.size() >= maxLen_) return Error::text("repair queue full");
+        q_.push_back(std::move(f));
+    }
+    if (hasData_) hasData_();
+    return Error::nil();
+}
+
+const RepairFrame* RepairQueue::Peek() {   // repair_queue.go:73-80
+    std::lock_guard<std::mutex> lk(mu_);
+    return q_.empty() ? nullptr : &q_.front();
+}
+
+void RepairQueue::Pop() {   // repair_queue.go:82-90
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!q_.empty()) q_.pop_front();
+}
+
+void RepairQueue::CloseWithError(Error e) {   // repair_queue.go:92-95
+    std::lock_guard<std::mutex> lk(mu_);
+    closeErr_ = std::move(e);
+    closed_ = true;
+}
+
+size_t RepairQueue::Len() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return q_.size();
+}
+
+// ------------------------------------------------------------------ BatchEncoder
+
+namespace {
+constexpr size_t kSlotMax = (kMaxFECPacketBufferSize + kRepairPayloadMetadataLen + 15) & ~size_t(15);   // 1440
+size_t round16(size_t x) { return (x + 15) & ~size_t(15); }
+Error hip_error(hipError_t e, const char* what) {
+    (void)hipGetLastError();
+    return Error{std::string(what) + ": " + hipGetErrorString(e), FEC_ERR_HIP};
+}
+Error codec_rc(int rc) { return rc ? Error{fec_strerror(rc), rc} : Error::nil(); }
+}  // namespace
+
+Error BatchEncoder::New(DecoderFECScheme scheme, int k, int m, size_t maxBlocks, std::shared_ptr<Engine> engine,
+                        std::unique_ptr<BatchEncoder>* out) {
+    out->reset();
+    if (maxBlocks == 0) return Error::text("batch must hold at least one block");
+    std::unique_ptr<BatchEncoder> e(new BatchEncoder(scheme, k, m, maxBlocks, std::move(engine)));
+    if (scheme == ReedSolomonFECScheme) {
+        Error err = ReedSolomonScheme::New(k, m, e->engine_, &e->rs_);
+        if (!err.ok()) return err;
+    } else if (scheme == XORFECScheme) {
+        if (m != 1) return Error::text("xor only supports 1 repair symbol");
+        if (k < 1 || k > 255) return Error::text("invalid number of source symbols");
+        e->xor_.reset(new XorScheme(e->engine_));
+    } else {
+        return Error::text("no FEC scheme");
+    }
+    *out = std::move(e);
+    return Error::nil();
+}
+
+BatchEncoder::~BatchEncoder() {
+    for (Set& s : sets_) {
+        if (s.inFlight && s.done) (void)hipEventSynchronize((hipEvent_t)s.done);
+        if (s.done) (void)hipEventDestroy((hipEvent_t)s.done);
+        if (s.h_in) (void)hipHostFree(s.h_in);
+        if (s.h_out) (void)hipHostFree(s.h_out);
+        if (s.d_in) (void)hipFree(s.d_in);
+        if (s.d_out) (void)hipFree(s.d_out);
+    }
+}
+
+Error BatchEncoder::init() {
+    fec_ctx* ctx = nullptr;
+    Error e = engine_->ctx(&ctx);
+    if (!e.ok()) return e;
+    const size_t in_bytes = maxBlocks_ * (size_t)k_ * kSlotMax;
+    const size_t out_bytes = maxBlocks_ * (size_t)m_ * kSlotMax;
+    for (Set& s : sets_) {
+        hipError_t h;
+        if ((h = hipHostMalloc(&s.h_in, in_bytes, hipHostMallocDefault)) != hipSuccess) return hip_error(h, "hipHostMalloc");
+        if ((h = hipHostMalloc(&s.h_out, out_bytes, hipHostMallocDefault)) != hipSuccess) return hip_error(h, "hipHostMalloc");
+        if ((h = hipMalloc(&s.d_in, in_bytes)) != hipSuccess) return hip_error(h, "hipMalloc");
+        if ((h = hipMalloc(&s.d_out, out_bytes)) != hipSuccess) return hip_error(h, "hipMalloc");
+        hipEvent_t ev;
+        if ((h = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hip_error(h, "hipEventCreate");
+        s.done = ev;
+    }
+    ready_ = true;
+    return Error::nil();
+}
+
+Error BatchEncoder::Submit(Block& b, RepairQueue* q) {
+    if (!q) return Error::text("nil repair queue");
+    // Validate first (the reference's errors take precedence over any device work), staging
+    // into a host scratch slot until the pinned sets exist.
+    const size_t want = round16(kRepairPayloadMetadataLen + (size_t)std::max(0, b.biggestSourceSymbolLenSoFar));
+    if (!ready_) {
+        std::vector<uint8_t> scratch((size_t)std::max(k_, 1) * kSlotMax);
+        size_t L = 0;
+        int count = 0;
+        Error e = rs_ ? rs_->stageRepairInput(b, scratch.data(), kSlotMax, &L)
+                      : xor_->stageRepairInput(b, scratch.data(), kSlotMax, &L, &count);
+        if (!e.ok()) return e;
+        if (xor_ && count != k_) return Error::text("block does not match the encoder's source symbol count");
+        e = init();
+        if (!e.ok()) return e;
+    }
+    Set* s = &sets_[cur_];
+    if (s->inFlight) {   // a retired batch whose frames did not fit their queue yet
+        Error e = waitSet(*s);
+        if (e.ok()) e = deliver(*s, nullptr);
+        if (!e.ok()) return e;
+    }
+    if (!s->blocks.empty() && (s->blocks.size() >= maxBlocks_ || std::max<size_t>(want, 16) > s->slot)) {
+        Error e = flushImpl(nullptr);
+        if (!e.ok()) return e;
+        s = &sets_[cur_];
+    }
+    if (s->blocks.empty()) s->slot = std::min(kSlotMax, std::max<size_t>(want, 16));
+    uint8_t* dst = s->h_in + s->blocks.size() * (size_t)k_ * s->slot;
+    size_t L = 0;
+    int count = 0;
+    Error e = rs_ ? rs_->stageRepairInput(b, dst, s->slot, &L) : xor_->stageRepairInput(b, dst, s->slot, &L, &count);
+    if (!e.ok()) return e;
+    if (xor_ && count != k_) return Error::text("block does not match the encoder's source symbol count");
+    s->blocks.push_back(Pending{q, b.id, L});
+    s->maxLen = std::max(s->maxLen, L);
+    return Error::nil();
+}
+
+Error BatchEncoder::Flush() { return flushImpl(nullptr); }
+
+Error BatchEncoder::flushImpl(size_t* delivered) {
+    Set& s = sets_[cur_];
+    if (s.inFlight) {   // undelivered frames of a retired batch still hold this set
+        Error e = waitSet(s);
+        if (e.ok()) e = deliver(s, delivered);
+        if (!e.ok()) return e;
+    }
+    if (s.blocks.empty()) return Error::nil();
+    fec_ctx* ctx = nullptr;
+    Error e = engine_->ctx(&ctx);
+    if (!e.ok()) return e;
+    hipStream_t st = (hipStream_t)fec_ctx_stream(ctx);
+    const size_t B = s.blocks.size();
+    hipError_t h = hipMemcpyAsync(s.d_in, s.h_in, B * (size_t)k_ * s.slot, hipMemcpyHostToDevice, st);
+    if (h != hipSuccess) return hip_error(h, "hipMemcpyAsync H2D");
+    int rc;
+    if (rs_)
+        rc = fec_rs_encode_batch(ctx, k_, m_, s.maxLen, B, s.d_in, (size_t)k_ * s.slot, s.d_out, (size_t)m_ * s.slot,
+                                 s.slot, FEC_DEVICE);
+    else
+        rc = fec_xor_encode_batch(ctx, k_, s.maxLen, B, s.d_in, (size_t)k_ * s.slot, s.d_out, s.slot, s.slot,
+                                  FEC_DEVICE);
+    if (rc) return codec_rc(rc);
+    if ((h = hipMemcpyAsync(s.h_out, s.d_out, B * (size_t)m_ * s.slot, hipMemcpyDeviceToHost, st)) != hipSuccess)
+        return hip_error(h, "hipMemcpyAsync D2H");
+    if ((h = hipEventRecord((hipEvent_t)s.done, st)) != hipSuccess) return hip_error(h, "hipEventRecord");
+    s.inFlight = true;
+    s.delivered = 0;
+    cur_ ^= 1;
+    // the other set becomes the staging set: retire it if its batch is still out
+    Set& next = sets_[cur_];
+    if (next.inFlight) {
+        if ((e = waitSet(next)).ok()) e = deliver(next, delivered);
+        if (!e.ok()) return e;
+    }
+    return Error::nil();
+}
+
+Error BatchEncoder::waitSet(Set& s) {
+    const hipError_t h = hipEventSynchronize((hipEvent_t)s.done);
+    return h == hipSuccess ? Error::nil() : hip_error(h, "hipEventSynchronize");
+}
+
+Error BatchEncoder::deliver(Set& s, size_t* blocks) {
+    const size_t B = s.blocks.size();
+    for (; s.delivered < B; ++s.delivered) {
+        const Pending& p = s.blocks[s.delivered];
+        if (p.q->Len() + (size_t)m_ > p.q->MaxLen()) return Error::text("repair queue full");
+        for (int i = 0; i < m_; ++i) {
+            // repairSymbols makes RS payloads as make([]byte, 0, MaxPacketBufferSize)[:L']
+            // (reed_solomon.go:44-49) and the XOR payload as make([]byte, L) (xor.go:28-33)
+            Slice pl = rs_ ? Slice::make(0, kMaxPacketBufferSize).reslice(0, p.len) : Slice::make(p.len, p.len);
+            memcpy(pl.data(), s.h_out + (s.delivered * (size_t)m_ + i) * s.slot, p.len);
+            Error e = p.q->Add(RepairFrame{p.id, (ParityID)i, pl});
+            if (!e.ok()) return e;
+        }
+        if (blocks) ++*blocks;
+    }
+    s.blocks.clear();
+    s.maxLen = 0;
+    s.delivered = 0;
+    s.inFlight = false;
+    return Error::nil();
+}
+
+Error BatchEncoder::Poll(size_t* blocks) {
+    if (blocks) *blocks = 0;
+    // the older batch is the one not being staged
+    for (int i = 1; i >= 0; --i) {
+        Set& s = sets_[cur_ ^ i];
+        if (!s.inFlight) continue;
+        const hipError_t h = hipEventQuery((hipEvent_t)s.done);
+        if (h == hipErrorNotReady) break;   // later batches complete later (one stream)
+        if (h != hipSuccess) return hip_error(h, "hipEventQuery");
+        Error e = deliver(s, blocks);
+        if (!e.ok()) return e;
+    }
+    return Error::nil();
+}
+
+Error BatchEncoder::Drain(size_t* blocks) {
+    size_t before = 0;
+    Error e = flushImpl(&before);   // may retire (and deliver) the older batch
+    if (blocks) *blocks = 0;
+    if (!e.ok()) return e;
+    for (int i = 1; i >= 0; --i) {
+        Set& s = sets_[cur_ ^ i];
+        if (!s.inFlight) continue;
+        if (!(e = waitSet(s)).ok()) return e;
+        size_t n = 0;
+        if (!(e = deliver(s, &n)).ok()) return e;
+        before += n;
+    }
+    if (blocks) *blocks = before;
+    return Error::nil();
+}
+
+size_t BatchEncoder::Staged() const { return sets_[cur_].blocks.size(); }
+
+size_t BatchEncoder::InFlight() const {
+    const Set& o = sets_[cur_ ^ 1];
+    return o.inFlight ? o.blocks.size() - o.delivered : 0;
+}
+
+}  // namespace fec

@@ -11,7 +11,10 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 
+#include "../../include/fec_batch.h"
+#include "../../include/fec_batch.hpp"
 #include "../../include/fec_hip.h"
 #include "../../include/fec_scheme.h"
 
@@ -159,38 +162,53 @@ Error ReedSolomonScheme::addLengthToSourceSymbolPayload(Block& b, SourceSymbolID
     return Error::nil();
 }
 
-Error ReedSolomonScheme::repairSymbols(Block& b, std::vector<RepairFrame>* out) {   // reed_solomon.go:26-68
-    out->clear();
+Error ReedSolomonScheme::stageRepairInput(Block& b, uint8_t* dst, size_t stride, size_t* shard_len) {
+    // reed_solomon.go:26-51, up to the enc.Encode call: the same checks in the same order
     if (!b.isComplete()) return Error::text(kIncomplete);
     if (b.biggestSourceSymbolLenSoFar > (int)kMaxFECPacketBufferSize) return too_big(b.biggestSourceSymbolLenSoFar);
-    const int nsh = b.totNumSourceSymbols + b.totNumRepairSymbols;
-    std::vector<Slice> shards(nsh > 0 ? nsh : 0);
-    for (int i = 0; i < b.totNumSourceSymbols; ++i) {
-        Error e = addLengthToSourceSymbolPayload(b, b.smallestSSID + (SourceSymbolID)i, &shards[i]);
-        if (!e.ok()) return e;
-    }
     const size_t L = kRepairPayloadMetadataLen + (size_t)b.biggestSourceSymbolLenSoFar;
-    for (int i = 0; i < b.totNumRepairSymbols; ++i)
-        shards[b.totNumSourceSymbols + i] = Slice::make(0, kMaxPacketBufferSize).reslice(0, L);
+    for (int i = 0; i < b.totNumSourceSymbols; ++i) {
+        Slice shard;
+        Error e = addLengthToSourceSymbolPayload(b, b.smallestSSID + (SourceSymbolID)i, &shard);
+        if (!e.ok()) return e;
+        if (i < k_) {
+            if (L > stride) return Error::text(fmt("shard len (%zu) exceeds the staging slot (%zu)", L, stride));
+            memcpy(dst + (size_t)i * stride, shard.data(), L);
+            memset(dst + (size_t)i * stride + L, 0, std::min(stride, (L + 15) & ~(size_t)15) - L);
+        }
+    }
     // enc.Encode(shards): klauspost checks the shard count, then encodes shards[k:] from shards[:k]
-    if (nsh != k_ + m_) return Error::text(std::string("unable to make parity shards: ") + fec_strerror(FEC_ERR_TOO_FEW_SHARDS));
+    if (b.totNumSourceSymbols + b.totNumRepairSymbols != k_ + m_)
+        return Error::text(std::string("unable to make parity shards: ") + fec_strerror(FEC_ERR_TOO_FEW_SHARDS));
     if (L == 0) return Error::text(std::string("unable to make parity shards: ") + fec_strerror(FEC_ERR_SHARD_NO_DATA));
+    *shard_len = L;
+    return Error::nil();
+}
+
+Error ReedSolomonScheme::repairSymbols(Block& b, std::vector<RepairFrame>* out) {   // reed_solomon.go:26-68
+    out->clear();
+    const size_t stride = std::max<size_t>(1, kRepairPayloadMetadataLen + (size_t)std::max(0, b.biggestSourceSymbolLenSoFar));
+    std::vector<uint8_t> host((size_t)(k_ + m_) * stride);
+    size_t L = 0;
+    Error e = stageRepairInput(b, host.data(), stride, &L);
+    if (!e.ok()) return e;
+    const int nsh = k_ + m_;
     if (m_ > 0) {
         fec_ctx* ctx = nullptr;
-        Error e = engine_->ctx(&ctx);
+        e = engine_->ctx(&ctx);
         if (!e.ok()) return e;
-        std::vector<uint8_t> host((size_t)nsh * L);
-        for (int i = 0; i < k_; ++i) memcpy(&host[(size_t)i * L], shards[i].data(), L);
         const int rc = fec_rs_encode_batch(ctx, k_, m_, L, 1, host.data(), (size_t)nsh * L, host.data() + (size_t)k_ * L,
                                            (size_t)nsh * L, L, FEC_HOST);
         if (rc) return Error{std::string("unable to make parity shards: ") + fec_strerror(rc), rc};
-        for (int i = k_; i < nsh; ++i) memcpy(shards[i].data(), &host[(size_t)i * L], L);
     }
     out->resize(b.totNumRepairSymbols);
     for (int i = 0; i < b.totNumRepairSymbols; ++i) {
+        // repair shards: make([]byte, 0, MaxPacketBufferSize)[:L'] (reed_solomon.go:44-49)
+        Slice rep = Slice::make(0, kMaxPacketBufferSize).reslice(0, L);
+        memcpy(rep.data(), &host[(size_t)(k_ + i) * L], L);
         (*out)[i].block_id = b.id;
         (*out)[i].parity_id = (ParityID)i;
-        (*out)[i].payload = shards[b.totNumSourceSymbols + i];
+        (*out)[i].payload = rep;
     }
     return Error::nil();
 }
@@ -289,23 +307,39 @@ static Error xor_reduce(std::shared_ptr<Engine>& engine, std::vector<uint8_t>& s
     return rc ? codec_error(rc) : Error::nil();
 }
 
-Error XorScheme::repairSymbols(Block& b, std::vector<RepairFrame>* out) {   // xor.go:14-42
-    out->clear();
+Error XorScheme::stageRepairInput(Block& b, uint8_t* dst, size_t stride, size_t* shard_len, int* count) {
+    // xor.go:14-33: the same checks in the same order, then every source framed into a slot
     if (!b.isComplete()) return Error::text(kIncomplete);
     if (b.totNumRepairSymbols != 1)
         return Error::text(fmt("xor only supports 1 repair symbol. Expected 1, received %d", b.totNumRepairSymbols));
     if (b.biggestSourceSymbolLenSoFar > (int)kMaxFECPacketBufferSize) return too_big(b.biggestSourceSymbolLenSoFar);
     if (b.biggestSourceSymbolLenSoFar < 0) return Error::text("negative repair payload length");
     const size_t L = kRepairPayloadMetadataLen + (size_t)b.biggestSourceSymbolLenSoFar;
-    const int count = (int)b.ssidToSourcePayload.size();
-    std::vector<uint8_t> shards((size_t)count * L);
+    if (L > stride) return Error::text(fmt("shard len (%zu) exceeds the staging slot (%zu)", L, stride));
     int i = 0;
-    for (auto& kv : b.ssidToSourcePayload)
-        if (!xor_frame(kv.second, b.biggestSourceSymbolLenSoFar, L, &shards[(size_t)(i++) * L]))
+    for (auto& kv : b.ssidToSourcePayload) {
+        uint8_t* slot = dst + (size_t)i * stride;
+        if (!xor_frame(kv.second, b.biggestSourceSymbolLenSoFar, L, slot))
             return Error::text(fmt("source payload of %zu bytes overruns the %zu-byte repair symbol",
                                    kv.second.len, L));   // Go: index out of range panic
+        memset(slot + L, 0, std::min(stride, (L + 15) & ~(size_t)15) - L);
+        ++i;
+    }
+    *shard_len = L;
+    *count = i;
+    return Error::nil();
+}
+
+Error XorScheme::repairSymbols(Block& b, std::vector<RepairFrame>* out) {   // xor.go:14-42
+    out->clear();
+    const size_t stride = kRepairPayloadMetadataLen + (size_t)std::max(0, b.biggestSourceSymbolLenSoFar);
+    std::vector<uint8_t> shards(b.ssidToSourcePayload.size() * stride + 1);
+    size_t L = 0;
+    int count = 0;
+    Error e = stageRepairInput(b, shards.data(), stride, &L, &count);
+    if (!e.ok()) return e;
     Slice rep = Slice::make(L, L);
-    Error e = xor_reduce(engine_, shards, count, L, rep.data());
+    e = xor_reduce(engine_, shards, count, L, rep.data());
     if (!e.ok()) return e;
     out->resize(1);
     (*out)[0].block_id = b.id;
@@ -393,6 +427,22 @@ Error Manager::AddSourceSymbolFrame(const SourceSymbolFrame& f, std::vector<Repa
         bs.block.reset();
         bs.isProcessed = true;
         *out = std::move(rep);
+    }
+    return Error::nil();
+}
+
+Error Manager::AddSourceSymbolFrameBatched(const SourceSymbolFrame& f, BatchEncoder* enc, RepairQueue* q) {
+    // manager.go:123-158 with repairSymbols replaced by staging into the batch encoder
+    if (!enc) return Error::text("nil batch encoder");
+    BlockStatus& bs = statusFor(sidToBlockID(f.ssid));
+    if (bs.isProcessed) return Error::nil();
+    Error e = bs.block->addSourceSymbol(f);
+    if (!e.ok()) return e;
+    if (bs.block->isComplete()) {
+        e = enc->Submit(*bs.block, q);
+        if (!e.ok()) return e;
+        bs.block.reset();
+        bs.isProcessed = true;
     }
     return Error::nil();
 }
@@ -686,6 +736,96 @@ int fec_manager_handle_source_symbol_frame(fec_manager* m, uint64_t ssid, const 
         report(m->m->HandleSourceSymbolFrame(fec::SourceSymbolFrame{ssid, fec::Slice::from(p, len, cap)}, &r));
     if (rc == FEC_OK && !r.nil()) *out = new fec_bytes{r};
     return rc;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ C ABI (include/fec_batch.h)
+
+struct fec_repair_queue {
+    std::unique_ptr<fec::RepairQueue> q;
+    std::atomic<uint64_t> has_data{0};
+};
+struct fec_batch_encoder {
+    std::unique_ptr<fec::BatchEncoder> e;
+};
+
+extern "C" {
+
+fec_repair_queue* fec_repair_queue_new(size_t max_len) {
+    fec_repair_queue* r = new fec_repair_queue();
+    r->q.reset(new fec::RepairQueue([r] { r->has_data.fetch_add(1); },
+                                    max_len ? max_len : fec::RepairQueue::kMaxRepairSendQueueLen));
+    return r;
+}
+
+void fec_repair_queue_free(fec_repair_queue* q) { delete q; }
+
+int fec_repair_queue_add(fec_repair_queue* q, uint64_t block_id, uint64_t parity_id, const uint8_t* p, size_t len) {
+    if (!q || (len && !p)) return FEC_ERR_INVALID_ARG;
+    return report(q->q->Add(fec::RepairFrame{block_id, parity_id, fec::Slice::from(p, len, len)}));
+}
+
+int fec_repair_queue_peek(fec_repair_queue* q, uint64_t* block_id, uint64_t* parity_id, const uint8_t** payload,
+                          size_t* len, size_t* cap) {
+    if (!q) return FEC_ERR_INVALID_ARG;
+    const fec::RepairFrame* f = q->q->Peek();
+    if (!f) return 0;
+    if (block_id) *block_id = f->block_id;
+    if (parity_id) *parity_id = f->parity_id;
+    if (payload) *payload = f->payload.data();
+    if (len) *len = f->payload.len;
+    if (cap) *cap = f->payload.cap;
+    return 1;
+}
+
+void fec_repair_queue_pop(fec_repair_queue* q) {
+    if (q) q->q->Pop();
+}
+
+size_t fec_repair_queue_len(fec_repair_queue* q) { return q ? q->q->Len() : 0; }
+
+uint64_t fec_repair_queue_has_data_calls(fec_repair_queue* q) { return q ? q->has_data.load() : 0; }
+
+void fec_repair_queue_close(fec_repair_queue* q, const char* msg) {
+    if (q) q->q->CloseWithError(fec::Error::text(msg && *msg ? msg : "closed"));
+}
+
+fec_batch_encoder* fec_batch_encoder_new(int scheme_id, int k, int m, size_t max_blocks, int device, int* err) {
+    std::unique_ptr<fec::BatchEncoder> e;
+    const int rc = report(fec::BatchEncoder::New((fec::DecoderFECScheme)scheme_id, k, m, max_blocks,
+                                                 engine_for(device), &e));
+    if (err) *err = rc;
+    if (rc) return nullptr;
+    return new fec_batch_encoder{std::move(e)};
+}
+
+void fec_batch_encoder_free(fec_batch_encoder* e) { delete e; }
+
+int fec_batch_encoder_submit(fec_batch_encoder* e, fec_block* b, fec_repair_queue* q) {
+    if (!e || !b || !q) return FEC_ERR_INVALID_ARG;
+    return report(e->e->Submit(b->b, q->q.get()));
+}
+
+int fec_batch_encoder_flush(fec_batch_encoder* e) { return e ? report(e->e->Flush()) : FEC_ERR_INVALID_ARG; }
+
+int fec_batch_encoder_poll(fec_batch_encoder* e, size_t* blocks) {
+    return e ? report(e->e->Poll(blocks)) : FEC_ERR_INVALID_ARG;
+}
+
+int fec_batch_encoder_drain(fec_batch_encoder* e, size_t* blocks) {
+    return e ? report(e->e->Drain(blocks)) : FEC_ERR_INVALID_ARG;
+}
+
+size_t fec_batch_encoder_staged(const fec_batch_encoder* e) { return e ? e->e->Staged() : 0; }
+
+size_t fec_batch_encoder_in_flight(const fec_batch_encoder* e) { return e ? e->e->InFlight() : 0; }
+
+int fec_manager_add_source_symbol_frame_batched(fec_manager* m, uint64_t ssid, const uint8_t* p, size_t len,
+                                                size_t cap, fec_batch_encoder* e, fec_repair_queue* q) {
+    if (!m || !e || !q || (len && !p)) return FEC_ERR_INVALID_ARG;
+    fec::SourceSymbolFrame f{ssid, fec::Slice::from(p, len, cap)};
+    return report(m->m->AddSourceSymbolFrameBatched(f, e->e.get(), q->q.get()));
 }
 
 }  // extern "C"

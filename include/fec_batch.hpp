@@ -1,0 +1,125 @@
+// fec_batch.hpp — the sender-side batching layer the GPU needs.
+//
+// In the reference, repair symbols are generated synchronously, one block at a time, inside
+// the packet packer (packet_packer.go:1001-1011 -> manager.go:145 -> reed_solomon.go:51), and
+// queued per connection in a 32-frame ring (repair_queue.go:17-99). A GPU launch per block
+// costs more than the reference's whole per-block encode, so here the encode is deferred:
+//
+//   RepairQueue   repair_queue.go restated (Add / Peek / Pop / CloseWithError, hasData
+//                 callback, the 32-frame limit). The reference panics when full; the mirror
+//                 returns the error "repair queue full" instead. The limit is a constructor
+//                 argument because a batch delivers many blocks' frames at once.
+//   BatchEncoder  collects complete blocks from any number of connections (each with its own
+//                 RepairQueue) into pinned staging, [block][k][S] with S = the batch's 16-byte
+//                 slot; Flush() issues one H2D copy, one encode launch and one D2H copy on the
+//                 encoder's stream and returns; Poll() hands the repair frames of completed
+//                 batches to their queues in submission order. Two staging sets: a batch
+//                 stages while the previous one is in flight.
+//
+// Frames are bit-identical to the per-block path: a block's repair payload is the first
+// L = biggest + 2 bytes of its parity shards, and zero padding of the other blocks of the
+// batch (shard_len = the batch's largest L) does not change those bytes (the code is
+// byte-wise). Payloads are made as repairSymbols makes them (make(0, 1452)[:L] for RS,
+// make(L, L) for XOR).
+#pragma once
+
+#include <stdint.h>
+
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "fec_scheme.hpp"
+
+namespace fec {
+
+// repair_queue.go:17-99
+class RepairQueue {
+public:
+    static constexpr size_t kMaxRepairSendQueueLen = 32;   // repair_queue.go:14
+
+    explicit RepairQueue(std::function<void()> hasData = nullptr, size_t maxLen = kMaxRepairSendQueueLen)
+        : hasData_(std::move(hasData)), maxLen_(maxLen) {}
+    // Add queues a new REPAIR frame for sending (repair_queue.go:40-69).
+    Error Add(RepairFrame f);
+    // Peek gets the next REPAIR frame for sending; nullptr when empty (repair_queue.go:73-80).
+    // The pointer stays valid until the next Pop.
+    const RepairFrame* Peek();
+    // Pop removes the frame Peek returned (repair_queue.go:82-90).
+    void Pop();
+    // CloseWithError (repair_queue.go:92-95): later Adds return the error.
+    void CloseWithError(Error e);
+    size_t Len();
+    size_t MaxLen() const { return maxLen_; }
+
+private:
+    std::mutex mu_;
+    std::deque<RepairFrame> q_;
+    std::function<void()> hasData_;
+    size_t maxLen_;
+    bool closed_ = false;
+    Error closeErr_;
+};
+
+class BatchEncoder {
+public:
+    // scheme: ReedSolomonFECScheme (k, m) or XORFECScheme (k, 1). maxBlocks: blocks per batch.
+    static Error New(DecoderFECScheme scheme, int k, int m, size_t maxBlocks, std::shared_ptr<Engine> engine,
+                     std::unique_ptr<BatchEncoder>* out);
+    ~BatchEncoder();
+
+    // Validate (exactly as repairSymbols: same errors, same order) and stage a complete block;
+    // its frames go to q when its batch completes. A full batch, or a block whose shards do not
+    // fit the batch's slot, flushes first.
+    Error Submit(Block& b, RepairQueue* q);
+    // Start encoding the staged blocks (asynchronous). No-op when nothing is staged.
+    Error Flush();
+    // Deliver the frames of every completed batch (non-blocking); *blocks = blocks delivered.
+    Error Poll(size_t* blocks = nullptr);
+    // Flush, wait for every batch and deliver.
+    Error Drain(size_t* blocks = nullptr);
+    size_t Staged() const;     // blocks staged, not yet flushed
+    size_t InFlight() const;   // blocks flushed, not yet delivered
+    int k() const { return k_; }
+    int m() const { return m_; }
+    DecoderFECScheme scheme() const { return scheme_; }
+
+private:
+    struct Pending {
+        RepairQueue* q;
+        BlockID id;
+        size_t len;
+    };
+    struct Set {
+        uint8_t* h_in = nullptr;    // pinned [maxBlocks][k][kSlotMax]
+        uint8_t* h_out = nullptr;   // pinned [maxBlocks][m][kSlotMax]
+        uint8_t* d_in = nullptr;
+        uint8_t* d_out = nullptr;
+        void* done = nullptr;       // hipEvent_t
+        std::vector<Pending> blocks;
+        size_t slot = 0;            // S of this batch (16-byte multiple)
+        size_t maxLen = 0;          // largest L of this batch
+        size_t delivered = 0;       // blocks of a completed batch already delivered
+        bool inFlight = false;
+    };
+    BatchEncoder(DecoderFECScheme scheme, int k, int m, size_t maxBlocks, std::shared_ptr<Engine> e)
+        : scheme_(scheme), k_(k), m_(m), maxBlocks_(maxBlocks), engine_(std::move(e)) {}
+    Error init();
+    Error flushImpl(size_t* delivered);
+    Error waitSet(Set& s);
+    Error deliver(Set& s, size_t* blocks);
+
+    DecoderFECScheme scheme_;
+    int k_, m_;
+    size_t maxBlocks_;
+    std::shared_ptr<Engine> engine_;
+    std::unique_ptr<ReedSolomonScheme> rs_;
+    std::unique_ptr<XorScheme> xor_;
+    Set sets_[2];
+    int cur_ = 0;   // the set being staged
+    bool ready_ = false;
+};
+
+}  // namespace fec

@@ -123,6 +123,10 @@ public:
     Error recoverSymbolPayloads(Block& b, Slice* out) override;
     int dataShards() const { return k_; }
     int parityShards() const { return m_; }
+    // repairSymbols up to the enc.Encode call (same checks, same errors, same order): writes the
+    // block's k framed shards to dst + i*stride (zero pad to the 16-byte boundary) and their
+    // length L. The batch encoder (fec_batch.hpp) stages blocks with it.
+    Error stageRepairInput(Block& b, uint8_t* dst, size_t stride, size_t* shard_len);
 
 private:
     ReedSolomonScheme(int k, int m, std::shared_ptr<Engine> e) : k_(k), m_(m), engine_(std::move(e)) {}
@@ -137,6 +141,9 @@ public:
     explicit XorScheme(std::shared_ptr<Engine> engine) : engine_(std::move(engine)) {}
     Error repairSymbols(Block& b, std::vector<RepairFrame>* out) override;
     Error recoverSymbolPayloads(Block& b, Slice* out) override;
+    // repairSymbols up to the XOR reduction: the sources framed (payload, BE16 length XORed at
+    // [biggest]) into dst + i*stride, their count and length L.
+    Error stageRepairInput(Block& b, uint8_t* dst, size_t stride, size_t* shard_len, int* count);
 
 private:
     std::shared_ptr<Engine> engine_;
@@ -153,6 +160,11 @@ public:
     Error HandleSourceSymbolFrame(const SourceSymbolFrame& f, Slice* out);
     BlockID sidToBlockID(SourceSymbolID sid) const;
     size_t trackedBlocks() const { return blockStatuses_.size(); }
+    // AddSourceSymbolFrame with the encode deferred to a batch: on the k-th source symbol the
+    // block is staged into `enc` (validated exactly as repairSymbols would), dropped and marked
+    // processed; its repair frames reach `q` when the batch completes (fec_batch.hpp).
+    Error AddSourceSymbolFrameBatched(const SourceSymbolFrame& f, class BatchEncoder* enc, class RepairQueue* q);
+    BlockFECScheme* scheme() { return scheme_.get(); }
 
 private:
     struct BlockStatus {
