@@ -9,7 +9,7 @@
 import ctypes
 
 from . import lib, FEC_OK
-from .scheme import MAX_PACKET_BUFFER_SIZE, Manager, _err
+from .scheme import MAX_PACKET_BUFFER_SIZE, Manager, _bytes, _err
 
 _vp, _sz, _i, _u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
 
@@ -42,6 +42,26 @@ lib.fec_batch_encoder_staged.argtypes = [_vp]
 lib.fec_batch_encoder_in_flight.restype = _sz
 lib.fec_batch_encoder_in_flight.argtypes = [_vp]
 lib.fec_manager_add_source_symbol_frame_batched.argtypes = [_vp, _u64, ctypes.c_char_p, _sz, _sz, _vp, _vp]
+lib.fec_recovered_queue_new.restype = _vp
+lib.fec_recovered_queue_new.argtypes = []
+lib.fec_recovered_queue_free.argtypes = [_vp]
+lib.fec_recovered_queue_free.restype = None
+lib.fec_recovered_queue_len.restype = _sz
+lib.fec_recovered_queue_len.argtypes = [_vp]
+lib.fec_recovered_queue_pop.argtypes = [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_vp)]
+lib.fec_batch_decoder_new.restype = _vp
+lib.fec_batch_decoder_new.argtypes = [_i, _i, _i, _sz, _i, ctypes.POINTER(_i)]
+lib.fec_batch_decoder_free.argtypes = [_vp]
+lib.fec_batch_decoder_free.restype = None
+lib.fec_batch_decoder_submit.argtypes = [_vp, _vp, _vp, ctypes.POINTER(_i)]
+lib.fec_batch_decoder_flush.argtypes = [_vp]
+lib.fec_batch_decoder_poll.argtypes = [_vp, ctypes.POINTER(_sz)]
+lib.fec_batch_decoder_drain.argtypes = [_vp, ctypes.POINTER(_sz)]
+lib.fec_batch_decoder_staged.restype = _sz
+lib.fec_batch_decoder_staged.argtypes = [_vp]
+lib.fec_batch_decoder_in_flight.restype = _sz
+lib.fec_batch_decoder_in_flight.argtypes = [_vp]
+lib.fec_manager_handle_repair_frame_batched.argtypes = [_vp, _u64, _u64, ctypes.c_char_p, _sz, _vp, _vp]
 
 
 class RepairQueue:
@@ -151,3 +171,92 @@ def add_source_symbol_frame_batched(manager, ssid, payload, encoder, queue, cap=
 Manager.add_source_symbol_frame_batched = (
     lambda self, ssid, payload, encoder, queue, cap=MAX_PACKET_BUFFER_SIZE:
     add_source_symbol_frame_batched(self, ssid, payload, encoder, queue, cap))
+
+
+class RecoveredQueue:
+    """Recovered payloads of one connection, in the order their blocks became recoverable."""
+
+    def __init__(self):
+        self._h = lib.fec_recovered_queue_new()
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib.fec_recovered_queue_free(self._h)
+            self._h = None
+
+    def __len__(self):
+        return lib.fec_recovered_queue_len(self._h)
+
+    def pop(self):
+        bid, out = _u64(), _vp()
+        if not lib.fec_recovered_queue_pop(self._h, ctypes.byref(bid), ctypes.byref(out)):
+            return None
+        return bid.value, _bytes(out.value)
+
+    def drain(self):
+        out = []
+        while True:
+            it = self.pop()
+            if it is None:
+                return out
+            out.append(it)
+
+
+class BatchDecoder:
+    """Deferred, batched recoverSymbolPayloads over many blocks (fec_batch.hpp)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def new(cls, scheme_id, k, m, max_blocks=1024, device=0):
+        err = _i(0)
+        h = lib.fec_batch_decoder_new(scheme_id, k, m, max_blocks, device, ctypes.byref(err))
+        if err.value != FEC_OK:
+            return None, lib.fec_last_error().decode()
+        return cls(h), None
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib.fec_batch_decoder_free(self._h)
+            self._h = None
+
+    def submit(self, block, queue):
+        """-> (staged, err); staged False for an already complete block (nil, nil)."""
+        st = _i(0)
+        rc = lib.fec_batch_decoder_submit(self._h, block._h, queue._h, ctypes.byref(st))
+        return bool(st.value), _err(rc)
+
+    def flush(self):
+        return _err(lib.fec_batch_decoder_flush(self._h))
+
+    def poll(self):
+        n = _sz()
+        rc = lib.fec_batch_decoder_poll(self._h, ctypes.byref(n))
+        return n.value, _err(rc)
+
+    def drain(self):
+        n = _sz()
+        rc = lib.fec_batch_decoder_drain(self._h, ctypes.byref(n))
+        return n.value, _err(rc)
+
+    @property
+    def staged(self):
+        return lib.fec_batch_decoder_staged(self._h)
+
+    @property
+    def in_flight(self):
+        return lib.fec_batch_decoder_in_flight(self._h)
+
+
+def handle_repair_frame_batched(manager, block_id, parity_id, payload, decoder, queue):
+    """Manager.HandleRepairFrame (manager.go:160-198) with the recovery deferred to `decoder`;
+    the recovered payload reaches `queue` when its batch completes. Returns err."""
+    payload = bytes(payload)
+    return _err(lib.fec_manager_handle_repair_frame_batched(manager._h, block_id, parity_id, payload, len(payload),
+                                                            decoder._h, queue._h))
+
+
+Manager.handle_repair_frame_batched = (
+    lambda self, block_id, parity_id, payload, decoder, queue:
+    handle_repair_frame_batched(self, block_id, parity_id, payload, decoder, queue))

@@ -254,3 +254,260 @@ size_t BatchEncoder::InFlight() const {
 }
 
 }  // namespace fec
+
+namespace fec {
+
+// ------------------------------------------------------------------ RecoveredQueue
+
+void RecoveredQueue::Push(Item it) {
+    std::lock_guard<std::mutex> lk(mu_);
+    q_.push_back(std::move(it));
+}
+
+bool RecoveredQueue::Pop(Item* out) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (q_.empty()) return false;
+    *out = std::move(q_.front());
+    q_.pop_front();
+    return true;
+}
+
+size_t RecoveredQueue::Len() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return q_.size();
+}
+
+// ------------------------------------------------------------------ BatchDecoder
+
+Error BatchDecoder::New(DecoderFECScheme scheme, int k, int m, size_t maxBlocks, std::shared_ptr<Engine> engine,
+                        std::unique_ptr<BatchDecoder>* out) {
+    out->reset();
+    if (maxBlocks == 0) return Error::text("batch must hold at least one block");
+    std::unique_ptr<BatchDecoder> d(new BatchDecoder(scheme, k, m, maxBlocks, std::move(engine)));
+    if (scheme == ReedSolomonFECScheme) {
+        Error err = ReedSolomonScheme::New(k, m, d->engine_, &d->rs_);
+        if (!err.ok()) return err;
+        if (k + m > FEC_MAX_DECODE_SHARDS) return codec_rc(FEC_ERR_MAX_SHARD_NUM);
+    } else if (scheme == XORFECScheme) {
+        if (m != 1) return Error::text("xor only supports 1 repair symbol");
+        if (k < 1 || k > 255) return Error::text("invalid number of source symbols");
+        d->xor_.reset(new XorScheme(d->engine_));
+    } else {
+        return Error::text("no FEC scheme");
+    }
+    *out = std::move(d);
+    return Error::nil();
+}
+
+BatchDecoder::~BatchDecoder() {
+    for (Set& s : sets_) {
+        if (s.inFlight && s.done) (void)hipEventSynchronize((hipEvent_t)s.done);
+        if (s.done) (void)hipEventDestroy((hipEvent_t)s.done);
+        for (void* p : {(void*)s.h_in, (void*)s.h_out, (void*)s.h_masks, (void*)s.h_status})
+            if (p) (void)hipHostFree(p);
+        for (void* p : {(void*)s.d_in, (void*)s.d_out, (void*)s.d_masks, (void*)s.d_status})
+            if (p) (void)hipFree(p);
+    }
+}
+
+Error BatchDecoder::init() {
+    fec_ctx* ctx = nullptr;
+    Error e = engine_->ctx(&ctx);
+    if (!e.ok()) return e;
+    const size_t n = (size_t)k_ + m_;
+    const size_t in_bytes = maxBlocks_ * n * kSlotMax, out_bytes = maxBlocks_ * (size_t)m_ * kSlotMax;
+    for (Set& s : sets_) {
+        hipError_t h;
+        if ((h = hipHostMalloc(&s.h_in, in_bytes, hipHostMallocDefault)) != hipSuccess ||
+            (h = hipHostMalloc(&s.h_out, out_bytes, hipHostMallocDefault)) != hipSuccess ||
+            (h = hipHostMalloc(&s.h_masks, maxBlocks_ * 4, hipHostMallocDefault)) != hipSuccess ||
+            (h = hipHostMalloc(&s.h_status, maxBlocks_ * 4, hipHostMallocDefault)) != hipSuccess ||
+            (h = hipMalloc(&s.d_in, in_bytes)) != hipSuccess || (h = hipMalloc(&s.d_out, out_bytes)) != hipSuccess ||
+            (h = hipMalloc(&s.d_masks, maxBlocks_ * 4)) != hipSuccess ||
+            (h = hipMalloc(&s.d_status, maxBlocks_ * 4)) != hipSuccess)
+            return hip_error(h, "staging allocation");
+        hipEvent_t ev;
+        if ((h = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hip_error(h, "hipEventCreate");
+        s.done = ev;
+    }
+    ready_ = true;
+    return Error::nil();
+}
+
+Error BatchDecoder::stage(Block& b, uint8_t* dst, size_t slot, Pending* p, bool* nothing) {
+    *nothing = false;
+    p->id = b.id;
+    p->meta = Block{};
+    p->meta.id = b.id;
+    p->meta.totNumSourceSymbols = b.totNumSourceSymbols;
+    p->meta.totNumRepairSymbols = b.totNumRepairSymbols;
+    p->meta.smallestSSID = b.smallestSSID;
+    p->meta.largestSSID = b.largestSSID;
+    p->meta.biggestSourceSymbolLenSoFar = b.biggestSourceSymbolLenSoFar;
+    if (rs_) {
+        Error e = rs_->stageRecoverInput(b, dst, slot, &p->plan);
+        if (!e.ok()) return e;
+        *nothing = p->plan.nothing;
+        return Error::nil();
+    }
+    int count = 0;
+    Error e = xor_->stageRecoverInput(b, dst, slot, (size_t)k_, nothing, &count);
+    if (!e.ok()) return e;
+    p->plan = ReedSolomonScheme::RecoverPlan{};
+    p->plan.len = slot;
+    return Error::nil();
+}
+
+Error BatchDecoder::Submit(Block& b, RecoveredQueue* q, bool* staged) {
+    if (staged) *staged = false;
+    if (!q) return Error::text("nil recovered queue");
+    size_t want = kRepairPayloadMetadataLen + (size_t)std::max(0, b.biggestSourceSymbolLenSoFar);
+    for (auto& kv : b.pidToRepairPayload) want = std::max(want, kv.second.len);
+    want = std::min(kSlotMax, std::max<size_t>(16, round16(want)));
+    const size_t n = (size_t)k_ + m_;
+    bool nothing = false;
+    Pending p;
+    if (!ready_) {   // validate before any device work
+        std::vector<uint8_t> scratch(n * kSlotMax);
+        Error e = stage(b, scratch.data(), kSlotMax, &p, &nothing);
+        if (!e.ok() || nothing) return e;
+        if (!(e = init()).ok()) return e;
+    }
+    Set* s = &sets_[cur_];
+    if (s->inFlight) {
+        Error e = waitSet(*s);
+        if (e.ok()) e = deliver(*s, nullptr);
+        if (!e.ok()) return e;
+    }
+    if (!s->blocks.empty() && (s->blocks.size() >= maxBlocks_ || want > s->slot)) {
+        Error e = flushImpl(nullptr);
+        if (!e.ok()) return e;
+        s = &sets_[cur_];
+    }
+    if (s->blocks.empty()) s->slot = want;
+    const size_t idx = s->blocks.size();
+    Error e = stage(b, s->h_in + idx * n * s->slot, s->slot, &p, &nothing);
+    if (!e.ok() || nothing) return e;
+    s->h_masks[idx] = p.plan.mask;
+    s->maxLen = std::max(s->maxLen, rs_ ? p.plan.len : s->slot);
+    s->outSlots = std::max(s->outSlots, rs_ ? p.plan.missing.size() : (size_t)1);
+    p.q = q;
+    s->blocks.push_back(std::move(p));
+    if (staged) *staged = true;
+    return Error::nil();
+}
+
+Error BatchDecoder::Flush() { return flushImpl(nullptr); }
+
+Error BatchDecoder::flushImpl(size_t* delivered) {
+    Set& s = sets_[cur_];
+    if (s.inFlight) {
+        Error e = waitSet(s);
+        if (e.ok()) e = deliver(s, delivered);
+        if (!e.ok()) return e;
+    }
+    if (s.blocks.empty()) return Error::nil();
+    fec_ctx* ctx = nullptr;
+    Error e = engine_->ctx(&ctx);
+    if (!e.ok()) return e;
+    hipStream_t st = (hipStream_t)fec_ctx_stream(ctx);
+    const size_t B = s.blocks.size(), n = (size_t)k_ + m_, S = s.slot;
+    const size_t nin = rs_ ? n : (size_t)k_;   // XOR stages its k inputs only
+    hipError_t h = hipMemcpyAsync(s.d_in, s.h_in, B * n * S, hipMemcpyHostToDevice, st);
+    if (h != hipSuccess) return hip_error(h, "hipMemcpyAsync H2D");
+    int rc;
+    if (rs_) {
+        if ((h = hipMemcpyAsync(s.d_masks, s.h_masks, B * 4, hipMemcpyHostToDevice, st)) != hipSuccess)
+            return hip_error(h, "hipMemcpyAsync H2D");
+        rc = fec_rs_recover_batch(ctx, k_, m_, s.maxLen, B, s.d_in, n * S, s.d_in + (size_t)k_ * S, n * S, S,
+                                  s.d_masks, s.d_out, s.outSlots * S, (int)s.outSlots, s.d_status, FEC_DEVICE);
+    } else {
+        rc = fec_xor_encode_batch(ctx, (int)nin, s.maxLen, B, s.d_in, n * S, s.d_out, S, S, FEC_DEVICE);
+    }
+    if (rc) return codec_rc(rc);
+    if ((h = hipMemcpyAsync(s.h_out, s.d_out, B * s.outSlots * S, hipMemcpyDeviceToHost, st)) != hipSuccess)
+        return hip_error(h, "hipMemcpyAsync D2H");
+    if (rs_ && (h = hipMemcpyAsync(s.h_status, s.d_status, B * 4, hipMemcpyDeviceToHost, st)) != hipSuccess)
+        return hip_error(h, "hipMemcpyAsync D2H");
+    if ((h = hipEventRecord((hipEvent_t)s.done, st)) != hipSuccess) return hip_error(h, "hipEventRecord");
+    s.inFlight = true;
+    s.delivered = 0;
+    cur_ ^= 1;
+    Set& next = sets_[cur_];
+    if (next.inFlight) {
+        if ((e = waitSet(next)).ok()) e = deliver(next, delivered);
+        if (!e.ok()) return e;
+    }
+    return Error::nil();
+}
+
+Error BatchDecoder::waitSet(Set& s) {
+    const hipError_t h = hipEventSynchronize((hipEvent_t)s.done);
+    return h == hipSuccess ? Error::nil() : hip_error(h, "hipEventSynchronize");
+}
+
+Error BatchDecoder::deliver(Set& s, size_t* blocks) {
+    const size_t B = s.blocks.size(), S = s.slot;
+    for (; s.delivered < B; ++s.delivered) {
+        Pending& p = s.blocks[s.delivered];
+        Slice out;
+        Error e;
+        if (rs_) {
+            if (s.h_status[s.delivered] != (int32_t)p.plan.missing.size())
+                return codec_rc(s.h_status[s.delivered] < 0 ? s.h_status[s.delivered] : FEC_ERR_HIP);
+            std::vector<const uint8_t*> rebuilt;
+            for (size_t r = 0; r < p.plan.missing.size(); ++r)
+                rebuilt.push_back(s.h_out + (s.delivered * s.outSlots + r) * S);
+            e = rs_->finishRecover(p.meta, p.plan, rebuilt.data(), &out);
+        } else {
+            e = xor_->finishRecover(p.meta, s.h_out + s.delivered * S, S, &out);
+        }
+        if (!e.ok()) return e;
+        p.q->Push(RecoveredQueue::Item{p.id, out});
+        if (blocks) ++*blocks;
+    }
+    s.blocks.clear();
+    s.maxLen = s.outSlots = s.delivered = 0;
+    s.inFlight = false;
+    return Error::nil();
+}
+
+Error BatchDecoder::Poll(size_t* blocks) {
+    if (blocks) *blocks = 0;
+    for (int i = 1; i >= 0; --i) {
+        Set& s = sets_[cur_ ^ i];
+        if (!s.inFlight) continue;
+        const hipError_t h = hipEventQuery((hipEvent_t)s.done);
+        if (h == hipErrorNotReady) break;
+        if (h != hipSuccess) return hip_error(h, "hipEventQuery");
+        Error e = deliver(s, blocks);
+        if (!e.ok()) return e;
+    }
+    return Error::nil();
+}
+
+Error BatchDecoder::Drain(size_t* blocks) {
+    size_t before = 0;
+    Error e = flushImpl(&before);
+    if (blocks) *blocks = 0;
+    if (!e.ok()) return e;
+    for (int i = 1; i >= 0; --i) {
+        Set& s = sets_[cur_ ^ i];
+        if (!s.inFlight) continue;
+        if (!(e = waitSet(s)).ok()) return e;
+        size_t n = 0;
+        if (!(e = deliver(s, &n)).ok()) return e;
+        before += n;
+    }
+    if (blocks) *blocks = before;
+    return Error::nil();
+}
+
+size_t BatchDecoder::Staged() const { return sets_[cur_].blocks.size(); }
+
+size_t BatchDecoder::InFlight() const {
+    const Set& o = sets_[cur_ ^ 1];
+    return o.inFlight ? o.blocks.size() - o.delivered : 0;
+}
+
+}  // namespace fec

@@ -213,17 +213,22 @@ Error ReedSolomonScheme::repairSymbols(Block& b, std::vector<RepairFrame>* out) 
     return Error::nil();
 }
 
-Error ReedSolomonScheme::recoverSymbolPayloads(Block& b, Slice* out) {   // reed_solomon.go:92-136
-    *out = Slice{};
+Error ReedSolomonScheme::stageRecoverInput(Block& b, uint8_t* dst, size_t stride, RecoverPlan* plan) {
+    // reed_solomon.go:92-124, up to the enc.ReconstructData call: the same checks in the same
+    // order, then the present shards into dst + i*stride (n slots; absent slots untouched)
+    plan->nothing = false;
+    plan->missing.clear();
     if (!b.isRecoverable()) return Error::text(kNotRecoverable);
-    if (b.isComplete()) return Error::nil();
+    if (b.isComplete()) {
+        plan->nothing = true;   // nil, nil
+        return Error::nil();
+    }
     const int nsh = b.totNumSourceSymbols + b.totNumRepairSymbols;
     std::vector<Slice> shards(nsh > 0 ? nsh : 0);
-    std::vector<int> missing;
     for (int i = 0; i < b.totNumSourceSymbols; ++i) {
         const SourceSymbolID ssid = b.smallestSSID + (SourceSymbolID)i;
         if (!b.ssidToSourcePayload.count(ssid)) {
-            missing.push_back(i);
+            plan->missing.push_back(i);
             continue;
         }
         Error e = addLengthToSourceSymbolPayload(b, ssid, &shards[i]);
@@ -239,8 +244,8 @@ Error ReedSolomonScheme::recoverSymbolPayloads(Block& b, Slice* out) {   // reed
     // enc.ReconstructData(shards): klauspost shard-count / size / presence checks
     if (nsh != k_ + m_) return codec_error(FEC_ERR_TOO_FEW_SHARDS);
     size_t L = 0;
-    for (auto& s : shards)
-        if (!s.nil() && s.len) { L = s.len; break; }
+    for (auto& sh : shards)
+        if (!sh.nil() && sh.len) { L = sh.len; break; }
     if (L == 0) return codec_error(FEC_ERR_SHARD_NO_DATA);
     uint32_t mask = 0;
     int present = 0;
@@ -252,22 +257,25 @@ Error ReedSolomonScheme::recoverSymbolPayloads(Block& b, Slice* out) {   // reed
     }
     if (present < k_) return codec_error(FEC_ERR_TOO_FEW_SHARDS);
     if (nsh > FEC_MAX_DECODE_SHARDS) return codec_error(FEC_ERR_MAX_SHARD_NUM);
-    fec_ctx* ctx = nullptr;
-    Error e = engine_->ctx(&ctx);
-    if (!e.ok()) return e;
-    std::vector<uint8_t> host((size_t)nsh * L, 0);
+    if (L > stride) return Error::text(fmt("shard len (%zu) exceeds the staging slot (%zu)", L, stride));
     for (int i = 0; i < nsh; ++i)
-        if (mask >> i & 1u) memcpy(&host[(size_t)i * L], shards[i].data(), L);
-    int32_t st = 0;
-    const int rc = fec_rs_reconstruct_batch(ctx, k_, m_, L, 1, host.data(), (size_t)nsh * L, host.data() + (size_t)k_ * L,
-                                            (size_t)nsh * L, L, &mask, &st, FEC_HOST);
-    if (rc) return codec_error(rc);
-    // concatenation of the rebuilt payloads, each cut to its trailer length
+        if (mask >> i & 1u) {
+            memcpy(dst + (size_t)i * stride, shards[i].data(), L);
+            memset(dst + (size_t)i * stride + L, 0, std::min(stride, (L + 15) & ~(size_t)15) - L);
+        }
+    plan->len = L;
+    plan->mask = mask;
+    return Error::nil();
+}
+
+Error ReedSolomonScheme::finishRecover(const Block& b, const RecoverPlan& plan, const uint8_t* const* rebuilt,
+                                       Slice* out) {
+    // reed_solomon.go:126-135: concatenation of the rebuilt payloads, each cut to its trailer
+    const size_t L = plan.len;
     const int big = b.biggestSourceSymbolLenSoFar;
-    Slice res = Slice::make(0, missing.size() * (size_t)std::max(big, 0));
     std::vector<uint8_t> acc;
-    for (int i : missing) {
-        const uint8_t* sh = &host[(size_t)i * L];
+    for (size_t r = 0; r < plan.missing.size(); ++r) {
+        const uint8_t* sh = rebuilt[r];
         if (big < 0 || (size_t)big + 2 > L)   // Go: index out of range panic
             return Error::text(fmt("length trailer at %d outside shard of %zu bytes", big, L));
         const size_t payloadLen = ((size_t)sh[big] << 8) | sh[big + 1];
@@ -275,9 +283,35 @@ Error ReedSolomonScheme::recoverSymbolPayloads(Block& b, Slice* out) {   // reed
             return Error::text(fmt("recovered payload length %zu exceeds shard length %zu", payloadLen, L));
         acc.insert(acc.end(), sh, sh + payloadLen);
     }
-    res = Slice::from(acc.data(), acc.size(), std::max(acc.size(), missing.size() * (size_t)std::max(big, 0)));
-    *out = res;
+    *out = Slice::from(acc.data(), acc.size(), std::max(acc.size(), plan.missing.size() * (size_t)std::max(big, 0)));
     return Error::nil();
+}
+
+Error ReedSolomonScheme::recoverSymbolPayloads(Block& b, Slice* out) {   // reed_solomon.go:92-136
+    *out = Slice{};
+    const int nsh = std::max(0, b.totNumSourceSymbols + b.totNumRepairSymbols);
+    size_t stride = 0;
+    for (auto& kv : b.pidToRepairPayload) stride = std::max(stride, kv.second.len);
+    stride = std::max<size_t>(1, std::max(stride, kRepairPayloadMetadataLen + (size_t)std::max(0, b.biggestSourceSymbolLenSoFar)));
+    std::vector<uint8_t> host((size_t)nsh * stride + 1, 0);
+    RecoverPlan plan;
+    Error e = stageRecoverInput(b, host.data(), stride, &plan);
+    if (!e.ok() || plan.nothing) return e;
+    const size_t L = plan.len;
+    // repack to the shard length (stride may exceed L)
+    std::vector<uint8_t> dense((size_t)nsh * L, 0);
+    for (int i = 0; i < nsh; ++i) memcpy(&dense[(size_t)i * L], &host[(size_t)i * stride], L);
+    fec_ctx* ctx = nullptr;
+    e = engine_->ctx(&ctx);
+    if (!e.ok()) return e;
+    uint32_t mask = plan.mask;
+    int32_t st = 0;
+    const int rc = fec_rs_reconstruct_batch(ctx, k_, m_, L, 1, dense.data(), (size_t)nsh * L, dense.data() + (size_t)k_ * L,
+                                            (size_t)nsh * L, L, &mask, &st, FEC_HOST);
+    if (rc) return codec_error(rc);
+    std::vector<const uint8_t*> rebuilt;
+    for (int i : plan.missing) rebuilt.push_back(&dense[(size_t)i * L]);
+    return finishRecover(b, plan, rebuilt.data(), out);
 }
 
 // ------------------------------------------------------------------ XOR (xor.go)
@@ -348,30 +382,46 @@ Error XorScheme::repairSymbols(Block& b, std::vector<RepairFrame>* out) {   // x
     return Error::nil();
 }
 
-Error XorScheme::recoverSymbolPayloads(Block& b, Slice* out) {   // xor.go:66-104
-    *out = Slice{};
+Error XorScheme::stageRecoverInput(Block& b, uint8_t* dst, size_t stride, size_t slots, bool* nothing, int* count) {
+    // xor.go:66-86 up to the XOR loop: the same checks, then the repair payloads (whole) and
+    // the present sources (framed) into dst + i*stride; slots past the inputs are zeroed
+    *nothing = false;
     if (!b.isRecoverable()) return Error::text(kNotRecoverable);
-    if (b.isComplete()) return Error::nil();
-    const size_t L = kMaxPacketBufferSize;
-    const int count = (int)(b.pidToRepairPayload.size() + b.ssidToSourcePayload.size());
-    std::vector<uint8_t> shards((size_t)count * L, 0);
+    if (b.isComplete()) {
+        *nothing = true;
+        return Error::nil();
+    }
+    const size_t L = std::min(stride, kMaxPacketBufferSize);
+    const size_t n = b.pidToRepairPayload.size() + b.ssidToSourcePayload.size();
+    if (n > slots) return Error::text(fmt("%zu XOR inputs exceed the %zu staging slots", n, slots));
     int i = 0;
     for (auto& kv : b.pidToRepairPayload) {   // xorRepair: whole repair payload
         if (kv.second.len > L) return Error::text("repair payload longer than the packet buffer");
-        if (kv.second.len) memcpy(&shards[(size_t)i * L], kv.second.data(), kv.second.len);
+        uint8_t* slot = dst + (size_t)i * stride;
+        memset(slot, 0, stride);
+        if (kv.second.len) memcpy(slot, kv.second.data(), kv.second.len);
         ++i;
     }
-    for (auto& kv : b.ssidToSourcePayload)
-        if (!xor_frame(kv.second, b.biggestSourceSymbolLenSoFar, L, &shards[(size_t)(i++) * L]))
+    for (auto& kv : b.ssidToSourcePayload) {
+        uint8_t* slot = dst + (size_t)(i++) * stride;
+        memset(slot, 0, stride);
+        if (!xor_frame(kv.second, b.biggestSourceSymbolLenSoFar, L, slot))
             return Error::text("source payload overruns the packet buffer");
-    Slice rec = Slice::make(L, L);
-    Error e = xor_reduce(engine_, shards, count, L, rec.data());
-    if (!e.ok()) return e;
+    }
+    for (size_t z = (size_t)i; z < slots; ++z) memset(dst + z * stride, 0, stride);
+    *count = i;
+    return Error::nil();
+}
+
+Error XorScheme::finishRecover(Block& b, const uint8_t* rec, size_t len, Slice* out) {
+    // xor.go:86-103: the length trailer names the payload; it is stored for the missing SSID
+    Slice full = Slice::make(kMaxPacketBufferSize, kMaxPacketBufferSize);
+    memcpy(full.data(), rec, std::min(len, kMaxPacketBufferSize));
     const int big = b.biggestSourceSymbolLenSoFar;
-    if (big < 0 || (size_t)big + 2 > L) return Error::text("length trailer outside the packet buffer");
-    const size_t payloadLen = ((size_t)rec.data()[big] << 8) | rec.data()[big + 1];
-    if (payloadLen > L) return Error::text("recovered payload length exceeds the packet buffer");
-    Slice recovered = rec.reslice(0, payloadLen);
+    if (big < 0 || (size_t)big + 2 > kMaxPacketBufferSize) return Error::text("length trailer outside the packet buffer");
+    const size_t payloadLen = ((size_t)full.data()[big] << 8) | full.data()[big + 1];
+    if (payloadLen > kMaxPacketBufferSize) return Error::text("recovered payload length exceeds the packet buffer");
+    Slice recovered = full.reslice(0, payloadLen);
     for (SourceSymbolID ssid = b.smallestSSID;; ++ssid) {
         if (!b.ssidToSourcePayload.count(ssid)) b.ssidToSourcePayload[ssid] = recovered;
         if (ssid == b.largestSSID) break;
@@ -379,6 +429,21 @@ Error XorScheme::recoverSymbolPayloads(Block& b, Slice* out) {   // xor.go:66-10
     if (!b.isComplete()) return Error::text("block is not complete after recovery");
     *out = recovered;
     return Error::nil();
+}
+
+Error XorScheme::recoverSymbolPayloads(Block& b, Slice* out) {   // xor.go:66-104
+    *out = Slice{};
+    const size_t L = kMaxPacketBufferSize;
+    const size_t slots = b.pidToRepairPayload.size() + b.ssidToSourcePayload.size();
+    std::vector<uint8_t> shards(std::max<size_t>(slots, 1) * L, 0);
+    bool nothing = false;
+    int count = 0;
+    Error e = stageRecoverInput(b, shards.data(), L, slots, &nothing, &count);
+    if (!e.ok() || nothing) return e;
+    std::vector<uint8_t> rec(L, 0);
+    e = xor_reduce(engine_, shards, count, L, rec.data());
+    if (!e.ok()) return e;
+    return finishRecover(b, rec.data(), L, out);
 }
 
 // ------------------------------------------------------------------ manager (manager.go)
@@ -440,6 +505,22 @@ Error Manager::AddSourceSymbolFrameBatched(const SourceSymbolFrame& f, BatchEnco
     if (!e.ok()) return e;
     if (bs.block->isComplete()) {
         e = enc->Submit(*bs.block, q);
+        if (!e.ok()) return e;
+        bs.block.reset();
+        bs.isProcessed = true;
+    }
+    return Error::nil();
+}
+
+Error Manager::HandleRepairFrameBatched(const RepairFrame& f, BatchDecoder* dec, RecoveredQueue* q) {
+    // manager.go:160-198 with recoverSymbolPayloads replaced by staging into the batch decoder
+    if (!dec) return Error::text("nil batch decoder");
+    BlockStatus& bs = statusFor(f.block_id);
+    if (bs.isProcessed) return Error::nil();
+    Error e = bs.block->addRepairSymbol(f);
+    if (!e.ok()) return e;
+    if (bs.block->isRecoverable()) {
+        e = dec->Submit(*bs.block, q);
         if (!e.ok()) return e;
         bs.block.reset();
         bs.isProcessed = true;
@@ -826,6 +907,74 @@ int fec_manager_add_source_symbol_frame_batched(fec_manager* m, uint64_t ssid, c
     if (!m || !e || !q || (len && !p)) return FEC_ERR_INVALID_ARG;
     fec::SourceSymbolFrame f{ssid, fec::Slice::from(p, len, cap)};
     return report(m->m->AddSourceSymbolFrameBatched(f, e->e.get(), q->q.get()));
+}
+
+
+}  // extern "C"
+
+struct fec_recovered_queue {
+    fec::RecoveredQueue q;
+};
+struct fec_batch_decoder {
+    std::unique_ptr<fec::BatchDecoder> d;
+};
+
+extern "C" {
+
+fec_recovered_queue* fec_recovered_queue_new(void) { return new fec_recovered_queue(); }
+
+void fec_recovered_queue_free(fec_recovered_queue* q) { delete q; }
+
+size_t fec_recovered_queue_len(fec_recovered_queue* q) { return q ? q->q.Len() : 0; }
+
+int fec_recovered_queue_pop(fec_recovered_queue* q, uint64_t* block_id, fec_bytes** out) {
+    if (!q || !out) return FEC_ERR_INVALID_ARG;
+    *out = nullptr;
+    fec::RecoveredQueue::Item it;
+    if (!q->q.Pop(&it)) return 0;
+    if (block_id) *block_id = it.block_id;
+    *out = new fec_bytes{it.payload};
+    return 1;
+}
+
+fec_batch_decoder* fec_batch_decoder_new(int scheme_id, int k, int m, size_t max_blocks, int device, int* err) {
+    std::unique_ptr<fec::BatchDecoder> d;
+    const int rc = report(fec::BatchDecoder::New((fec::DecoderFECScheme)scheme_id, k, m, max_blocks,
+                                                 engine_for(device), &d));
+    if (err) *err = rc;
+    if (rc) return nullptr;
+    return new fec_batch_decoder{std::move(d)};
+}
+
+void fec_batch_decoder_free(fec_batch_decoder* d) { delete d; }
+
+int fec_batch_decoder_submit(fec_batch_decoder* d, fec_block* b, fec_recovered_queue* q, int* staged) {
+    if (!d || !b || !q) return FEC_ERR_INVALID_ARG;
+    bool st = false;
+    const int rc = report(d->d->Submit(b->b, &q->q, &st));
+    if (staged) *staged = st ? 1 : 0;
+    return rc;
+}
+
+int fec_batch_decoder_flush(fec_batch_decoder* d) { return d ? report(d->d->Flush()) : FEC_ERR_INVALID_ARG; }
+
+int fec_batch_decoder_poll(fec_batch_decoder* d, size_t* blocks) {
+    return d ? report(d->d->Poll(blocks)) : FEC_ERR_INVALID_ARG;
+}
+
+int fec_batch_decoder_drain(fec_batch_decoder* d, size_t* blocks) {
+    return d ? report(d->d->Drain(blocks)) : FEC_ERR_INVALID_ARG;
+}
+
+size_t fec_batch_decoder_staged(const fec_batch_decoder* d) { return d ? d->d->Staged() : 0; }
+
+size_t fec_batch_decoder_in_flight(const fec_batch_decoder* d) { return d ? d->d->InFlight() : 0; }
+
+int fec_manager_handle_repair_frame_batched(fec_manager* m, uint64_t block_id, uint64_t parity_id, const uint8_t* p,
+                                            size_t len, fec_batch_decoder* d, fec_recovered_queue* q) {
+    if (!m || !d || !q || (len && !p)) return FEC_ERR_INVALID_ARG;
+    fec::RepairFrame f{block_id, parity_id, fec::Slice::from(p, len, len)};
+    return report(m->m->HandleRepairFrameBatched(f, d->d.get(), &q->q));
 }
 
 }  // extern "C"

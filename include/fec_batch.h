@@ -14,6 +14,11 @@
  *                                                 packet_packer.go:1005 / manager.go:145)
  *   fec_manager_add_source_symbol_frame_batched   AddSourceSymbolFrame    manager.go:123-158,
  *                                                 encode deferred to a batch encoder
+ *   fec_recovered_queue_*                         the payloads HandleRepairFrame returns
+ *                                                 (manager.go:182 -> connection.go:1342)
+ *   fec_batch_decoder_*                           deferred recoverSymbolPayloads for many blocks
+ *   fec_manager_handle_repair_frame_batched       HandleRepairFrame       manager.go:160-198,
+ *                                                 recovery deferred to a batch decoder
  */
 #ifndef FEC_BATCH_H
 #define FEC_BATCH_H
@@ -57,6 +62,28 @@ size_t fec_batch_encoder_in_flight(const fec_batch_encoder *e);
 
 int fec_manager_add_source_symbol_frame_batched(fec_manager *m, uint64_t ssid, const uint8_t *p, size_t len,
                                                 size_t cap, fec_batch_encoder *e, fec_repair_queue *q);
+
+typedef struct fec_recovered_queue fec_recovered_queue;
+typedef struct fec_batch_decoder fec_batch_decoder;
+
+fec_recovered_queue *fec_recovered_queue_new(void);
+void fec_recovered_queue_free(fec_recovered_queue *q);
+size_t fec_recovered_queue_len(fec_recovered_queue *q);
+/* 1 and the oldest recovered payload (caller frees *out with fec_bytes_free), or 0 when empty. */
+int fec_recovered_queue_pop(fec_recovered_queue *q, uint64_t *block_id, fec_bytes **out);
+
+fec_batch_decoder *fec_batch_decoder_new(int scheme_id, int k, int m, size_t max_blocks, int device, int *err);
+void fec_batch_decoder_free(fec_batch_decoder *d);
+/* *staged = 0 when the block was already complete (the reference's nil, nil). */
+int fec_batch_decoder_submit(fec_batch_decoder *d, fec_block *b, fec_recovered_queue *q, int *staged);
+int fec_batch_decoder_flush(fec_batch_decoder *d);
+int fec_batch_decoder_poll(fec_batch_decoder *d, size_t *blocks);
+int fec_batch_decoder_drain(fec_batch_decoder *d, size_t *blocks);
+size_t fec_batch_decoder_staged(const fec_batch_decoder *d);
+size_t fec_batch_decoder_in_flight(const fec_batch_decoder *d);
+
+int fec_manager_handle_repair_frame_batched(fec_manager *m, uint64_t block_id, uint64_t parity_id, const uint8_t *p,
+                                            size_t len, fec_batch_decoder *d, fec_recovered_queue *q);
 
 #ifdef __cplusplus
 }

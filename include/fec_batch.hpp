@@ -122,4 +122,81 @@ private:
     bool ready_ = false;
 };
 
+// Receive side: recovered payloads of one connection, in the order their
+// blocks became recoverable. HandleRepairFrame returns the payload directly in the reference
+// (manager.go:160-198, connection.go:1342); batched, it arrives here when the batch completes.
+class RecoveredQueue {
+public:
+    struct Item {
+        BlockID block_id;
+        Slice payload;   // recoverSymbolPayloads' result (the concatenation, or XOR's payload)
+    };
+    void Push(Item it);
+    bool Pop(Item* out);   // false when empty
+    size_t Len();
+
+private:
+    std::mutex mu_;
+    std::deque<Item> q_;
+};
+
+// Deferred, batched recoverSymbolPayloads: recoverable blocks of any number of connections are
+// staged into pinned memory ([block][n][S], present shards + present masks), decoded with one
+// H2D copy, one fec_rs_recover_batch (or XOR) launch and one D2H copy per batch, and their
+// payloads handed to each block's RecoveredQueue in submission order. Two staging sets.
+class BatchDecoder {
+public:
+    static Error New(DecoderFECScheme scheme, int k, int m, size_t maxBlocks, std::shared_ptr<Engine> engine,
+                     std::unique_ptr<BatchDecoder>* out);
+    ~BatchDecoder();
+    // Validate (exactly as recoverSymbolPayloads: same errors, same order) and stage a
+    // recoverable block. A block that is already complete is the reference's nil, nil: nothing
+    // is staged or delivered (*staged = false).
+    Error Submit(Block& b, RecoveredQueue* q, bool* staged = nullptr);
+    Error Flush();
+    Error Poll(size_t* blocks = nullptr);
+    Error Drain(size_t* blocks = nullptr);
+    size_t Staged() const;
+    size_t InFlight() const;
+
+private:
+    struct Pending {
+        RecoveredQueue* q;
+        BlockID id;
+        Block meta;                // id, biggest, SSID range (payload maps not kept)
+        ReedSolomonScheme::RecoverPlan plan;   // RS: mask, length, missing indices
+    };
+    struct Set {
+        uint8_t* h_in = nullptr;    // pinned [maxBlocks][n][kSlotMax]
+        uint8_t* h_out = nullptr;   // pinned [maxBlocks][m][kSlotMax]
+        uint32_t* h_masks = nullptr;
+        int32_t* h_status = nullptr;
+        uint8_t* d_in = nullptr;
+        uint8_t* d_out = nullptr;
+        uint32_t* d_masks = nullptr;
+        int32_t* d_status = nullptr;
+        void* done = nullptr;
+        std::vector<Pending> blocks;
+        size_t slot = 0, maxLen = 0, outSlots = 0, delivered = 0;
+        bool inFlight = false;
+    };
+    BatchDecoder(DecoderFECScheme scheme, int k, int m, size_t maxBlocks, std::shared_ptr<Engine> e)
+        : scheme_(scheme), k_(k), m_(m), maxBlocks_(maxBlocks), engine_(std::move(e)) {}
+    Error init();
+    Error stage(Block& b, uint8_t* dst, size_t slot, Pending* p, bool* nothing);
+    Error flushImpl(size_t* delivered);
+    Error waitSet(Set& s);
+    Error deliver(Set& s, size_t* blocks);
+
+    DecoderFECScheme scheme_;
+    int k_, m_;
+    size_t maxBlocks_;
+    std::shared_ptr<Engine> engine_;
+    std::unique_ptr<ReedSolomonScheme> rs_;
+    std::unique_ptr<XorScheme> xor_;
+    Set sets_[2];
+    int cur_ = 0;
+    bool ready_ = false;
+};
+
 }  // namespace fec

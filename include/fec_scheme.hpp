@@ -127,6 +127,18 @@ public:
     // block's k framed shards to dst + i*stride (zero pad to the 16-byte boundary) and their
     // length L. The batch encoder (fec_batch.hpp) stages blocks with it.
     Error stageRepairInput(Block& b, uint8_t* dst, size_t stride, size_t* shard_len);
+    // recoverSymbolPayloads up to the enc.ReconstructData call (same checks, same order): the
+    // present shards into dst + i*stride (n slots), the present mask, shard length and missing
+    // data indices; plan->nothing when the block is already complete (nil result).
+    struct RecoverPlan {
+        bool nothing = false;
+        size_t len = 0;
+        uint32_t mask = 0;
+        std::vector<int> missing;   // ascending missing data shard indices
+    };
+    Error stageRecoverInput(Block& b, uint8_t* dst, size_t stride, RecoverPlan* plan);
+    // The rest of recoverSymbolPayloads: rebuilt[r] = the rebuilt shard of plan.missing[r].
+    Error finishRecover(const Block& b, const RecoverPlan& plan, const uint8_t* const* rebuilt, Slice* out);
 
 private:
     ReedSolomonScheme(int k, int m, std::shared_ptr<Engine> e) : k_(k), m_(m), engine_(std::move(e)) {}
@@ -144,6 +156,11 @@ public:
     // repairSymbols up to the XOR reduction: the sources framed (payload, BE16 length XORed at
     // [biggest]) into dst + i*stride, their count and length L.
     Error stageRepairInput(Block& b, uint8_t* dst, size_t stride, size_t* shard_len, int* count);
+    // recoverSymbolPayloads up to the XOR loop (same checks): repairs and framed sources into
+    // `slots` slots of `stride` bytes (unused slots zeroed); *nothing when already complete.
+    Error stageRecoverInput(Block& b, uint8_t* dst, size_t stride, size_t slots, bool* nothing, int* count);
+    // The rest of recoverSymbolPayloads from the XOR of the inputs (len bytes of it).
+    Error finishRecover(Block& b, const uint8_t* rec, size_t len, Slice* out);
 
 private:
     std::shared_ptr<Engine> engine_;
@@ -164,6 +181,10 @@ public:
     // block is staged into `enc` (validated exactly as repairSymbols would), dropped and marked
     // processed; its repair frames reach `q` when the batch completes (fec_batch.hpp).
     Error AddSourceSymbolFrameBatched(const SourceSymbolFrame& f, class BatchEncoder* enc, class RepairQueue* q);
+    // HandleRepairFrame with the recovery deferred to a batch: when the block becomes
+    // recoverable it is staged into `dec`, dropped and marked processed; its recovered payload
+    // reaches `q` when the batch completes.
+    Error HandleRepairFrameBatched(const RepairFrame& f, class BatchDecoder* dec, class RecoveredQueue* q);
     BlockFECScheme* scheme() { return scheme_.get(); }
 
 private:

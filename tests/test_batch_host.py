@@ -70,3 +70,19 @@ def test_batch_encoder_validates_before_device_work(B, S):
     b = S.Block.literal(tot_src=2, tot_rep=1, sources={5: (b"\x01", 1452)})
     assert xenc.submit(b, q) == "block does not have enough source symbols to generate repair symbols"
     assert len(q) == 0 and enc.staged == 0 and enc.in_flight == 0
+
+
+def test_batch_decoder_validates_before_device_work(B, S):
+    dec, err = B.BatchDecoder.new(S.REED_SOLOMON_FEC_SCHEME, 2, 1)
+    assert err is None
+    q = B.RecoveredQueue()
+    b = S.Block.literal(tot_src=2, tot_rep=1, sources={0: (b"\x01\x02", 1452)})
+    staged, err = dec.submit(b, q)
+    assert not staged and err == "not enough present symbols to repair the missing ones"
+    # complete block: the reference's nil, nil — nothing staged, no error, no device needed
+    b = S.Block.literal(tot_src=2, tot_rep=1, smallest=0, largest=1,
+                        sources={0: (b"\x01", 1452), 1: (b"\x02", 1452)})
+    staged, err = dec.submit(b, q)
+    assert not staged and err is None and len(q) == 0
+    d2, err = B.BatchDecoder.new(S.XOR_FEC_SCHEME, 2, 3)
+    assert d2 is None and "xor only supports 1 repair symbol" in err

@@ -92,3 +92,73 @@ def test_full_queue_holds_frames_until_room(B, S):
     assert err is None and len(q) == 2
     got += q.drain_frames()
     assert [f[0] for f in got] == [0, 1, 2, 3]
+
+
+@pytest.mark.parametrize("scheme,k,m,max_blocks,lens,loss", [
+    ("rs", 20, 10, 4, [1200], 0.15),
+    ("rs", 8, 4, 3, [1, 17, 600, 1200, 1434], 0.25),
+    ("rs", 2, 1, 64, [1200, 1434], 0.3),
+    ("xor", 2, 1, 3, [1, 100, 1200, 1434], 0.3),
+])
+def test_batched_recovery_equals_per_block_recovery(B, S, scheme, k, m, max_blocks, lens, loss):
+    """Receiver: the payloads HandleRepairFrame returns per block (manager.go:160-198) equal,
+    in order, those the batched path delivers to the connection's RecoveredQueue, under random
+    source and repair losses (some blocks unrecoverable, some complete before any repair)."""
+    rng = np.random.default_rng(k * 7 + max_blocks)
+    sid = S.XOR_FEC_SCHEME if scheme == "xor" else S.REED_SOLOMON_FEC_SCHEME
+    nconn, nblocks = 3, 9
+    streams = _streams(rng, nconn, nblocks, k, lens)
+    # the senders' frames, then a loss pattern per connection
+    arrivals = []
+    for pl in streams:
+        snd, _ = S.new_manager(sid, k, m)
+        ev = []
+        for blk in range(nblocks):
+            reps = []
+            for j in range(k):
+                ssid = blk * k + j
+                fr, err = snd.add_source_symbol_frame(ssid, pl[ssid])
+                assert err is None
+                if rng.random() >= loss:
+                    ev.append(("src", ssid, pl[ssid]))
+                reps += fr or []
+            for (bid, pid, payload) in reps:
+                if rng.random() >= loss / 2:
+                    ev.append(("rep", bid, pid, payload))
+        arrivals.append(ev)
+    # per-block receivers
+    want = []
+    for ev in arrivals:
+        rcv, _ = S.new_manager(sid, k, m)
+        got = []
+        for e in ev:
+            if e[0] == "src":
+                _, err = rcv.handle_source_symbol_frame(e[1], e[2])
+            else:
+                rec, err = rcv.handle_repair_frame(e[1], e[2], e[3])
+                if rec is not None:
+                    got.append((e[1], rec))
+            assert err is None
+        want.append(got)
+    assert sum(len(w) for w in want) > 0
+    # batched receivers sharing one decoder, arrivals interleaved across connections
+    dec, err = B.BatchDecoder.new(sid, k, m, max_blocks=max_blocks)
+    assert err is None
+    rcvs = [S.new_manager(sid, k, m)[0] for _ in range(nconn)]
+    queues = [B.RecoveredQueue() for _ in range(nconn)]
+    for i in range(max(len(ev) for ev in arrivals)):
+        for c in range(nconn):
+            if i >= len(arrivals[c]):
+                continue
+            e = arrivals[c][i]
+            if e[0] == "src":
+                _, err = rcvs[c].handle_source_symbol_frame(e[1], e[2])
+            else:
+                err = rcvs[c].handle_repair_frame_batched(e[1], e[2], e[3], dec, queues[c])
+            assert err is None
+        if i % 11 == 5:
+            assert dec.poll()[1] is None
+    n, err = dec.drain()
+    assert err is None and dec.staged == 0 and dec.in_flight == 0
+    for c in range(nconn):
+        assert queues[c].drain() == want[c], c
