@@ -506,7 +506,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 10 ? &fk::g_tune.dec_wpc : key == 11 ? &fk::g_tune.enc_fixed
               : key == 12 ? &fk::g_tune.dec_swz : key == 13 ? &fk::g_tune.gen_wpc
               : key == 14 ? &fk::g_tune.enc_queue : key == 15 ? &fk::g_tune.enc_qwpc
-              : key == 16 ? &fk::g_tune.enc_qdepth : key == 17 ? &fk::g_tune.dec_wave : nullptr;
+              : key == 16 ? &fk::g_tune.enc_qdepth : key == 17 ? &fk::g_tune.dec_wave
+              : key == 18 ? &fk::g_tune.enc_diag : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

@@ -288,6 +288,12 @@ struct FixedEncode {
         uint32_t acc[M][4];
 #pragma unroll
         for (int r = 0; r < M; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0;
+        if constexpr ((POL & 4) != 0) {   // diagnostics (knob enc_diag): traffic only, no field math
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+#pragma unroll
+                for (int d = 0; d < 4; ++d) acc[j % M][d] ^= word_of(x[j], d);
+        } else
 #pragma unroll
         for (int j = 0; j < K; j += 2) {
             Idx ia[4], ib[4];
@@ -399,6 +405,39 @@ __global__ __launch_bounds__(kThreads) void rs_encode_queue_kernel(EncodeArgs a)
     }
     // The last workgroup to finish rewinds the counters for the next launch on this stream
     // (every workgroup's draws precede its arrival, released by the fence).
+    if (threadIdx.x == 0) {
+        __threadfence();
+        uint32_t* done = a.ctr + 8 * kCtrStride;
+        if (atomicAdd(done, 1u) == gridDim.x - 1) {
+            for (int x = 0; x < 8; ++x) atomicExch(a.ctr + x * kCtrStride, 0u);
+            atomicExch(done, 0u);
+        }
+    }
+}
+
+// Ticket queue without prefetch (prefetch depth 0): draw, barrier, load, compute, store.
+// DRAIN: the barrier is HIP's __syncthreads, which also waits for the workgroup's stores.
+template <int K, int M, int POL, bool DRAIN>
+__global__ __launch_bounds__(kThreads) void rs_encode_queue0_kernel(EncodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ uint32_t tk[2];
+    uint32_t* ctr = a.ctr + (blockIdx.x & 7u) * kCtrStride;
+    const FixedEncode<K, M, POL> f{a, stage_tabs<K, M>(smem, a.tabs)};
+    const uint32_t lo = (blockIdx.x & 7u) * a.per_xcd;
+    const uint32_t hi = min(a.total, lo + a.per_xcd);
+    for (uint32_t t = 0;; ++t) {
+        if (threadIdx.x == 0) tk[t & 1] = atomicAdd(ctr, 1u);
+        if constexpr (DRAIN) __syncthreads();
+        else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        const uint32_t base = lo + tk[t & 1] * kThreads;
+        if (base >= hi) break;
+        const uint32_t it = base + threadIdx.x;
+        if (it < hi) {
+            uint4 x[K];
+            f.load(x, it);
+            f.compute_store(x, it);
+        }
+    }
     if (threadIdx.x == 0) {
         __threadfence();
         uint32_t* done = a.ctr + 8 * kCtrStride;
@@ -814,7 +853,13 @@ bool fixed_encode_applies(uint32_t k, uint32_t m) {
 template <int K, int M>
 static hipError_t enc_fixed_dispatch(const EncodeArgs& a, int grid, size_t lds, bool queue, hipStream_t s) {
     if (queue) {
-        if (g_tune.enc_qdepth >= 2 && K <= 8)   // K = 16 at depth 2 exceeds the register file
+        if (g_tune.enc_qdepth == 0)
+            hipLaunchKernelGGL((rs_encode_queue0_kernel<K, M, 3, true>), dim3(grid), dim3(kThreads), lds, s, a);
+        else if (g_tune.enc_qdepth < 0)
+            hipLaunchKernelGGL((rs_encode_queue0_kernel<K, M, 3, false>), dim3(grid), dim3(kThreads), lds, s, a);
+        else if (g_tune.enc_diag)
+            hipLaunchKernelGGL((rs_encode_queue_kernel<K, M, 7, 1>), dim3(grid), dim3(kThreads), lds, s, a);
+        else if (g_tune.enc_qdepth >= 2 && K <= 8)   // K = 16 at depth 2 exceeds the register file
             hipLaunchKernelGGL((rs_encode_queue_kernel<K, M, 3, (K <= 8 ? 2 : 1)>), dim3(grid), dim3(kThreads), lds, s, a);
         else
             hipLaunchKernelGGL((rs_encode_queue_kernel<K, M, 3, 1>), dim3(grid), dim3(kThreads), lds, s, a);

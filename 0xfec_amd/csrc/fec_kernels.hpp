@@ -112,8 +112,9 @@ struct Tuning {
     int enc_fixed = 1;        // compile-time-shape encode for RS(2,3), RS(8,12), RS(16,24)
     int enc_queue = 1;        // ... as the persistent ticket-queue kernel (0: flat grid)
     int enc_qwpc = 2;         // resident workgroups per CU of the queue kernel
-    int enc_qdepth = 1;       // chunks the queue kernel loads ahead of the one it computes
+    int enc_qdepth = 0;       // chunks the queue kernel loads ahead (0: none, __syncthreads; -1: none, LDS-only barrier)
     int dec_wave = 1;         // reconstruct: wave-private plan staging (shards of 32+ chunks)
+    int enc_diag = 0;         // diagnostics only: queue kernel without the field arithmetic (wrong output)
 };
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):

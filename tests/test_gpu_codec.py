@@ -292,6 +292,8 @@ def test_rs_recover_out_of_place(codec, oracle, torch, fec, k, m, slots):
 ENC_VARIANTS = {
     "generic": dict(enc_fixed=0),
     "fixed_flat": dict(enc_fixed=1, enc_queue=0, enc_wpc=3),
+    "queue_d0": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=0),
+    "queue_d0_nodrain": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=-1),
     "queue_d1": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=1),
     "queue_d2": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=2),
     "queue_d1_1wg": dict(enc_fixed=1, enc_queue=1, enc_qwpc=1, enc_qdepth=1),
