@@ -1,4 +1,4 @@
-// batch_bench.cpp — host-resident sender path, per block vs batched (diagnostics).
+// batch_bench.cpp — host-resident sender and receiver paths, per block vs batched (diagnostics).
 //
 // Feeds `conns` connections x `blocks` blocks of k source symbols (random bytes, `len`-byte
 // payloads) through the C++ mirror of internal/fec:
@@ -6,8 +6,10 @@
 //              (the reference's call pattern, packet_packer.go:1005 -> manager.go:145)
 //   batched:   Manager::AddSourceSymbolFrameBatched -> BatchEncoder (max_blocks per batch,
 //              pinned staging, one H2D + launch + D2H per batch), frames into RepairQueues
-// and reports wall time, blocks/s and payload GB/s for each, checking the two produce the
-// same frames. Build: tools/batch_bench.sh.
+// and the receiver the same way (HandleRepairFrame per block vs HandleRepairFrameBatched ->
+// BatchDecoder), one lost source symbol per block; reports wall time, blocks/s and payload GB/s
+// for each, checking the two produce the same frames and recovered payloads.
+// Build: tools/batch_bench.sh.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -111,13 +113,93 @@ int main(int argc, char** argv) {
         }
         same = same && i == want[c].size();
     }
+    // ---- receive side: every block loses source symbol (b % k); the repair frames arrive
+    // after the surviving sources (HandleRepairFrame fires recovery on the first repair)
+    std::vector<std::vector<std::pair<BlockID, std::vector<uint8_t>>>> rwant(conns);
+    std::vector<std::unique_ptr<Manager>> rm(conns), rbm(conns);
+    for (int c = 0; c < conns; ++c) {
+        std::unique_ptr<ReedSolomonScheme> s1, s2;
+        ReedSolomonScheme::New(k, m, engine, &s1);
+        ReedSolomonScheme::New(k, m, engine, &s2);
+        Manager::New(std::move(s1), k, m, &rm[c]);
+        Manager::New(std::move(s2), k, m, &rbm[c]);
+    }
+    auto feed_sources = [&](std::vector<std::unique_ptr<Manager>>& ms, int blk) {
+        for (int c = 0; c < conns; ++c)
+            for (int j = 0; j < k; ++j) {
+                if (j == blk % k) continue;
+                const int sym = blk * k + j;
+                const auto& p = payloads[((size_t)c * blocks * k) + sym];
+                Slice out;
+                ms[c]->HandleSourceSymbolFrame(SourceSymbolFrame{(uint64_t)sym, Slice::from(p.data(), len, kMaxPacketBufferSize)}, &out);
+            }
+    };
+    t0 = now();
+    for (int blk = 0; blk < blocks; ++blk) {
+        feed_sources(rm, blk);
+        for (int c = 0; c < conns; ++c) {
+            const RepairFrame& f = want[c][(size_t)blk * m];
+            Slice out;
+            Error e2 = rm[c]->HandleRepairFrame(RepairFrame{f.block_id, f.parity_id, Slice::from(f.payload.data(), f.payload.len, f.payload.len)}, &out);
+            if (!e2.ok()) { fprintf(stderr, "per-block recv: %s\n", e2.msg.c_str()); return 1; }
+            if (!out.nil()) rwant[c].push_back({f.block_id, out.bytes()});
+        }
+    }
+    const double t_rblock = now() - t0;
+    std::unique_ptr<BatchDecoder> dec;
+    if (!BatchDecoder::New(ReedSolomonFECScheme, k, m, maxb, std::make_shared<Engine>(0), &dec).ok()) return 1;
+    std::vector<std::unique_ptr<RecoveredQueue>> rq(conns);
+    for (auto& q : rq) q.reset(new RecoveredQueue());
+    {   // warm: staging allocation, context
+        std::unique_ptr<ReedSolomonScheme> s;
+        ReedSolomonScheme::New(k, m, engine, &s);
+        std::unique_ptr<Manager> w;
+        Manager::New(std::move(s), k, m, &w);
+        RecoveredQueue wq;
+        Slice out;
+        for (int j = 1; j < k; ++j)
+            w->HandleSourceSymbolFrame(SourceSymbolFrame{(uint64_t)j, Slice::from(payloads[j].data(), len, kMaxPacketBufferSize)}, &out);
+        const RepairFrame& f = want[0][0];
+        w->HandleRepairFrameBatched(RepairFrame{f.block_id, f.parity_id, Slice::from(f.payload.data(), f.payload.len, f.payload.len)}, dec.get(), &wq);
+        dec->Drain();
+    }
+    t0 = now();
+    for (int blk = 0; blk < blocks; ++blk) {
+        feed_sources(rbm, blk);
+        for (int c = 0; c < conns; ++c) {
+            const RepairFrame& f = want[c][(size_t)blk * m];
+            Error e2 = rbm[c]->HandleRepairFrameBatched(RepairFrame{f.block_id, f.parity_id, Slice::from(f.payload.data(), f.payload.len, f.payload.len)}, dec.get(), rq[c].get());
+            if (!e2.ok()) { fprintf(stderr, "batched recv: %s\n", e2.msg.c_str()); return 1; }
+        }
+        dec->Poll();
+    }
+    e = dec->Drain();
+    const double t_rbatch = now() - t0;
+    if (!e.ok()) { fprintf(stderr, "recv drain: %s\n", e.msg.c_str()); return 1; }
+    bool rsame = true;
+    for (int c = 0; c < conns && rsame; ++c) {
+        RecoveredQueue::Item it;
+        size_t i = 0;
+        while (rq[c]->Pop(&it)) {
+            if (i >= rwant[c].size() || it.block_id != rwant[c][i].first || it.payload.bytes() != rwant[c][i].second) {
+                rsame = false;
+                break;
+            }
+            ++i;
+        }
+        rsame = rsame && i == rwant[c].size();
+    }
+
     const double nblk = (double)conns * blocks;
     const double bytes = nblk * k * len;
     printf("{\"k\": %d, \"m\": %d, \"connections\": %d, \"blocks\": %.0f, \"payload_bytes\": %zu, \"max_batch\": %zu, "
            "\"per_block_s\": %.4f, \"per_block_blocks_per_s\": %.0f, \"per_block_GB/s\": %.3f, "
            "\"batched_s\": %.4f, \"batched_blocks_per_s\": %.0f, \"batched_GB/s\": %.3f, \"speedup\": %.1f, "
-           "\"frames_identical\": %s}\n",
+           "\"frames_identical\": %s, \"recv_per_block_s\": %.4f, \"recv_per_block_blocks_per_s\": %.0f, "
+           "\"recv_batched_s\": %.4f, \"recv_batched_blocks_per_s\": %.0f, \"recv_speedup\": %.1f, "
+           "\"recovered_identical\": %s}\n",
            k, m, conns, nblk, len, maxb, t_block, nblk / t_block, bytes / t_block / 1e9, t_batch, nblk / t_batch,
-           bytes / t_batch / 1e9, t_block / t_batch, same ? "true" : "false");
-    return same ? 0 : 2;
+           bytes / t_batch / 1e9, t_block / t_batch, same ? "true" : "false", t_rblock, nblk / t_rblock, t_rbatch,
+           nblk / t_rbatch, t_rblock / t_rbatch, rsame ? "true" : "false");
+    return same && rsame ? 0 : 2;
 }
