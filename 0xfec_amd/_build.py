@@ -6,9 +6,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "lib0xfec_hip.so")
 
-SOURCES = ["fec_kernels.hip", "fec_capi.cpp", "fec_scheme.cpp", "fec_batch.cpp"]
+SOURCES = ["fec_kernels.hip", "fec_capi.cpp", "fec_scheme.cpp", "fec_batch.cpp", "fec_wire.cpp"]
 HEADERS = ["fec_kernels.hpp", "gf256.h", "rs_matrix.hpp"]
-PUBLIC = ["fec_hip.h", "fec_scheme.h", "fec_batch.h", "fec_batch.hpp", "fec_scheme.hpp"]
+PUBLIC = ["fec_hip.h", "fec_scheme.h", "fec_batch.h", "fec_batch.hpp", "fec_scheme.hpp", "fec_wire.h"]
 
 
 def _hipcc():

@@ -147,6 +147,57 @@ Error BatchEncoder::Submit(Block& b, RepairQueue* q) {
     return Error::nil();
 }
 
+// The staging set to write the next block into, with slot >= want (flushes when needed).
+Error BatchEncoder::slotFor(size_t want, Set** out) {
+    if (!ready_) {
+        Error e = init();
+        if (!e.ok()) return e;
+    }
+    Set* s = &sets_[cur_];
+    if (s->inFlight) {
+        Error e = waitSet(*s);
+        if (e.ok()) e = deliver(*s, nullptr);
+        if (!e.ok()) return e;
+    }
+    if (!s->blocks.empty() && (s->blocks.size() >= maxBlocks_ || std::max<size_t>(want, 16) > s->slot)) {
+        Error e = flushImpl(nullptr);
+        if (!e.ok()) return e;
+        s = &sets_[cur_];
+    }
+    if (s->blocks.empty()) s->slot = std::min(kSlotMax, std::max<size_t>(want, 16));
+    *out = s;
+    return Error::nil();
+}
+
+Error BatchEncoder::SubmitPayloads(BlockID id, const uint8_t* const* payloads, const size_t* lens, int count,
+                                   RepairQueue* q) {
+    if (!q) return Error::text("nil repair queue");
+    if (count < 0 || (count && (!payloads || !lens))) return Error::text("invalid payload list");
+    // repairSymbols' checks for a block holding exactly these payloads: complete (reed_solomon.go:27,
+    // xor.go:15) -> (XOR: one repair symbol) -> size (reed_solomon.go:31, xor.go:23)
+    if (count != k_) return errIncomplete();
+    size_t biggest = 0;
+    for (int i = 0; i < count; ++i) biggest = std::max(biggest, lens[i]);
+    if (biggest > kMaxFECPacketBufferSize) return errTooBig((int)biggest);
+    const size_t L = biggest + kRepairPayloadMetadataLen;
+    Set* s = nullptr;
+    Error e = slotFor(round16(L), &s);
+    if (!e.ok()) return e;
+    uint8_t* dst = s->h_in + s->blocks.size() * (size_t)k_ * s->slot;
+    for (int i = 0; i < count; ++i) {
+        uint8_t* slot = dst + (size_t)i * s->slot;
+        if (lens[i]) memcpy(slot, payloads[i], lens[i]);
+        memset(slot + lens[i], 0, round16(L) - lens[i]);
+        // RS: big-endian length trailer at [biggest] (reed_solomon.go:77-87); XOR: the same
+        // BE16 XORed in (xor.go:49-53), which for one framed payload is the same bytes
+        slot[biggest] = (uint8_t)(lens[i] >> 8);
+        slot[biggest + 1] = (uint8_t)(lens[i] & 0xFF);
+    }
+    s->blocks.push_back(Pending{q, id, L});
+    s->maxLen = std::max(s->maxLen, L);
+    return Error::nil();
+}
+
 Error BatchEncoder::Flush() { return flushImpl(nullptr); }
 
 Error BatchEncoder::flushImpl(size_t* delivered) {

@@ -418,6 +418,7 @@ const char* fec_strerror(int code) {
         case FEC_ERR_HIP: return "HIP runtime error";
         case FEC_ERR_NOMEM: return "out of memory";
         case FEC_ERR_NO_DEVICE: return "no HIP device";
+        case -21: return "EOF";   // FEC_ERR_EOF (fec_wire.h): io.EOF
         default: return "unknown error";
     }
 }

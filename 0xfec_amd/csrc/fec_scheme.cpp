@@ -17,6 +17,7 @@
 #include "../../include/fec_batch.hpp"
 #include "../../include/fec_hip.h"
 #include "../../include/fec_scheme.h"
+#include "../../include/fec_wire.h"
 
 namespace fec {
 
@@ -128,6 +129,8 @@ Error Engine::ctx(fec_ctx** out) {
 static const char* kIncomplete = "block does not have enough source symbols to generate repair symbols";
 static const char* kNotRecoverable = "not enough present symbols to repair the missing ones";
 
+Error errIncomplete() { return Error::text(kIncomplete); }
+
 static Error too_big(int biggest) {
     return Error::text(fmt("source symbol payload len is greater is too big for FEC headers. Max %d and got %d",
                            (int)kMaxFECPacketBufferSize, biggest));
@@ -161,6 +164,8 @@ Error ReedSolomonScheme::addLengthToSourceSymbolPayload(Block& b, SourceSymbolID
     *out = shard;
     return Error::nil();
 }
+
+Error errTooBig(int biggest) { return too_big(biggest); }
 
 Error ReedSolomonScheme::stageRepairInput(Block& b, uint8_t* dst, size_t stride, size_t* shard_len) {
     // reed_solomon.go:26-51, up to the enc.Encode call: the same checks in the same order
@@ -975,6 +980,13 @@ int fec_manager_handle_repair_frame_batched(fec_manager* m, uint64_t block_id, u
     if (!m || !d || !q || (len && !p)) return FEC_ERR_INVALID_ARG;
     fec::RepairFrame f{block_id, parity_id, fec::Slice::from(p, len, len)};
     return report(m->m->HandleRepairFrameBatched(f, d->d.get(), &q->q));
+}
+
+
+int fec_batch_encoder_submit_payloads(fec_batch_encoder* e, uint64_t block_id, const uint8_t* const* payloads,
+                                      const size_t* lens, int count, fec_repair_queue* q) {
+    if (!e || !q) return FEC_ERR_INVALID_ARG;
+    return report(e->e->SubmitPayloads(block_id, payloads, lens, count, q->q.get()));
 }
 
 }  // extern "C"

@@ -74,6 +74,12 @@ public:
     // its frames go to q when its batch completes. A full batch, or a block whose shards do not
     // fit the batch's slot, flushes first.
     Error Submit(Block& b, RepairQueue* q);
+    // Zero-copy form for integrations that keep their own block bookkeeping (SURVEY.md §8f row
+    // 4): the k source payloads of block `id`, in SSID order, framed straight from the caller's
+    // packet buffers into pinned staging (one copy; nothing retained after the call, so cgo
+    // may pass Go slices). Same checks and errors as repairSymbols for a block holding exactly
+    // these payloads.
+    Error SubmitPayloads(BlockID id, const uint8_t* const* payloads, const size_t* lens, int count, RepairQueue* q);
     // Start encoding the staged blocks (asynchronous). No-op when nothing is staged.
     Error Flush();
     // Deliver the frames of every completed batch (non-blocking); *blocks = blocks delivered.
@@ -110,6 +116,7 @@ private:
     Error flushImpl(size_t* delivered);
     Error waitSet(Set& s);
     Error deliver(Set& s, size_t* blocks);
+    Error slotFor(size_t want, Set** out);
 
     DecoderFECScheme scheme_;
     int k_, m_;

@@ -90,6 +90,10 @@ struct Block {
     bool isComplete() const;
 };
 
+// The reference's error values shared with the batching layer (reed_solomon.go:28,32).
+Error errIncomplete();
+Error errTooBig(int biggest);
+
 // internal/fec/scheme.go:5-10
 class BlockFECScheme {
 public:

@@ -162,3 +162,26 @@ def test_batched_recovery_equals_per_block_recovery(B, S, scheme, k, m, max_bloc
     assert err is None and dec.staged == 0 and dec.in_flight == 0
     for c in range(nconn):
         assert queues[c].drain() == want[c], c
+
+
+@pytest.mark.parametrize("scheme,k,m", [("rs", 20, 10), ("rs", 8, 4), ("xor", 2, 1)])
+def test_submit_payloads_equals_manager_path(B, S, scheme, k, m):
+    """Zero-copy staging of source payloads (fec_wire.h) yields the frames the per-block
+    manager path returns for the same symbols."""
+    W = importlib.import_module("0xfec_amd.wire")
+    rng = np.random.default_rng(5 * k)
+    sid = S.XOR_FEC_SCHEME if scheme == "xor" else S.REED_SOLOMON_FEC_SCHEME
+    nblocks = 11
+    pl = _streams(rng, 1, nblocks, k, [1, 33, 700, 1200, 1434])[0]
+    mgr, _ = S.new_manager(sid, k, m)
+    want = []
+    for ssid, p in enumerate(pl):
+        fr, err = mgr.add_source_symbol_frame(ssid, p)
+        assert err is None
+        want += fr or []
+    enc, _ = B.BatchEncoder.new(sid, k, m, max_blocks=4)
+    q = B.RepairQueue(max_len=nblocks * m)
+    for blk in range(nblocks):
+        assert W.submit_payloads(enc, blk, pl[blk * k:(blk + 1) * k], q) is None
+    assert enc.drain()[1] is None
+    assert q.drain_frames() == want
