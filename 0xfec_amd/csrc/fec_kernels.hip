@@ -853,7 +853,9 @@ bool fixed_encode_applies(uint32_t k, uint32_t m) {
 template <int K, int M>
 static hipError_t enc_fixed_dispatch(const EncodeArgs& a, int grid, size_t lds, bool queue, hipStream_t s) {
     if (queue) {
-        if (g_tune.enc_qdepth == 0)
+        if (g_tune.enc_qdepth == 0 && g_tune.enc_diag)
+            hipLaunchKernelGGL((rs_encode_queue0_kernel<K, M, 7, true>), dim3(grid), dim3(kThreads), lds, s, a);
+        else if (g_tune.enc_qdepth == 0)
             hipLaunchKernelGGL((rs_encode_queue0_kernel<K, M, 3, true>), dim3(grid), dim3(kThreads), lds, s, a);
         else if (g_tune.enc_qdepth < 0)
             hipLaunchKernelGGL((rs_encode_queue0_kernel<K, M, 3, false>), dim3(grid), dim3(kThreads), lds, s, a);
@@ -875,12 +877,12 @@ static hipError_t enc_fixed_dispatch(const EncodeArgs& a, int grid, size_t lds, 
 hipError_t launch_rs_encode_fixed(EncodeArgs a, int ncu, hipStream_t s) {
     const uint32_t chunks = (a.total + kThreads - 1) / kThreads;
     if (chunks == 0) return hipSuccess;
-    // Per shape (measured): RS(8,12) runs the ticket queue at 2 workgroups/CU;
-    // RS(2,3) (2 loads per lane: little in flight per wave) the flat grid at full residency;
-    // RS(16,24) (VALU-heavy: 128 coefficients) the flat grid at 4 workgroups/CU.
+    // Per shape (measured): RS(8,12) and RS(16,24) run the flat grid at
+    // g_tune.enc_wpc (4) workgroups per CU; RS(2,3) (2 loads per lane: little in flight per
+    // wave) at full residency. The ticket-queue form stays selectable (enc_queue).
     const bool queue = g_tune.enc_queue && a.ctr != nullptr && a.k == 8;
     int grid = (int)chunks;
-    int wpc = a.k == 2 ? 0 : a.k == 16 ? 4 : g_tune.enc_wpc;
+    int wpc = a.k == 2 ? 0 : g_tune.enc_wpc;
     if (queue) {
         wpc = g_tune.enc_qwpc > 0 ? g_tune.enc_qwpc : 2;
         grid = ncu * wpc;

@@ -106,11 +106,11 @@ struct Tuning {
     int rotate = 0;           // rotate chunk order so shard boundaries share a wave (measured: no gain)
     int xcd_swz = 1;          // encode / XOR: workgroups of one XCD take one contiguous range of the grid
     int dec_swz = 0;          // same for reconstruct
-    int enc_wpc = 3;          // resident workgroups per CU, fixed-shape encode (0: as many as fit)
+    int enc_wpc = 4;          // resident workgroups per CU, fixed-shape encode (0: as many as fit)
     int gen_wpc = 0;          // same for the generic encode and XOR encode
     int dec_wpc = 0;          // same for reconstruct
     int enc_fixed = 1;        // compile-time-shape encode for RS(2,3), RS(8,12), RS(16,24)
-    int enc_queue = 1;        // ... as the persistent ticket-queue kernel (0: flat grid)
+    int enc_queue = 0;        // ... as the persistent ticket-queue kernel (0: flat grid, measured faster)
     int enc_qwpc = 2;         // resident workgroups per CU of the queue kernel
     int enc_qdepth = 0;       // chunks the queue kernel loads ahead (0: none, __syncthreads; -1: none, LDS-only barrier)
     int dec_wave = 1;         // reconstruct: wave-private plan staging (shards of 32+ chunks)

@@ -35,14 +35,14 @@ SHARD_STRIDE = 1216              # 16-byte aligned device slot per shard
 HBM_PEAK = 8.0e12                # MI355X HBM3E spec, bytes/s (MI355X_MICROARCH.md)
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of this bench (separate passes, tools/pmc_traffic.py,
 # gfx950 FETCH_SIZE x2 correction): HBM bytes per launch of each codec kernel
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "pmc_traffic_v7.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "pmc_traffic_v8.json")
 
 
 def encode_kernel_name(k, m):
     """The kernel fec_rs_encode_batch runs for (k, m) at the library's default tuning
-    (fec_kernels.hpp Tuning: fixed shapes run the ticket-queue kernel)."""
+    (fec_kernels.hpp Tuning: the fixed shapes run the flat fixed-shape kernel)."""
     if (k, m) in ((2, 1), (8, 4), (16, 8)):
-        return ("rs_encode_queue0_kernel<%d, %d" if k == 8 else "rs_encode_fixed_kernel<%d, %d") % (k, m)
+        return "rs_encode_fixed_kernel<%d, %d" % (k, m)
     return "rs_encode_kernel<"
 
 

@@ -56,18 +56,12 @@ def main():
         "codec encode qwpc3": (lambda: (codec.set_tuning(enc_qwpc=3),
                                         codec.rs_encode_raw(k, m, L, B, dp, k * S, pp, m * S, S, fec.FEC_DEVICE),
                                         codec.set_tuning(enc_qwpc=2)), B * (k + m) * L),
-        "codec encode depth2": (lambda: (codec.set_tuning(enc_qdepth=2),
-                                         codec.rs_encode_raw(k, m, L, B, dp, k * S, pp, m * S, S, fec.FEC_DEVICE),
-                                         codec.set_tuning(enc_qdepth=1)), B * (k + m) * L),
-        "codec encode depth0 drain": (lambda: (codec.set_tuning(enc_qdepth=0),
-                                               codec.rs_encode_raw(k, m, L, B, dp, k * S, pp, m * S, S, fec.FEC_DEVICE),
-                                               codec.set_tuning(enc_qdepth=1)), B * (k + m) * L),
-        "codec encode depth0 nodrain": (lambda: (codec.set_tuning(enc_qdepth=-1),
-                                                 codec.rs_encode_raw(k, m, L, B, dp, k * S, pp, m * S, S, fec.FEC_DEVICE),
-                                                 codec.set_tuning(enc_qdepth=1)), B * (k + m) * L),
-        "codec encode depth0 drain qwpc3": (lambda: (codec.set_tuning(enc_qdepth=0, enc_qwpc=3),
-                                                     codec.rs_encode_raw(k, m, L, B, dp, k * S, pp, m * S, S, fec.FEC_DEVICE),
-                                                     codec.set_tuning(enc_qdepth=1, enc_qwpc=2)), B * (k + m) * L),
+        "codec encode qwpc4": (lambda: (codec.set_tuning(enc_qwpc=4),
+                                        codec.rs_encode_raw(k, m, L, B, dp, k * S, pp, m * S, S, fec.FEC_DEVICE),
+                                        codec.set_tuning(enc_qwpc=2)), B * (k + m) * L),
+        "codec encode flat fixed wpc4": (lambda: (codec.set_tuning(enc_queue=0, enc_wpc=4),
+                                                  codec.rs_encode_raw(k, m, L, B, dp, k * S, pp, m * S, S, fec.FEC_DEVICE),
+                                                  codec.set_tuning(enc_queue=1, enc_wpc=3)), B * (k + m) * L),
         "probe 8r4w flat swz wg2": (lambda: probe.mix_probe(dp, pp, k * S, m * S, S, cps, B, 8, 4, 1, 1, 64 << 10, st),
                                     B * cps * 16 * 12),
         "probe 8r4w ticket-queue wg2": (lambda: probe.mix_persist_probe(dp, pp, k * S, m * S, S, cps, B, 8, 4, 1, 512,
