@@ -217,6 +217,8 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
     if (rc) return rc;
     const uint32_t G = fk::pick_tile_blocks(cps, k, maxe, lay);
     const size_t lds = fk::recon_lds_bytes(G, k, maxe, lay);
+    const bool wave = fk::wave_recon_applies(cps, k, maxe, lay.stride);
+    const bool fused = wave && fk::g_tune.dec_fused;
     for (size_t b0 = 0; b0 < nblocks; b0 += per_launch) {
         const size_t nb = std::min(per_launch, nblocks - b0);
         fk::PlanArgs p{};
@@ -231,7 +233,7 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         p.maxe = maxe;
         p.lay = lay;
         p.max_out = out ? out_slots : 0;
-        HIP_TRY(fk::launch_rs_plan(p, ctx->stream));
+        if (!fused) HIP_TRY(fk::launch_rs_plan(p, ctx->stream));
         fk::ReconArgs a{};
         a.data = data + b0 * dbs;
         a.parity = parity + b0 * pbs;
@@ -253,7 +255,17 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         a.swz = (uint32_t)fk::g_tune.dec_swz;
         a.out = out ? out + b0 * out_bs : nullptr;
         a.out_bs = out_bs;
-        if (fk::wave_recon_applies(cps, k, maxe, lay.stride)) {
+        if (fused) {
+            a.masks = p.masks;
+            a.status = p.status;
+            a.err = p.err;
+            a.prows = p.prows;
+            a.m = m;
+            a.max_out = p.max_out;
+            HIP_TRY(fk::launch_rs_recover_fused(a, ctx->stream));
+            continue;
+        }
+        if (wave) {
             HIP_TRY(fk::launch_rs_reconstruct_wave(a, ctx->stream));
             continue;
         }
@@ -508,7 +520,7 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 12 ? &fk::g_tune.dec_swz : key == 13 ? &fk::g_tune.gen_wpc
               : key == 14 ? &fk::g_tune.enc_queue : key == 15 ? &fk::g_tune.enc_qwpc
               : key == 16 ? &fk::g_tune.enc_qdepth : key == 17 ? &fk::g_tune.dec_wave
-              : key == 18 ? &fk::g_tune.enc_diag : nullptr;
+              : key == 18 ? &fk::g_tune.enc_diag : key == 19 ? &fk::g_tune.dec_fused : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

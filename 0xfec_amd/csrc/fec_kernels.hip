@@ -691,14 +691,56 @@ __host__ __device__ inline size_t wave_slice_bytes(uint32_t k, uint32_t maxe, ui
     return (size_t)kWaveBlocks * maxe * k * 32 + (size_t)kWaveBlocks * stride;
 }
 
-template <int MAXE, int POL>
+// Fused form: the wave also builds its blocks' plan records (the work of rs_plan_kernel) from
+// the present masks, lanes in parallel: slots and erased indices by prefix popcounts, one
+// erasure by the single-parity-row solution, several by the Lagrange coefficients (see
+// rs_plan_kernel) with the k^2 + e*k lookups spread over the 64 lanes. No plan kernel, no plan
+// buffer round trip through HBM.
+struct FusedLds {
+    size_t prows, slices, slice;   // offsets: exp [0,512), log [512,768), prows, wave slices
+};
+__host__ __device__ inline size_t fused_slice_bytes(uint32_t k, uint32_t maxe, uint32_t stride) {
+    return (wave_slice_bytes(k, maxe, stride) + (size_t)k + maxe + 15) & ~(size_t)15;
+}
+__host__ __device__ inline FusedLds fused_lds(uint32_t m, uint32_t k, uint32_t maxe, uint32_t stride) {
+    FusedLds l;
+    l.prows = 768;
+    l.slices = (l.prows + (size_t)m * k + 15) & ~(size_t)15;
+    l.slice = fused_slice_bytes(k, maxe, stride);
+    return l;
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int MAXE, int POL, bool FUSED>
 __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs a) {
     constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t k = a.k, maxe = a.maxe;
     const PlanLayout lay = a.lay;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    uint8_t* slice = smem + (size_t)wave * wave_slice_bytes(k, maxe, lay.stride);
+    uint8_t* slice;
+    const uint8_t *s_exp = nullptr, *s_log = nullptr, *s_prows = nullptr;
+    if constexpr (FUSED) {
+        const FusedLds L = fused_lds(a.m, k, maxe, lay.stride);
+        uint8_t* e8 = smem;
+        uint8_t* l8 = smem + 512;
+        uint8_t* p8 = smem + L.prows;
+        for (uint32_t i = threadIdx.x; i < 512; i += kThreads) e8[i] = gf::kTables.exp[i];
+        for (uint32_t i = threadIdx.x; i < 256; i += kThreads) l8[i] = gf::kTables.log[i];
+        for (uint32_t i = threadIdx.x; i < a.m * k; i += kThreads) p8[i] = a.prows[i];
+        __syncthreads();
+        s_exp = e8;
+        s_log = l8;
+        s_prows = p8;
+        slice = smem + L.slices + (size_t)wave * L.slice;
+    } else {
+        slice = smem + (size_t)wave * wave_slice_bytes(k, maxe, lay.stride);
+    }
     gf::PermTab* tabs = reinterpret_cast<gf::PermTab*>(slice);                      // 3*maxe*k
     uint8_t* plans = slice + (size_t)kWaveBlocks * maxe * k * sizeof(gf::PermTab);  // 3*stride
     const uint32_t total = a.nblocks * a.cps;
@@ -706,14 +748,87 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
     if (i0 >= total) return;
     const uint32_t bfirst = fdiv(i0, a.div_cps);
     const uint32_t nb = fdiv(min(i0 + 63u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
-    {
+    if constexpr (!FUSED) {
         const uint32_t nw = nb * lay.stride / 16;
         const uint4* src = reinterpret_cast<const uint4*>(a.plans + (uint64_t)bfirst * lay.stride);
         if (lane < nw) reinterpret_cast<uint4*>(plans)[lane] = src[lane];
+    } else {
+        uint8_t* Dt = plans + (size_t)kWaveBlocks * lay.stride;   // k bytes
+        uint8_t* Nt = Dt + k;                                       // maxe bytes
+        const uint32_t m = a.m, n = k + m;
+        const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
+        const uint32_t kmask = (1u << k) - 1u;
+        auto mul = [&](uint32_t x, uint32_t y) -> uint32_t { return (x && y) ? s_exp[s_log[x] + s_log[y]] : 0u; };
+        // the wave's (<= 3) masks in one load, then broadcast
+        const uint32_t mine = lane < nb ? a.masks[bfirst + lane] : 0u;
+        for (uint32_t g = 0; g < nb; ++g) {
+            const uint32_t b = bfirst + g;
+            uint8_t* P = plans + g * lay.stride;
+            const uint32_t mask = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)g) & all;
+            const uint32_t e = k - __popc(mask & kmask);
+            int32_t st = a.max_out ? (int32_t)e : 0;
+            uint32_t nout = 0;
+            if (e != 0) {
+                if ((uint32_t)__popc(mask) < k) {
+                    st = -4;   // FEC_ERR_TOO_FEW_SHARDS
+                    if (lane == 0) atomicOr(a.err, 1);
+                } else if (a.max_out && e > a.max_out) {
+                    st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
+                    if (lane == 0) atomicOr(a.err, 2);
+                } else {
+                    nout = e;
+                }
+            }
+            if (lane == 0) {
+                P[lay.nout_off] = (uint8_t)nout;
+                if (a.status) a.status[b] = st;
+            }
+            if (nout) {
+                // the first k present shards (index order) and the erased data shards
+                const uint32_t below = lane < 32 ? ((1u << lane) - 1u) : 0xFFFFFFFFu;
+                if (lane < n && ((mask >> lane) & 1u)) {
+                    const uint32_t pos = __popc(mask & below);
+                    if (pos < k) P[lay.in_off + pos] = (uint8_t)lane;
+                }
+                if (lane < k && !((mask >> lane) & 1u)) P[lay.out_off + (lane - __popc(mask & kmask & below))] = (uint8_t)lane;
+                wave_sync();
+                const uint8_t* S = P + lay.in_off;
+                uint8_t* C = P + lay.coef_off;
+                if (e == 1) {
+                    const uint32_t E0 = __ffs(~mask & kmask) - 1;
+                    const uint32_t R0 = __ffs(mask >> k) - 1;
+                    const uint8_t* row = s_prows + R0 * k;
+                    const uint32_t inv = s_exp[255 - s_log[row[E0]]];
+                    if (lane < k) {
+                        const uint32_t sj = S[lane];
+                        C[lane] = (uint8_t)(sj < k ? mul(inv, row[sj]) : inv);
+                    }
+                } else {
+                    if (lane < k) {
+                        const uint32_t sp = S[lane];
+                        uint32_t d = 0;
+                        for (uint32_t q = 0; q < k; ++q)
+                            if (q != lane) d += s_log[sp ^ S[q]];
+                        Dt[lane] = (uint8_t)(d % 255u);
+                    }
+                    if (lane < e) {
+                        const uint32_t i = P[lay.out_off + lane];
+                        uint32_t ns = 0;
+                        for (uint32_t q = 0; q < k; ++q) ns += s_log[i ^ S[q]];
+                        Nt[lane] = (uint8_t)(ns % 255u);
+                    }
+                    wave_sync();
+                    for (uint32_t t = lane; t < e * k; t += 64) {
+                        const uint32_t r = t / k, p = t - r * k;
+                        const uint32_t v = Nt[r] + 2u * 255u - s_log[P[lay.out_off + r] ^ S[p]] - Dt[p];
+                        C[r * k + p] = s_exp[v % 255u];
+                    }
+                }
+            }
+            wave_sync();
+        }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_sync();
     {
         const uint32_t ne = nb * maxe * k;
         for (uint32_t i = lane; i < ne; i += 64) {
@@ -724,9 +839,7 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
             if (r < P[lay.nout_off]) tabs[i] = gf::make_permtab(P[lay.coef_off + r * k + j]);
         }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_sync();
     const uint32_t item = i0 + lane;
     const bool inr = item < total;
     const uint32_t blk = inr ? fdiv(item, a.div_cps) : bfirst;
@@ -926,29 +1039,38 @@ static hipError_t recon_dispatch(const ReconArgs& a, int grid, hipStream_t s) {
 // The wave form applies to shards of 32+ chunks (at most 3 blocks per wave) while its LDS
 // (4 wave slices per workgroup) stays within 64 KiB.
 bool wave_recon_applies(uint32_t cps, uint32_t k, uint32_t maxe, uint32_t stride) {
-    return g_tune.dec_wave && cps >= 32 && 4 * wave_slice_bytes(k, maxe, stride) <= 65536;
+    return g_tune.dec_wave && cps >= 32 && 4 * fused_slice_bytes(k, maxe, stride) + 2048 <= 65536;
 }
 
-template <int POL>
+template <int POL, bool FUSED>
 static hipError_t recon_wave_dispatch(const ReconArgs& a, hipStream_t s) {
     const int grid = (int)(((uint64_t)a.nblocks * a.cps + kThreads - 1) / kThreads);
     if (grid == 0) return hipSuccess;
-    const size_t lds = occupancy_lds(g_tune.dec_wpc, 4 * wave_slice_bytes(a.k, a.maxe, a.lay.stride));
-    if (a.maxe <= 1) hipLaunchKernelGGL((rs_reconstruct_wave_kernel<1, POL>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (a.maxe <= 2) hipLaunchKernelGGL((rs_reconstruct_wave_kernel<2, POL>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (a.maxe <= 4) hipLaunchKernelGGL((rs_reconstruct_wave_kernel<4, POL>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (a.maxe <= 8) hipLaunchKernelGGL((rs_reconstruct_wave_kernel<8, POL>), dim3(grid), dim3(kThreads), lds, s, a);
-    else hipLaunchKernelGGL((rs_reconstruct_wave_kernel<16, POL>), dim3(grid), dim3(kThreads), lds, s, a);
+    size_t own = 4 * wave_slice_bytes(a.k, a.maxe, a.lay.stride);
+    if (FUSED) {
+        const FusedLds L = fused_lds(a.m, a.k, a.maxe, a.lay.stride);
+        own = L.slices + 4 * L.slice;
+    }
+    const size_t lds = occupancy_lds(g_tune.dec_wpc, own);
+    if (a.maxe <= 1) hipLaunchKernelGGL((rs_reconstruct_wave_kernel<1, POL, FUSED>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (a.maxe <= 2) hipLaunchKernelGGL((rs_reconstruct_wave_kernel<2, POL, FUSED>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (a.maxe <= 4) hipLaunchKernelGGL((rs_reconstruct_wave_kernel<4, POL, FUSED>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (a.maxe <= 8) hipLaunchKernelGGL((rs_reconstruct_wave_kernel<8, POL, FUSED>), dim3(grid), dim3(kThreads), lds, s, a);
+    else hipLaunchKernelGGL((rs_reconstruct_wave_kernel<16, POL, FUSED>), dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_rs_reconstruct_wave(const ReconArgs& a, hipStream_t s) {
     switch (g_tune.dec_nt & 3) {
-        case 0: return recon_wave_dispatch<0>(a, s);
-        case 1: return recon_wave_dispatch<1>(a, s);
-        case 2: return recon_wave_dispatch<2>(a, s);
-        default: return recon_wave_dispatch<3>(a, s);
+        case 0: return recon_wave_dispatch<0, false>(a, s);
+        case 1: return recon_wave_dispatch<1, false>(a, s);
+        case 2: return recon_wave_dispatch<2, false>(a, s);
+        default: return recon_wave_dispatch<3, false>(a, s);
     }
+}
+
+hipError_t launch_rs_recover_fused(const ReconArgs& a, hipStream_t s) {
+    return (g_tune.dec_nt & 3) == 3 ? recon_wave_dispatch<3, true>(a, s) : recon_wave_dispatch<0, true>(a, s);
 }
 
 hipError_t launch_rs_reconstruct(const ReconArgs& a, int grid, hipStream_t s) {

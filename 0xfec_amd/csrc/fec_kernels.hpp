@@ -75,6 +75,12 @@ struct ReconArgs {
     uint8_t* out;              // recover: rebuilt shard r of block b at out + b*out_bs + r*ss
     uint64_t out_bs;           //          (nullptr: rebuild in place into the data region)
     uint32_t swz;
+    // fused form (plans built in the reconstruct kernel, no rs_plan_kernel): as PlanArgs
+    const uint32_t* masks;
+    int32_t* status;
+    int* err;
+    const uint8_t* prows;
+    uint32_t m, max_out;
 };
 
 struct XorArgs {
@@ -114,6 +120,7 @@ struct Tuning {
     int enc_qwpc = 2;         // resident workgroups per CU of the queue kernel
     int enc_qdepth = 0;       // chunks the queue kernel loads ahead (0: none, __syncthreads; -1: none, LDS-only barrier)
     int dec_wave = 1;         // reconstruct: wave-private plan staging (shards of 32+ chunks)
+    int dec_fused = 0;        // ... with the plans built inside the wave kernel (measured 11 % slower: off)
     int enc_diag = 0;         // diagnostics only: queue kernel without the field arithmetic (wrong output)
 };
 
@@ -143,6 +150,7 @@ hipError_t launch_rs_plan(const PlanArgs& a, hipStream_t s);
 hipError_t launch_rs_reconstruct(const ReconArgs& a, int grid, hipStream_t s);
 bool wave_recon_applies(uint32_t cps, uint32_t k, uint32_t maxe, uint32_t stride);
 hipError_t launch_rs_reconstruct_wave(const ReconArgs& a, hipStream_t s);
+hipError_t launch_rs_recover_fused(const ReconArgs& a, hipStream_t s);
 hipError_t launch_xor_encode(const XorArgs& a, int grid, hipStream_t s);
 hipError_t launch_xor_reconstruct(const XorArgs& a, int grid, hipStream_t s);
 

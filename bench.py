@@ -63,7 +63,7 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--k", type=int, default=8)
     p.add_argument("--m", type=int, default=4)
     p.add_argument("--blocks", type=int, default=1 << 20, help="blocks per GPU")
@@ -180,13 +180,13 @@ def main():
         if rc != 0:
             raise fec.FecError(rc, "decode_inplace")
 
-    for _ in range(args.warmup):
-        encode()
-        decode()
+    encode()
+    decode()
     codec.sync()
 
-    # correctness at full size (outside the timed region): the recovered shard of every block
-    # equals the erased original; then wipe every erased shard, rebuild in place, compare
+    # correctness at full size (before warmup, outside the timed region): the recovered shard
+    # of every block equals the erased original; then wipe every erased shard, rebuild in
+    # place, compare
     rows = torch.arange(B, device=dev)
     ok_recover = bool(torch.equal(recovered[:, 0, :SHARD_LEN], data[rows, erased, :SHARD_LEN]))
     ref = data[:, :, :SHARD_LEN].clone()
@@ -196,6 +196,11 @@ def main():
     ok_roundtrip = bool(torch.equal(data[:, :, :SHARD_LEN], ref)) and ok_recover
     del ref
     torch.cuda.empty_cache()
+
+    for _ in range(args.warmup):
+        encode()
+        decode()
+    codec.sync()
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]

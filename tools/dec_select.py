@@ -20,13 +20,13 @@ def main():
     erased = torch.randint(0, k, (B,), device="cuda")
     masks = ((1 << (k + m)) - 1 - (1 << erased)).to(torch.int32)
     dp, pp, op = data.data_ptr(), par.data_ptr(), out.data_ptr()
-    variants = {"wave": dict(dec_wave=1, dec_wpc=0, dec_swz=0)}
-    for w in (3, 4, 5, 6):
-        variants["wave wpc%d" % w] = dict(dec_wave=1, dec_wpc=w, dec_swz=0)
-    variants["wave swz"] = dict(dec_wave=1, dec_wpc=0, dec_swz=1)
-    variants["wave swz wpc4"] = dict(dec_wave=1, dec_wpc=4, dec_swz=1)
-    variants["tile"] = dict(dec_wave=0, dec_wpc=0, dec_swz=0)
-    base = codec.set_tuning(dec_wave=1, dec_wpc=0, dec_swz=0)
+    variants = {"wave fused": dict(dec_wave=1, dec_fused=1, dec_wpc=0, dec_swz=0),
+                "wave + plan kernel": dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=0)}
+    for w in (4, 5):
+        variants["wave fused wpc%d" % w] = dict(dec_wave=1, dec_fused=1, dec_wpc=w, dec_swz=0)
+    variants["wave fused swz"] = dict(dec_wave=1, dec_fused=1, dec_wpc=0, dec_swz=1)
+    variants["tile + plan kernel"] = dict(dec_wave=0, dec_fused=0, dec_wpc=0, dec_swz=0)
+    base = codec.set_tuning(dec_wave=1, dec_fused=1, dec_wpc=0, dec_swz=0)
 
     def run():
         codec.rs_recover_raw(k, m, L, B, dp, k * S, pp, m * S, S, masks.data_ptr(), op, S, 1, None)
