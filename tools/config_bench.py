@@ -141,10 +141,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
+    ap.add_argument("--tune", default="", help="knob=value,... applied with Codec.set_tuning")
     args = ap.parse_args()
     import torch
     fec = importlib.import_module("0xfec_amd")
     codec = fec.Codec(0).use_torch_stream()
+    if args.tune:
+        codec.set_tuning(**{kv.split("=")[0]: int(kv.split("=")[1]) for kv in args.tune.split(",")})
     cases = [("rs23", lambda: run_rs(torch, fec, codec, 2, 1, 65536, 0, max(args.iters, 100), 0x0FEC)),
              ("rs812", lambda: run_rs(torch, fec, codec, 8, 4, 1 << 20, 0, args.iters, 0x0FEC)),
              ("rs1624", lambda: run_rs(torch, fec, codec, 16, 8, 1 << 19, 8, args.iters, 0x0FEC)),
