@@ -62,6 +62,8 @@ lib.fec_batch_decoder_staged.argtypes = [_vp]
 lib.fec_batch_decoder_in_flight.restype = _sz
 lib.fec_batch_decoder_in_flight.argtypes = [_vp]
 lib.fec_manager_handle_repair_frame_batched.argtypes = [_vp, _u64, _u64, ctypes.c_char_p, _sz, _vp, _vp]
+lib.fec_manager_handle_source_symbol_frame_batched.argtypes = [_vp, _u64, ctypes.c_char_p, _sz, _sz,
+                                                               ctypes.POINTER(_vp), _vp, _vp]
 
 
 class RepairQueue:
@@ -260,3 +262,19 @@ def handle_repair_frame_batched(manager, block_id, parity_id, payload, decoder, 
 Manager.handle_repair_frame_batched = (
     lambda self, block_id, parity_id, payload, decoder, queue:
     handle_repair_frame_batched(self, block_id, parity_id, payload, decoder, queue))
+
+
+def handle_source_symbol_frame_batched(manager, ssid, payload, decoder, queue, cap=MAX_PACKET_BUFFER_SIZE):
+    """Manager.HandleSourceSymbolFrame (manager.go:200-227) -> (payload, err); with
+    set_recover_on_source(True), a source that makes its block recoverable stages the block
+    into `decoder` and the recovered payload reaches `queue` when its batch completes."""
+    payload = bytes(payload)
+    out = _vp()
+    rc = lib.fec_manager_handle_source_symbol_frame_batched(manager._h, ssid, payload, len(payload), cap,
+                                                            ctypes.byref(out), decoder._h, queue._h)
+    return (_bytes(out.value) if rc == FEC_OK else None), _err(rc)
+
+
+Manager.handle_source_symbol_frame_batched = (
+    lambda self, ssid, payload, decoder, queue, cap=MAX_PACKET_BUFFER_SIZE:
+    handle_source_symbol_frame_batched(self, ssid, payload, decoder, queue, cap))

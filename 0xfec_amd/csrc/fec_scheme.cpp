@@ -550,13 +550,43 @@ Error Manager::HandleRepairFrame(const RepairFrame& f, Slice* out) {   // manage
     return Error::nil();
 }
 
-Error Manager::HandleSourceSymbolFrame(const SourceSymbolFrame& f, Slice* out) {   // manager.go:200-227
+Error Manager::HandleSourceSymbolFrame(const SourceSymbolFrame& f, Slice* out, Slice* recovered) {
+    // manager.go:200-227 (+ the optional recover-on-source trigger, default off)
     *out = Slice{};
+    if (recovered) *recovered = Slice{};
     BlockStatus& bs = statusFor(sidToBlockID(f.ssid));
     if (bs.isProcessed) return Error::nil();
     Error e = bs.block->addSourceSymbol(f);
     if (!e.ok()) return e;
     if (bs.block->isComplete()) {
+        bs.block.reset();
+        bs.isProcessed = true;
+    } else if (recoverOnSource_ && bs.block->isRecoverable()) {
+        Slice rec;
+        e = scheme_->recoverSymbolPayloads(*bs.block, &rec);
+        if (!e.ok()) return e;
+        bs.block.reset();
+        bs.isProcessed = true;
+        if (recovered) *recovered = rec;
+    }
+    *out = f.payload;
+    return Error::nil();
+}
+
+Error Manager::HandleSourceSymbolFrameBatched(const SourceSymbolFrame& f, Slice* out, BatchDecoder* dec,
+                                              RecoveredQueue* q) {
+    *out = Slice{};
+    if (!dec) return Error::text("nil batch decoder");
+    BlockStatus& bs = statusFor(sidToBlockID(f.ssid));
+    if (bs.isProcessed) return Error::nil();
+    Error e = bs.block->addSourceSymbol(f);
+    if (!e.ok()) return e;
+    if (bs.block->isComplete()) {
+        bs.block.reset();
+        bs.isProcessed = true;
+    } else if (recoverOnSource_ && bs.block->isRecoverable()) {
+        e = dec->Submit(*bs.block, q);
+        if (!e.ok()) return e;
         bs.block.reset();
         bs.isProcessed = true;
     }
@@ -824,6 +854,25 @@ int fec_manager_handle_source_symbol_frame(fec_manager* m, uint64_t ssid, const 
     return rc;
 }
 
+int fec_manager_set_recover_on_source(fec_manager* m, int on) {
+    if (!m) return FEC_ERR_INVALID_ARG;
+    m->m->SetRecoverOnSource(on != 0);
+    return FEC_OK;
+}
+
+int fec_manager_handle_source_symbol_frame_recover(fec_manager* m, uint64_t ssid, const uint8_t* p, size_t len,
+                                                   size_t cap, fec_bytes** out, fec_bytes** recovered) {
+    if (!m || !out || !recovered || (len && !p)) return FEC_ERR_INVALID_ARG;
+    *out = nullptr;
+    *recovered = nullptr;
+    fec::Slice r, rec;
+    const int rc =
+        report(m->m->HandleSourceSymbolFrame(fec::SourceSymbolFrame{ssid, fec::Slice::from(p, len, cap)}, &r, &rec));
+    if (rc == FEC_OK && !r.nil()) *out = new fec_bytes{r};
+    if (rc == FEC_OK && !rec.nil()) *recovered = new fec_bytes{rec};
+    return rc;
+}
+
 }  // extern "C"
 
 // ------------------------------------------------------------------ C ABI (include/fec_batch.h)
@@ -982,6 +1031,17 @@ int fec_manager_handle_repair_frame_batched(fec_manager* m, uint64_t block_id, u
     return report(m->m->HandleRepairFrameBatched(f, d->d.get(), &q->q));
 }
 
+int fec_manager_handle_source_symbol_frame_batched(fec_manager* m, uint64_t ssid, const uint8_t* p, size_t len,
+                                                   size_t cap, fec_bytes** out, fec_batch_decoder* d,
+                                                   fec_recovered_queue* q) {
+    if (!m || !out || !d || !q || (len && !p)) return FEC_ERR_INVALID_ARG;
+    *out = nullptr;
+    fec::Slice r;
+    const int rc = report(m->m->HandleSourceSymbolFrameBatched(
+        fec::SourceSymbolFrame{ssid, fec::Slice::from(p, len, cap)}, &r, d->d.get(), &q->q));
+    if (rc == FEC_OK && !r.nil()) *out = new fec_bytes{r};
+    return rc;
+}
 
 int fec_batch_encoder_submit_payloads(fec_batch_encoder* e, uint64_t block_id, const uint8_t* const* payloads,
                                       const size_t* lens, int count, fec_repair_queue* q) {

@@ -71,6 +71,8 @@ lib.fec_manager_block_id.argtypes = [_vp, _u64]
 lib.fec_manager_add_source_symbol_frame.argtypes = [_vp, _u64, ctypes.c_char_p, _sz, _sz, _pp]
 lib.fec_manager_handle_repair_frame.argtypes = [_vp, _u64, _u64, ctypes.c_char_p, _sz, _pp]
 lib.fec_manager_handle_source_symbol_frame.argtypes = [_vp, _u64, ctypes.c_char_p, _sz, _sz, _pp]
+lib.fec_manager_set_recover_on_source.argtypes = [_vp, _i]
+lib.fec_manager_handle_source_symbol_frame_recover.argtypes = [_vp, _u64, ctypes.c_char_p, _sz, _sz, _pp, _pp]
 
 
 def _err(rc):
@@ -234,6 +236,21 @@ class Manager:
         rc = lib.fec_manager_handle_source_symbol_frame(self._h, ssid, payload, len(payload), cap,
                                                         ctypes.byref(out))
         return (_bytes(out.value) if rc == FEC_OK else None), _err(rc)
+
+    def set_recover_on_source(self, on=True):
+        """Extension (default off): also recover when a SOURCE symbol makes a block recoverable;
+        the reference recovers only on a REPAIR arrival (manager.go:181 vs :221-226)."""
+        lib.fec_manager_set_recover_on_source(self._h, 1 if on else 0)
+
+    def handle_source_symbol_frame_recover(self, ssid, payload, cap=MAX_PACKET_BUFFER_SIZE):
+        """HandleSourceSymbolFrame plus what it recovered -> (payload, recovered | None, err)."""
+        payload = bytes(payload)
+        out, rec = _vp(), _vp()
+        rc = lib.fec_manager_handle_source_symbol_frame_recover(self._h, ssid, payload, len(payload), cap,
+                                                                ctypes.byref(out), ctypes.byref(rec))
+        if rc != FEC_OK:
+            return None, None, _err(rc)
+        return _bytes(out.value), _bytes(rec.value), None
 
 
 def _mk(fn, *args):

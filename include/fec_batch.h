@@ -19,6 +19,10 @@
  *   fec_batch_decoder_*                           deferred recoverSymbolPayloads for many blocks
  *   fec_manager_handle_repair_frame_batched       HandleRepairFrame       manager.go:160-198,
  *                                                 recovery deferred to a batch decoder
+ *   fec_manager_handle_source_symbol_frame_batched HandleSourceSymbolFrame manager.go:200-227;
+ *                                                 with fec_manager_set_recover_on_source on, a
+ *                                                 source that makes its block recoverable
+ *                                                 stages it into the batch decoder
  */
 #ifndef FEC_BATCH_H
 #define FEC_BATCH_H
@@ -84,6 +88,9 @@ size_t fec_batch_decoder_in_flight(const fec_batch_decoder *d);
 
 int fec_manager_handle_repair_frame_batched(fec_manager *m, uint64_t block_id, uint64_t parity_id, const uint8_t *p,
                                             size_t len, fec_batch_decoder *d, fec_recovered_queue *q);
+int fec_manager_handle_source_symbol_frame_batched(fec_manager *m, uint64_t ssid, const uint8_t *p, size_t len,
+                                                   size_t cap, fec_bytes **out, fec_batch_decoder *d,
+                                                   fec_recovered_queue *q);
 
 #ifdef __cplusplus
 }

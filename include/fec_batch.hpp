@@ -165,6 +165,7 @@ public:
     Error Drain(size_t* blocks = nullptr);
     size_t Staged() const;
     size_t InFlight() const;
+    DecoderFECScheme scheme() const { return scheme_; }
 
 private:
     struct Pending {

@@ -29,6 +29,13 @@
  *   fec_manager_add_source_symbol_frame       AddSourceSymbolFrame    manager.go:123-158
  *   fec_manager_handle_repair_frame           HandleRepairFrame       manager.go:160-198
  *   fec_manager_handle_source_symbol_frame    HandleSourceSymbolFrame manager.go:200-227
+ *
+ * Extension (off by default so the default behaviour is the reference's):
+ *   fec_manager_set_recover_on_source         recovery also fires when a SOURCE symbol makes a
+ *                                             block recoverable (the reference only recovers on
+ *                                             a REPAIR arrival, manager.go:181 vs :221-226)
+ *   fec_manager_handle_source_symbol_frame_recover   HandleSourceSymbolFrame + the recovered
+ *                                             payloads (NULL unless this call recovered)
  */
 #ifndef FEC_SCHEME_H
 #define FEC_SCHEME_H
@@ -101,6 +108,10 @@ int fec_manager_handle_repair_frame(fec_manager *m, uint64_t block_id, uint64_t 
                                     const uint8_t *p, size_t len, fec_bytes **out);
 int fec_manager_handle_source_symbol_frame(fec_manager *m, uint64_t ssid, const uint8_t *p,
                                            size_t len, size_t cap, fec_bytes **out);
+int fec_manager_set_recover_on_source(fec_manager *m, int on);
+int fec_manager_handle_source_symbol_frame_recover(fec_manager *m, uint64_t ssid, const uint8_t *p,
+                                                   size_t len, size_t cap, fec_bytes **out,
+                                                   fec_bytes **recovered);
 
 #ifdef __cplusplus
 }

@@ -178,7 +178,15 @@ public:
     SourceSymbolID NextSSID();
     Error AddSourceSymbolFrame(const SourceSymbolFrame& f, std::vector<RepairFrame>* out);
     Error HandleRepairFrame(const RepairFrame& f, Slice* out);
-    Error HandleSourceSymbolFrame(const SourceSymbolFrame& f, Slice* out);
+    // manager.go:200-227. `recovered` (optional) receives the payloads recovered because this
+    // source made the block recoverable; only with SetRecoverOnSource(true), else it stays nil.
+    Error HandleSourceSymbolFrame(const SourceSymbolFrame& f, Slice* out, Slice* recovered = nullptr);
+    // Off by default (reference behaviour): recovery fires only on a REPAIR arrival
+    // (manager.go:181), so a block whose repairs arrived before its k-th surviving source is
+    // never recovered (manager.go:221-226 only checks isComplete). On: a source arrival that
+    // makes the block recoverable but not complete recovers it too.
+    void SetRecoverOnSource(bool on) { recoverOnSource_ = on; }
+    bool RecoverOnSource() const { return recoverOnSource_; }
     BlockID sidToBlockID(SourceSymbolID sid) const;
     size_t trackedBlocks() const { return blockStatuses_.size(); }
     // AddSourceSymbolFrame with the encode deferred to a batch: on the k-th source symbol the
@@ -189,6 +197,10 @@ public:
     // recoverable it is staged into `dec`, dropped and marked processed; its recovered payload
     // reaches `q` when the batch completes.
     Error HandleRepairFrameBatched(const RepairFrame& f, class BatchDecoder* dec, class RecoveredQueue* q);
+    // HandleSourceSymbolFrame (the payload is returned in *out, as there) with the
+    // recover-on-source recovery, when enabled, deferred to `dec` like HandleRepairFrameBatched.
+    Error HandleSourceSymbolFrameBatched(const SourceSymbolFrame& f, Slice* out, class BatchDecoder* dec,
+                                         class RecoveredQueue* q);
     BlockFECScheme* scheme() { return scheme_.get(); }
 
 private:
@@ -203,6 +215,7 @@ private:
     int numTotSourceSymbols_ = 0;
     int numTotRepairSymbols_ = 0;
     std::map<BlockID, BlockStatus> blockStatuses_;
+    bool recoverOnSource_ = false;
 };
 
 // manager.go:50-94: XOR -> (2,1), ReedSolomon -> (20,10); FECDisabled -> nil manager, nil error.

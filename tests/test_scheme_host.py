@@ -113,3 +113,17 @@ def test_receiver_source_path_and_processed_blocks(S):
     assert (got, err) == (None, None)
     got, err = m.handle_repair_frame(5, 0, b"\x01\x02\x03")   # block 5: 1 repair < k=2
     assert (got, err) == (None, None)
+
+
+def test_recover_on_source_flag_without_recovery(S):
+    """The recover-on-source extension (off by default) changes nothing while no block becomes
+    recoverable by a source: payloads come back, complete blocks are processed — no arithmetic."""
+    m, _ = S.new_receiver(S.XOR_FEC_SCHEME)
+    m.set_recover_on_source(True)
+    assert m.handle_source_symbol_frame_recover(0, b"first") == (b"first", None, None)
+    assert m.handle_source_symbol_frame_recover(1, b"second") == (b"second", None, None)
+    assert m.handle_source_symbol_frame_recover(0, b"again") == (None, None, None)   # processed
+    got, err = m.handle_repair_frame(5, 0, b"\x01\x02\x03")                          # 1 repair < k=2
+    assert (got, err) == (None, None)
+    m.set_recover_on_source(False)
+    assert m.handle_source_symbol_frame_recover(12, b"x") == (b"x", None, None)
