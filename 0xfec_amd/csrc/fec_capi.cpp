@@ -520,7 +520,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 12 ? &fk::g_tune.dec_swz : key == 13 ? &fk::g_tune.gen_wpc
               : key == 14 ? &fk::g_tune.enc_queue : key == 15 ? &fk::g_tune.enc_qwpc
               : key == 16 ? &fk::g_tune.enc_qdepth : key == 17 ? &fk::g_tune.dec_wave
-              : key == 18 ? &fk::g_tune.enc_diag : key == 19 ? &fk::g_tune.dec_fused : nullptr;
+              : key == 18 ? &fk::g_tune.enc_diag : key == 19 ? &fk::g_tune.dec_fused
+              : key == 20 ? &fk::g_tune.dec_ipl : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

@@ -630,6 +630,84 @@ __device__ __forceinline__ uint32_t wave_rows(uint32_t nout) {
     return rows;
 }
 
+// Two items per lane (the lane's chunk in this wave's first and second 64-item run): both
+// items' k loads are issued before either is folded, so a wave keeps twice the bytes in flight
+// behind one plan stage. Items of blocks with nothing to rebuild (nout == 0) load nothing.
+template <int MAXE, bool NTL, bool NTS>
+__device__ __forceinline__ void recon_pair(const ReconArgs& a, const uint8_t* PA, const gf::PermTab* TA,
+                                           uint32_t blkA, uint32_t cA, uint32_t rowsA, uint32_t noutA,
+                                           const uint8_t* PB, const gf::PermTab* TB, uint32_t blkB, uint32_t cB,
+                                           uint32_t rowsB, uint32_t noutB) {
+    const uint32_t k = a.k;
+    const PlanLayout& lay = a.lay;
+    uint8_t* dA = a.data + (uint64_t)blkA * a.dbs + (uint64_t)cA * kChunk;
+    const uint8_t* pA = a.parity + (uint64_t)blkA * a.pbs + (uint64_t)cA * kChunk;
+    uint8_t* dB = a.data + (uint64_t)blkB * a.dbs + (uint64_t)cB * kChunk;
+    const uint8_t* pB = a.parity + (uint64_t)blkB * a.pbs + (uint64_t)cB * kChunk;
+    uint32_t accA[MAXE][4], accB[MAXE][4];
+#pragma unroll
+    for (int r = 0; r < MAXE; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) accA[r][q] = accB[r][q] = 0;
+    for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
+        const uint2 slA = *reinterpret_cast<const uint2*>(PA + lay.in_off + j0);
+        const uint2 slB = *reinterpret_cast<const uint2*>(PB + lay.in_off + j0);
+        uint4 xa[kInGroup], xb[kInGroup];
+#pragma unroll
+        for (int jj = 0; jj < kInGroup; ++jj) {
+            const uint32_t sa = ((jj < 4 ? slA.x : slA.y) >> (8 * (jj & 3))) & 0xFFu;
+            const uint32_t sb = ((jj < 4 ? slB.x : slB.y) >> (8 * (jj & 3))) & 0xFFu;
+            xa[jj] = j0 + jj < k && noutA
+                         ? ld16<NTL>(sa < k ? dA + (uint64_t)sa * a.ss : pA + (uint64_t)(sa - k) * a.ss)
+                         : make_uint4(0, 0, 0, 0);
+            xb[jj] = j0 + jj < k && noutB
+                         ? ld16<NTL>(sb < k ? dB + (uint64_t)sb * a.ss : pB + (uint64_t)(sb - k) * a.ss)
+                         : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int jj = 0; jj < kInGroup; jj += 2) {
+            const uint32_t j = j0 + jj;
+            if (j + 1 < k) {
+                Idx ia[4], ib[4];
+                split4(ia, xa[jj]);
+                split4(ib, xa[jj + 1]);
+#pragma unroll
+                for (int r = 0; r < MAXE; ++r)
+                    if (r < (int)rowsA) mac2(accA[r], ia, ib, TA + r * k + j, TA + r * k + j + 1);
+                split4(ia, xb[jj]);
+                split4(ib, xb[jj + 1]);
+#pragma unroll
+                for (int r = 0; r < MAXE; ++r)
+                    if (r < (int)rowsB) mac2(accB[r], ia, ib, TB + r * k + j, TB + r * k + j + 1);
+            } else if (j < k) {
+                Idx ia[4];
+                split4(ia, xa[jj]);
+#pragma unroll
+                for (int r = 0; r < MAXE; ++r)
+                    if (r < (int)rowsA) mac1(accA[r], ia, TA + r * k + j);
+                split4(ia, xb[jj]);
+#pragma unroll
+                for (int r = 0; r < MAXE; ++r)
+                    if (r < (int)rowsB) mac1(accB[r], ia, TB + r * k + j);
+            }
+        }
+    }
+    const uint8_t* oiA = PA + lay.out_off;
+    const uint8_t* oiB = PB + lay.out_off;
+    uint8_t* oA = a.out ? a.out + (uint64_t)blkA * a.out_bs + (uint64_t)cA * kChunk : nullptr;
+    uint8_t* oB = a.out ? a.out + (uint64_t)blkB * a.out_bs + (uint64_t)cB * kChunk : nullptr;
+#pragma unroll
+    for (int r = 0; r < MAXE; ++r)
+        if (r < (int)noutA)
+            store_chunk<NTS>(oA ? oA + (uint64_t)r * a.ss : dA + (uint64_t)oiA[r] * a.ss, as_uint4(accA[r]),
+                             a.len - cA * kChunk, a.pad_zero);
+#pragma unroll
+    for (int r = 0; r < MAXE; ++r)
+        if (r < (int)noutB)
+            store_chunk<NTS>(oB ? oB + (uint64_t)r * a.ss : dB + (uint64_t)oiB[r] * a.ss, as_uint4(accB[r]),
+                             a.len - cB * kChunk, a.pad_zero);
+}
+
 // Tile form: a workgroup takes tiles of G consecutive blocks: it stages their plans in LDS,
 // expands every coefficient to its PermTab once, then lanes sweep the G*cps (block, chunk)
 // items. Rows beyond a block's own erasure count carry zero tables, and each item loops only
@@ -716,7 +794,7 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int MAXE, int POL, bool FUSED>
+template <int MAXE, int POL, bool FUSED, int IPL>
 __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs a) {
     constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -744,10 +822,10 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
     gf::PermTab* tabs = reinterpret_cast<gf::PermTab*>(slice);                      // 3*maxe*k
     uint8_t* plans = slice + (size_t)kWaveBlocks * maxe * k * sizeof(gf::PermTab);  // 3*stride
     const uint32_t total = a.nblocks * a.cps;
-    const uint32_t i0 = (xcd_order(a.swz) * kThreads) + (wave << 6);
+    const uint32_t i0 = (xcd_order(a.swz) * kThreads + (wave << 6)) * IPL;
     if (i0 >= total) return;
     const uint32_t bfirst = fdiv(i0, a.div_cps);
-    const uint32_t nb = fdiv(min(i0 + 63u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
+    const uint32_t nb = fdiv(min(i0 + 64u * IPL - 1u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
     if constexpr (!FUSED) {
         const uint32_t nw = nb * lay.stride / 16;
         const uint4* src = reinterpret_cast<const uint4*>(a.plans + (uint64_t)bfirst * lay.stride);
@@ -840,16 +918,30 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
         }
     }
     wave_sync();
-    const uint32_t item = i0 + lane;
-    const bool inr = item < total;
-    const uint32_t blk = inr ? fdiv(item, a.div_cps) : bfirst;
-    const uint32_t g = blk - bfirst;
-    const uint32_t c = item - blk * a.cps;
-    const uint8_t* P = plans + g * lay.stride;
-    const uint32_t nout = inr ? P[lay.nout_off] : 0;
-    const uint32_t rows = wave_rows<MAXE>(nout);
-    if (nout == 0) return;
-    recon_item<MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, blk, c, rows, nout);
+    if constexpr (IPL == 1) {
+        const uint32_t item = i0 + lane;
+        const bool inr = item < total;
+        const uint32_t blk = inr ? fdiv(item, a.div_cps) : bfirst;
+        const uint32_t g = blk - bfirst;
+        const uint32_t c = item - blk * a.cps;
+        const uint8_t* P = plans + g * lay.stride;
+        const uint32_t nout = inr ? P[lay.nout_off] : 0;
+        const uint32_t rows = wave_rows<MAXE>(nout);
+        if (nout == 0) return;
+        recon_item<MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, blk, c, rows, nout);
+    } else {
+        const uint32_t itA = i0 + lane, itB = itA + 64;
+        const bool inA = itA < total, inB = itB < total;
+        const uint32_t bA = inA ? fdiv(itA, a.div_cps) : bfirst;
+        const uint32_t bB = inB ? fdiv(itB, a.div_cps) : bfirst;
+        const uint8_t* PA = plans + (bA - bfirst) * lay.stride;
+        const uint8_t* PB = plans + (bB - bfirst) * lay.stride;
+        const uint32_t nA = inA ? PA[lay.nout_off] : 0, nB = inB ? PB[lay.nout_off] : 0;
+        const uint32_t rA = wave_rows<MAXE>(nA), rB = wave_rows<MAXE>(nB);
+        if ((nA | nB) == 0) return;
+        recon_pair<MAXE, NTL, NTS>(a, PA, tabs + (bA - bfirst) * maxe * k, bA, itA - bA * a.cps, rA, nA, PB,
+                                   tabs + (bB - bfirst) * maxe * k, bB, itB - bB * a.cps, rB, nB);
+    }
 }
 
 // ------------------------------------------------------------------ XOR
@@ -1042,9 +1134,10 @@ bool wave_recon_applies(uint32_t cps, uint32_t k, uint32_t maxe, uint32_t stride
     return g_tune.dec_wave && cps >= 32 && 4 * fused_slice_bytes(k, maxe, stride) + 2048 <= 65536;
 }
 
-template <int POL, bool FUSED>
+template <int POL, bool FUSED, int IPL>
 static hipError_t recon_wave_dispatch(const ReconArgs& a, hipStream_t s) {
-    const int grid = (int)(((uint64_t)a.nblocks * a.cps + kThreads - 1) / kThreads);
+    const uint64_t per_wg = (uint64_t)kThreads * IPL;
+    const int grid = (int)(((uint64_t)a.nblocks * a.cps + per_wg - 1) / per_wg);
     if (grid == 0) return hipSuccess;
     size_t own = 4 * wave_slice_bytes(a.k, a.maxe, a.lay.stride);
     if (FUSED) {
@@ -1052,25 +1145,41 @@ static hipError_t recon_wave_dispatch(const ReconArgs& a, hipStream_t s) {
         own = L.slices + 4 * L.slice;
     }
     const size_t lds = occupancy_lds(g_tune.dec_wpc, own);
-    if (a.maxe <= 1) hipLaunchKernelGGL((rs_reconstruct_wave_kernel<1, POL, FUSED>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (a.maxe <= 2) hipLaunchKernelGGL((rs_reconstruct_wave_kernel<2, POL, FUSED>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (a.maxe <= 4) hipLaunchKernelGGL((rs_reconstruct_wave_kernel<4, POL, FUSED>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (a.maxe <= 8) hipLaunchKernelGGL((rs_reconstruct_wave_kernel<8, POL, FUSED>), dim3(grid), dim3(kThreads), lds, s, a);
-    else hipLaunchKernelGGL((rs_reconstruct_wave_kernel<16, POL, FUSED>), dim3(grid), dim3(kThreads), lds, s, a);
+#define FEC_WAVE_LAUNCH(E) \
+    hipLaunchKernelGGL((rs_reconstruct_wave_kernel<E, POL, FUSED, IPL>), dim3(grid), dim3(kThreads), lds, s, a)
+    if (a.maxe <= 1) FEC_WAVE_LAUNCH(1);
+    else if (a.maxe <= 2) FEC_WAVE_LAUNCH(2);
+    else if (a.maxe <= 4) FEC_WAVE_LAUNCH(4);
+    else if constexpr (IPL == 1) {
+        if (a.maxe <= 8) FEC_WAVE_LAUNCH(8);
+        else FEC_WAVE_LAUNCH(16);
+    }
+#undef FEC_WAVE_LAUNCH
     return hipGetLastError();
+}
+
+// Items per lane of the wave form (knob dec_ipl: 0 auto, 1, 2). Two items per lane pay for
+// latency-bound shapes (RS(2,3): 57 -> 51.5 us per 2^16 blocks) and cost 17 % where HBM is
+// the bound (RS(8,12)), so auto picks 2 for k <= 4. Two need at most 4 rebuilt rows (registers)
+// and shards of 64+ chunks (the 128-item span then still covers at most 3 blocks).
+template <int POL, bool FUSED>
+static hipError_t recon_wave_ipl(const ReconArgs& a, hipStream_t s) {
+    const int ipl = g_tune.dec_ipl ? g_tune.dec_ipl : (a.k <= 4 ? 2 : 1);
+    if (ipl == 2 && a.maxe <= 4 && a.cps >= 64) return recon_wave_dispatch<POL, FUSED, 2>(a, s);
+    return recon_wave_dispatch<POL, FUSED, 1>(a, s);
 }
 
 hipError_t launch_rs_reconstruct_wave(const ReconArgs& a, hipStream_t s) {
     switch (g_tune.dec_nt & 3) {
-        case 0: return recon_wave_dispatch<0, false>(a, s);
-        case 1: return recon_wave_dispatch<1, false>(a, s);
-        case 2: return recon_wave_dispatch<2, false>(a, s);
-        default: return recon_wave_dispatch<3, false>(a, s);
+        case 0: return recon_wave_ipl<0, false>(a, s);
+        case 1: return recon_wave_ipl<1, false>(a, s);
+        case 2: return recon_wave_ipl<2, false>(a, s);
+        default: return recon_wave_ipl<3, false>(a, s);
     }
 }
 
 hipError_t launch_rs_recover_fused(const ReconArgs& a, hipStream_t s) {
-    return (g_tune.dec_nt & 3) == 3 ? recon_wave_dispatch<3, true>(a, s) : recon_wave_dispatch<0, true>(a, s);
+    return (g_tune.dec_nt & 3) == 3 ? recon_wave_ipl<3, true>(a, s) : recon_wave_ipl<0, true>(a, s);
 }
 
 hipError_t launch_rs_reconstruct(const ReconArgs& a, int grid, hipStream_t s) {

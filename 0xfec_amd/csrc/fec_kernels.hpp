@@ -122,6 +122,7 @@ struct Tuning {
     int dec_wave = 1;         // reconstruct: wave-private plan staging (shards of 32+ chunks)
     int dec_fused = 0;        // ... with the plans built inside the wave kernel (measured 11 % slower: off)
     int enc_diag = 0;         // diagnostics only: queue kernel without the field arithmetic (wrong output)
+    int dec_ipl = 0;          // wave-form reconstruct: items per lane (1, 2; 0: 2 for k <= 4, else 1)
 };
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):

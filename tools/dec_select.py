@@ -20,13 +20,14 @@ def main():
     erased = torch.randint(0, k, (B,), device="cuda")
     masks = ((1 << (k + m)) - 1 - (1 << erased)).to(torch.int32)
     dp, pp, op = data.data_ptr(), par.data_ptr(), out.data_ptr()
-    variants = {"wave fused": dict(dec_wave=1, dec_fused=1, dec_wpc=0, dec_swz=0),
-                "wave + plan kernel": dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=0)}
-    for w in (4, 5):
-        variants["wave fused wpc%d" % w] = dict(dec_wave=1, dec_fused=1, dec_wpc=w, dec_swz=0)
-    variants["wave fused swz"] = dict(dec_wave=1, dec_fused=1, dec_wpc=0, dec_swz=1)
-    variants["tile + plan kernel"] = dict(dec_wave=0, dec_fused=0, dec_wpc=0, dec_swz=0)
-    base = codec.set_tuning(dec_wave=1, dec_fused=1, dec_wpc=0, dec_swz=0)
+    variants = {"wave + plan kernel": dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=0, dec_ipl=1),
+                "ipl2 + plan kernel": dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=0, dec_ipl=2),
+                "ipl2 fused": dict(dec_wave=1, dec_fused=1, dec_wpc=0, dec_swz=0, dec_ipl=2),
+                "ipl2 swz": dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=1, dec_ipl=2)}
+    for w in (2, 3, 4):
+        variants["ipl2 wpc%d" % w] = dict(dec_wave=1, dec_fused=0, dec_wpc=w, dec_swz=0, dec_ipl=2)
+        variants["ipl2 wpc%d swz" % w] = dict(dec_wave=1, dec_fused=0, dec_wpc=w, dec_swz=1, dec_ipl=2)
+    base = codec.set_tuning(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=0, dec_ipl=1)
 
     def run():
         codec.rs_recover_raw(k, m, L, B, dp, k * S, pp, m * S, S, masks.data_ptr(), op, S, 1, None)
@@ -42,6 +43,16 @@ def main():
         torch.cuda.synchronize()
         return s.elapsed_time(e) / iters / 1e3
 
+    run()
+    torch.cuda.synchronize()
+    run_ref = out.clone()
+    for n, kv in variants.items():
+        codec.set_tuning(**kv)
+        out.zero_()
+        run()
+        torch.cuda.synchronize()
+        assert torch.equal(out, run_ref), n
+        codec.set_tuning(**base)
     res = {n: [] for n in variants}
     for _ in range(8):
         for n, kv in variants.items():
