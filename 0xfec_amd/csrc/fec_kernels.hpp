@@ -111,7 +111,7 @@ struct Tuning {
     int tiles_per_wg = 1;     // >0: decode grid = ntiles / tiles_per_wg; 0: persistent
     int rotate = 0;           // rotate chunk order so shard boundaries share a wave (measured: no gain)
     int xcd_swz = 1;          // encode / XOR: workgroups of one XCD take one contiguous range of the grid
-    int dec_swz = 0;          // same for reconstruct
+    int dec_swz = 1;          // same for reconstruct
     int enc_wpc = 4;          // resident workgroups per CU, fixed-shape encode (0: as many as fit)
     int gen_wpc = 0;          // same for the generic encode and XOR encode
     int dec_wpc = 0;          // same for reconstruct

@@ -20,44 +20,49 @@ def main():
     erased = torch.randint(0, k, (B,), device="cuda")
     masks = ((1 << (k + m)) - 1 - (1 << erased)).to(torch.int32)
     dp, pp, op = data.data_ptr(), par.data_ptr(), out.data_ptr()
-    variants = {"wave + plan kernel": dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=0, dec_ipl=1),
-                "ipl2 + plan kernel": dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=0, dec_ipl=2),
-                "ipl2 fused": dict(dec_wave=1, dec_fused=1, dec_wpc=0, dec_swz=0, dec_ipl=2),
-                "ipl2 swz": dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=1, dec_ipl=2)}
-    for w in (2, 3, 4):
-        variants["ipl2 wpc%d" % w] = dict(dec_wave=1, dec_fused=0, dec_wpc=w, dec_swz=0, dec_ipl=2)
-        variants["ipl2 wpc%d swz" % w] = dict(dec_wave=1, dec_fused=0, dec_wpc=w, dec_swz=1, dec_ipl=2)
-    base = codec.set_tuning(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=0, dec_ipl=1)
+    D = dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=1, dec_ipl=0)
+    # name -> (tuning, output slots per block: the recover plans min(k, m, slots) rows). With
+    # one erasure per block only slot 0 is written, so the 4-slot runs use the same one-slot
+    # buffer (block stride S): identical stores, only the planned row count differs.
+    variants = {"wave, 1 slot": (dict(D, dec_swz=0), 1),
+                "wave, 4 slots": (dict(D, dec_swz=0), 4),
+                "wave swz, 1 slot (default)": (D, 1),
+                "wave swz, 4 slots": (D, 4),
+                "wave fused swz, 1 slot": (dict(D, dec_fused=1, dec_swz=1), 1),
+                "wave ipl2 swz, 1 slot": (dict(D, dec_ipl=2, dec_swz=1), 1)}
+    for w in (4, 5, 6):
+        variants["wave swz wpc%d, 1 slot" % w] = (dict(D, dec_swz=1, dec_wpc=w), 1)
+    base = codec.set_tuning(**D)
 
-    def run():
-        codec.rs_recover_raw(k, m, L, B, dp, k * S, pp, m * S, S, masks.data_ptr(), op, S, 1, None)
+    def run(slots=1):
+        codec.rs_recover_raw(k, m, L, B, dp, k * S, pp, m * S, S, masks.data_ptr(), op, S, slots, None)
 
-    def t(iters=5):
-        run()
+    def t(slots, iters=5):
+        run(slots)
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         for _ in range(iters):
-            run()
+            run(slots)
         e.record()
         torch.cuda.synchronize()
         return s.elapsed_time(e) / iters / 1e3
 
     run()
     torch.cuda.synchronize()
-    run_ref = out.clone()
-    for n, kv in variants.items():
+    ref = out.clone()
+    for n, (kv, slots) in variants.items():
         codec.set_tuning(**kv)
         out.zero_()
-        run()
+        run(slots)
         torch.cuda.synchronize()
-        assert torch.equal(out, run_ref), n
+        assert torch.equal(out, ref), n
         codec.set_tuning(**base)
     res = {n: [] for n in variants}
     for _ in range(8):
-        for n, kv in variants.items():
+        for n, (kv, slots) in variants.items():
             codec.set_tuning(**kv)
-            res[n].append(B * (k + 1) * L / t() / 1e9)
+            res[n].append(B * (k + 1) * L / t(slots) / 1e9)
             codec.set_tuning(**base)
     print(json.dumps({n: [round(sorted(v)[len(v) // 2], 1), round(max(v), 1)] for n, v in res.items()}))
 

@@ -1,0 +1,24 @@
+#!/bin/bash
+# One GPU box call that refreshes every measured artifact of a round (run through gpurun from
+# the repo root; each GPU step under its own time limit, steps chained so the first failure
+# ends the call):
+#   gpu tests -> bench.py -> rocprofv3 kernel stats of bench.py -> PMC FETCH_SIZE / WRITE_SIZE
+#   passes -> per-kernel HBM bytes -> every BASELINE config (tools/config_bench.py)
+# usage: tools/gpu_round.sh TAG      (outputs under gpurun_out/TAG/)
+set -eo pipefail
+TAG=${1:?tag}
+R=$(pwd)
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$O/pytest_gpu.log" 2>&1
+tail -2 "$O/pytest_gpu.log"
+timeout -k 10 300 python -u bench.py > "$O/bench.log" 2>&1
+tail -1 "$O/bench.log"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- python3 "$R/bench.py" --steps 20 --no-cpu-baseline > "$O/prof.log" 2>&1
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$O/pmc_fetch.log" 2>&1
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$O/pmc_write.log" 2>&1
+cd "$R"
+python tools/pmc_traffic.py "$O/pmc_fetch" "$O/pmc_write" "$O/pmc_traffic.json"
+timeout -k 10 300 python -u tools/config_bench.py > "$O/config_bench.log" 2>&1
+grep -v amdgpu.ids "$O/config_bench.log"
