@@ -253,6 +253,7 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
         a.rot = fk::g_tune.rotate ? fk::line_rotation(ss, cps) : 0;
         a.swz = (uint32_t)fk::g_tune.dec_swz;
+        a.diag = (uint32_t)fk::g_tune.dec_diag;
         a.out = out ? out + b0 * out_bs : nullptr;
         a.out_bs = out_bs;
         if (fused) {
@@ -521,7 +522,7 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 14 ? &fk::g_tune.enc_queue : key == 15 ? &fk::g_tune.enc_qwpc
               : key == 16 ? &fk::g_tune.enc_qdepth : key == 17 ? &fk::g_tune.dec_wave
               : key == 18 ? &fk::g_tune.enc_diag : key == 19 ? &fk::g_tune.dec_fused
-              : key == 20 ? &fk::g_tune.dec_ipl : nullptr;
+              : key == 20 ? &fk::g_tune.dec_ipl : key == 21 ? &fk::g_tune.dec_diag : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

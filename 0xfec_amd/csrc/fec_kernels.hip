@@ -828,7 +828,7 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
     const uint32_t nb = fdiv(min(i0 + 64u * IPL - 1u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
     if constexpr (!FUSED) {
         const uint32_t nw = nb * lay.stride / 16;
-        const uint4* src = reinterpret_cast<const uint4*>(a.plans + (uint64_t)bfirst * lay.stride);
+        const uint4* src = reinterpret_cast<const uint4*>(a.plans + (a.diag ? 0 : (uint64_t)bfirst * lay.stride));
         if (lane < nw) reinterpret_cast<uint4*>(plans)[lane] = src[lane];
     } else {
         uint8_t* Dt = plans + (size_t)kWaveBlocks * lay.stride;   // k bytes

@@ -75,6 +75,7 @@ struct ReconArgs {
     uint8_t* out;              // recover: rebuilt shard r of block b at out + b*out_bs + r*ss
     uint64_t out_bs;           //          (nullptr: rebuild in place into the data region)
     uint32_t swz;
+    uint32_t diag;             // diagnostics (knob dec_diag): every wave stages block 0's plan (wrong output)
     // fused form (plans built in the reconstruct kernel, no rs_plan_kernel): as PlanArgs
     const uint32_t* masks;
     int32_t* status;
@@ -122,6 +123,7 @@ struct Tuning {
     int dec_wave = 1;         // reconstruct: wave-private plan staging (shards of 32+ chunks)
     int dec_fused = 0;        // ... with the plans built inside the wave kernel (measured 11 % slower: off)
     int enc_diag = 0;         // diagnostics only: queue kernel without the field arithmetic (wrong output)
+    int dec_diag = 0;         // diagnostics only: wave reconstruct with one shared plan (wrong output)
     int dec_ipl = 0;          // wave-form reconstruct: items per lane (1, 2; 0: 2 for k <= 4, else 1)
 };
 
