@@ -822,10 +822,11 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
     gf::PermTab* tabs = reinterpret_cast<gf::PermTab*>(slice);                      // 3*maxe*k
     uint8_t* plans = slice + (size_t)kWaveBlocks * maxe * k * sizeof(gf::PermTab);  // 3*stride
     const uint32_t total = a.nblocks * a.cps;
-    const uint32_t i0 = (xcd_order(a.swz) * kThreads + (wave << 6)) * IPL;
+    constexpr uint32_t NI = IPL < 0 ? -IPL : IPL;   // items per lane; IPL < 0: one after the other
+    const uint32_t i0 = (xcd_order(a.swz) * kThreads + (wave << 6)) * NI;
     if (i0 >= total) return;
     const uint32_t bfirst = fdiv(i0, a.div_cps);
-    const uint32_t nb = fdiv(min(i0 + 64u * IPL - 1u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
+    const uint32_t nb = fdiv(min(i0 + 64u * NI - 1u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
     if constexpr (!FUSED) {
         const uint32_t nw = nb * lay.stride / 16;
         const uint4* src = reinterpret_cast<const uint4*>(a.plans + (a.diag ? 0 : (uint64_t)bfirst * lay.stride));
@@ -918,7 +919,20 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
         }
     }
     wave_sync();
-    if constexpr (IPL == 1) {
+    if constexpr (IPL < 0) {
+        // the wave's items one 64-item run after the other, behind one plan stage
+        for (uint32_t u = 0; u < NI; ++u) {
+            const uint32_t item = i0 + u * 64 + lane;
+            const bool inr = item < total;
+            const uint32_t blk = inr ? fdiv(item, a.div_cps) : bfirst;
+            const uint32_t g = blk - bfirst;
+            const uint32_t c = item - blk * a.cps;
+            const uint8_t* P = plans + g * lay.stride;
+            const uint32_t nout = inr ? P[lay.nout_off] : 0;
+            const uint32_t rows = wave_rows<MAXE>(nout);
+            if (nout) recon_item<MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, blk, c, rows, nout);
+        }
+    } else if constexpr (IPL == 1) {
         const uint32_t item = i0 + lane;
         const bool inr = item < total;
         const uint32_t blk = inr ? fdiv(item, a.div_cps) : bfirst;
@@ -1136,7 +1150,7 @@ bool wave_recon_applies(uint32_t cps, uint32_t k, uint32_t maxe, uint32_t stride
 
 template <int POL, bool FUSED, int IPL>
 static hipError_t recon_wave_dispatch(const ReconArgs& a, hipStream_t s) {
-    const uint64_t per_wg = (uint64_t)kThreads * IPL;
+    const uint64_t per_wg = (uint64_t)kThreads * (IPL < 0 ? -IPL : IPL);
     const int grid = (int)(((uint64_t)a.nblocks * a.cps + per_wg - 1) / per_wg);
     if (grid == 0) return hipSuccess;
     size_t own = 4 * wave_slice_bytes(a.k, a.maxe, a.lay.stride);
@@ -1150,9 +1164,11 @@ static hipError_t recon_wave_dispatch(const ReconArgs& a, hipStream_t s) {
     if (a.maxe <= 1) FEC_WAVE_LAUNCH(1);
     else if (a.maxe <= 2) FEC_WAVE_LAUNCH(2);
     else if (a.maxe <= 4) FEC_WAVE_LAUNCH(4);
-    else if constexpr (IPL == 1) {
+    else if constexpr (IPL != 2) {   // the pair form is only built for up to 4 rows
         if (a.maxe <= 8) FEC_WAVE_LAUNCH(8);
         else FEC_WAVE_LAUNCH(16);
+    } else {
+        return hipErrorInvalidValue;
     }
 #undef FEC_WAVE_LAUNCH
     return hipGetLastError();
@@ -1166,6 +1182,7 @@ template <int POL, bool FUSED>
 static hipError_t recon_wave_ipl(const ReconArgs& a, hipStream_t s) {
     const int ipl = g_tune.dec_ipl ? g_tune.dec_ipl : (a.k <= 4 ? 2 : 1);
     if (ipl == 2 && a.maxe <= 4 && a.cps >= 64) return recon_wave_dispatch<POL, FUSED, 2>(a, s);
+    if (ipl == 3 && a.cps >= 64) return recon_wave_dispatch<POL, FUSED, -2>(a, s);
     return recon_wave_dispatch<POL, FUSED, 1>(a, s);
 }
 

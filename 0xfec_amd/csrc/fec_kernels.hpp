@@ -124,7 +124,8 @@ struct Tuning {
     int dec_fused = 0;        // ... with the plans built inside the wave kernel (measured 11 % slower: off)
     int enc_diag = 0;         // diagnostics only: queue kernel without the field arithmetic (wrong output)
     int dec_diag = 0;         // diagnostics only: wave reconstruct with one shared plan (wrong output)
-    int dec_ipl = 0;          // wave-form reconstruct: items per lane (1, 2; 0: 2 for k <= 4, else 1)
+    int dec_ipl = 0;          // wave-form reconstruct items per lane: 1; 2 loaded together; 3: 2 one
+                              // after the other (one plan stage); 0: 2 for k <= 4, else 1
 };
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):

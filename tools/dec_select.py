@@ -32,9 +32,11 @@ def main():
                 "wave ipl2 swz, 1 slot": (dict(D, dec_ipl=2, dec_swz=1), 1)}
     for w in (4, 5, 6):
         variants["wave swz wpc%d, 1 slot" % w] = (dict(D, dec_swz=1, dec_wpc=w), 1)
+    for w in (0, 4, 5):
+        variants["wave swz seq2 wpc%d, 1 slot" % w] = (dict(D, dec_ipl=3, dec_wpc=w), 1)
     # diagnostics (wrong output): every wave stages block 0's plan, an L2-resident load
     variants["DIAG shared plan"] = (dict(D, dec_diag=1), 1)
-    variants["DIAG shared plan, no swz"] = (dict(D, dec_diag=1, dec_swz=0), 1)
+    variants["DIAG shared plan wpc4"] = (dict(D, dec_diag=1, dec_wpc=4), 1)
     base = codec.set_tuning(**D)
 
     def run(slots=1):
