@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
 #include <map>
 #include <utility>
 #include <vector>
@@ -26,7 +27,37 @@ struct Code {
     std::vector<uint8_t> matrix;   // n x k
     uint8_t* d_prows = nullptr;    // m x k
     uint32_t* d_tabs = nullptr;    // m x k PermTabs
+    uint32_t* d_dytabs = nullptr;  // dyadic codes: leaf PermTabs of the split-recursive encode
 };
+
+// Parity row r, column j of a dyadic code is g(r ^ j), g = parity row 0 (fec_kernels.hip,
+// "dyadic encode"); k and m powers of two, m <= k. Returns the leaf constants of the recursion
+// conv(C, D) = (P ^ Q, R ^ P ^ Q) for each group h of m columns, in the kernel's order (P's
+// leaves, Q's, R's), or nothing when the matrix is not dyadic.
+std::vector<uint8_t> dyadic_leaves(const std::vector<uint8_t>& matrix, int k, int m) {
+    auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
+    if (!pow2(k) || !pow2(m) || m > k) return {};
+    const uint8_t* g = matrix.data() + (size_t)k * k;
+    for (int r = 1; r < m; ++r)
+        for (int j = 0; j < k; ++j)
+            if (g[(size_t)r * k + j] != g[r ^ j]) return {};
+    std::vector<uint8_t> out;
+    std::function<void(const std::vector<uint8_t>&)> leaves = [&](const std::vector<uint8_t>& c) {
+        if (c.size() == 1) {
+            out.push_back(c[0]);
+            return;
+        }
+        const size_t h = c.size() / 2;
+        std::vector<uint8_t> lo(c.begin(), c.begin() + h), hi(c.begin() + h, c.end()), sum(h);
+        for (size_t i = 0; i < h; ++i) sum[i] = (uint8_t)(lo[i] ^ hi[i]);
+        leaves(lo);
+        leaves(hi);
+        leaves(sum);
+    };
+    for (int h = 0; h < k / m; ++h) leaves(std::vector<uint8_t>(g + (size_t)h * m, g + (size_t)(h + 1) * m));
+    return out;
+}
+
 
 // Bytes of staged shards per FEC_HOST chunk (x2 buffers, in and out).
 constexpr size_t kStageBytes = size_t(128) << 20;
@@ -97,6 +128,16 @@ static int get_code(fec_ctx* ctx, int k, int m, Code** out) {
         HIP_TRY(hipMalloc(&c.d_tabs, tabs.size() * 4));
         HIP_TRY(hipMemcpy(c.d_prows, c.matrix.data() + (size_t)k * k, (size_t)m * k, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(c.d_tabs, tabs.data(), tabs.size() * 4, hipMemcpyHostToDevice));
+        const std::vector<uint8_t> leaves = dyadic_leaves(c.matrix, k, m);
+        if (!leaves.empty() && leaves.size() <= (size_t)m * k) {   // staged like m x k tables
+            std::vector<uint32_t> dy((size_t)m * k * 8, 0);
+            for (size_t i = 0; i < leaves.size(); ++i) {
+                gf::PermTab t = gf::make_permtab(leaves[i]);
+                memcpy(&dy[i * 8], &t, sizeof(t));
+            }
+            HIP_TRY(hipMalloc(&c.d_dytabs, dy.size() * 4));
+            HIP_TRY(hipMemcpy(c.d_dytabs, dy.data(), dy.size() * 4, hipMemcpyHostToDevice));
+        }
     }
     auto res = ctx->codes.emplace(key, std::move(c));
     *out = &res.first->second;
@@ -190,6 +231,7 @@ static int rs_encode_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks
             a.swz = (uint32_t)fk::g_tune.xcd_swz;
             if (fk::fixed_encode_applies((uint32_t)k, (uint32_t)mr)) {
                 a.ctr = ctx->d_ctr;
+                a.dytabs = (r0 == 0 && mr == code->m) ? code->d_dytabs : nullptr;
                 HIP_TRY(fk::launch_rs_encode_fixed(a, ctx->ncu, ctx->stream));
                 continue;
             }
@@ -486,6 +528,7 @@ void fec_ctx_destroy(fec_ctx* ctx) {
     for (auto& kv : ctx->codes) {
         if (kv.second.d_prows) (void)hipFree(kv.second.d_prows);
         if (kv.second.d_tabs) (void)hipFree(kv.second.d_tabs);
+        if (kv.second.d_dytabs) (void)hipFree(kv.second.d_dytabs);
     }
     if (ctx->d_plans) (void)hipFree(ctx->d_plans);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
@@ -522,7 +565,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 14 ? &fk::g_tune.enc_queue : key == 15 ? &fk::g_tune.enc_qwpc
               : key == 16 ? &fk::g_tune.enc_qdepth : key == 17 ? &fk::g_tune.dec_wave
               : key == 18 ? &fk::g_tune.enc_diag : key == 19 ? &fk::g_tune.dec_fused
-              : key == 20 ? &fk::g_tune.dec_ipl : key == 21 ? &fk::g_tune.dec_diag : nullptr;
+              : key == 20 ? &fk::g_tune.dec_ipl : key == 21 ? &fk::g_tune.dec_diag
+              : key == 22 ? &fk::g_tune.enc_dyadic : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

@@ -261,6 +261,70 @@ __global__ __launch_bounds__(kThreads) void rs_encode_kernel(EncodeArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ dyadic encode
+// For k = 2^a and m = 2^b (m <= k) klauspost's systematic matrix is dyadic: parity row i,
+// column j holds g(i ^ j) with g = parity row 0. (Its rows are the Lagrange basis on the
+// additive subgroup {0..k-1} of GF(2^8) evaluated at k ^ i; the subgroup's vanishing polynomial
+// is GF(2)-linear, so L_j(k ^ i) = W(k) / (K (k ^ i ^ j)) depends on i ^ j only.) With
+// j = h*m + v (v < m): parity_i = sum_h conv(G_h, D_h)[i], conv(C, D)[i] = sum_v C[v ^ i] D[v],
+// a convolution over the group Z_2^b. Split on the top index bit, with P = conv(C0, D0),
+// Q = conv(C1, D1), R = conv(C0 ^ C1, D0 ^ D1) over half the size:
+//   conv(C, D) = (P ^ Q, R ^ P ^ Q)
+// (field arithmetic is exact, so this is the same bytes as the matrix product). Recursing, a
+// group costs 3^b field products instead of 4^b: RS(8,12) 18 instead of 32, RS(16,24) 54
+// instead of 128. Products are linear in the data, so the split of D0 ^ D1 is the XOR of the
+// splits (3 ops, not 5). Leaf constants (C0 ^ C1 combinations) come from the host in the
+// recursion's order: P's leaves, Q's, R's (dyadic_leaf_tables()).
+template <int B>
+struct Pow3 {
+    static constexpr int v = 3 * Pow3<B - 1>::v;
+};
+template <>
+struct Pow3<0> {
+    static constexpr int v = 1;
+};
+
+template <int NC>
+__device__ __forceinline__ void dy_leaf(const Idx (&d)[NC], const gf::PermTab* t, uint32_t (&y)[NC]) {
+    const uint4 lo = *reinterpret_cast<const uint4*>(t);
+    const uint32_t t2 = t->t2;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const Prod3 p = gprod(d[c], lo, t2);
+        y[c] = xor3(p.p0, p.p1, p.p2);
+    }
+}
+
+// Y[i] = sum_l C[l ^ i] * D[l], i, l < 2^B, for NC dword columns; C by its leaf tables T.
+template <int B, int NC>
+__device__ __forceinline__ void dy_conv(const Idx (*D)[NC], const gf::PermTab* T, uint32_t (*Y)[NC]) {
+    if constexpr (B == 0) {
+        dy_leaf<NC>(D[0], T, Y[0]);
+    } else {
+        constexpr int H = 1 << (B - 1), L = Pow3<B - 1>::v;
+        uint32_t P[H][NC], R[H][NC];
+        dy_conv<B - 1, NC>(D, T, P);
+        dy_conv<B - 1, NC>(D + H, T + L, Y);   // Q, in the low half of Y
+        {
+            Idx S[H][NC];
+#pragma unroll
+            for (int i = 0; i < H; ++i)
+#pragma unroll
+                for (int c = 0; c < NC; ++c)
+                    S[i][c] = {D[i][c].a ^ D[i + H][c].a, D[i][c].b ^ D[i + H][c].b, D[i][c].c ^ D[i + H][c].c};
+            dy_conv<B - 1, NC>(S, T + 2 * L, R);
+        }
+#pragma unroll
+        for (int i = 0; i < H; ++i)
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const uint32_t q = Y[i][c];
+                Y[i][c] = P[i][c] ^ q;
+                Y[i + H][c] = xor3(R[i][c], P[i][c], q);
+            }
+    }
+}
+
 // ------------------------------------------------------------------ RS encode, fixed shape
 // The code shapes the reference benchmarks, with K and M compile-time: one lane = one 16-byte
 // column chunk, the K loads issued back to back, inputs folded in pairs (mac2), no runtime
@@ -293,6 +357,32 @@ struct FixedEncode {
             for (int j = 0; j < K; ++j)
 #pragma unroll
                 for (int d = 0; d < 4; ++d) acc[j % M][d] ^= word_of(x[j], d);
+        } else if constexpr ((POL & 8) != 0) {   // dyadic code: T holds the leaf tables
+            constexpr int B = M == 1 ? 0 : M == 2 ? 1 : M == 4 ? 2 : M == 8 ? 3 : 4;
+            constexpr int L = Pow3<B>::v;
+            constexpr int NC = K >= 16 ? 1 : 4;   // dword columns per pass (registers)
+#pragma unroll
+            for (int c0 = 0; c0 < 4; c0 += NC) {
+                // opaque zero per pass: the table reads stay in their pass (shared across
+                // passes they would be hoisted and held: 5 VGPRs per leaf)
+                uint32_t poff = 0;
+                asm volatile("" : "+s"(poff));
+                const gf::PermTab* tp = t + poff;
+#pragma unroll
+                for (int h = 0; h < K / M; ++h) {
+                    Idx D[M][NC];
+#pragma unroll
+                    for (int v = 0; v < M; ++v)
+#pragma unroll
+                        for (int c = 0; c < NC; ++c) D[v][c] = split(word_of(x[h * M + v], c0 + c));
+                    uint32_t Y[M][NC];
+                    dy_conv<B, NC>(D, tp + h * L, Y);
+#pragma unroll
+                    for (int i = 0; i < M; ++i)
+#pragma unroll
+                        for (int c = 0; c < NC; ++c) acc[i][c0 + c] = h ? acc[i][c0 + c] ^ Y[i][c] : Y[i][c];
+                }
+            }
         } else
 #pragma unroll
         for (int j = 0; j < K; j += 2) {
@@ -1084,6 +1174,13 @@ static hipError_t enc_fixed_dispatch(const EncodeArgs& a, int grid, size_t lds, 
             hipLaunchKernelGGL((rs_encode_queue_kernel<K, M, 3, (K <= 8 ? 2 : 1)>), dim3(grid), dim3(kThreads), lds, s, a);
         else
             hipLaunchKernelGGL((rs_encode_queue_kernel<K, M, 3, 1>), dim3(grid), dim3(kThreads), lds, s, a);
+    } else if (g_tune.enc_dyadic && a.dytabs && K >= 4) {
+        EncodeArgs d = a;
+        d.tabs = a.dytabs;
+        if (g_tune.enc_nt & 1)
+            hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 11>), dim3(grid), dim3(kThreads), lds, s, d);
+        else
+            hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 10>), dim3(grid), dim3(kThreads), lds, s, d);
     } else {
         if (g_tune.enc_nt & 1)
             hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 3>), dim3(grid), dim3(kThreads), lds, s, a);

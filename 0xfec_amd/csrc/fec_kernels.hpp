@@ -34,6 +34,8 @@ struct EncodeArgs {
     uint32_t* ctr;             // queue kernel: 8 ticket counters kCtrStride words apart, then the
                                // arrival counter; all zero at launch, rewound by the last workgroup
     uint32_t per_xcd;          // queue kernel: items per XCD range
+    const uint32_t* dytabs;    // dyadic codes (nullable): leaf PermTabs of the split-recursive
+                               // form, dyadic_leaf_tables(), padded to m * k entries
 };
 
 constexpr int kCtrStride = 32;      // one 128-byte line per ticket counter
@@ -123,6 +125,8 @@ struct Tuning {
     int dec_wave = 1;         // reconstruct: wave-private plan staging (shards of 32+ chunks)
     int dec_fused = 0;        // ... with the plans built inside the wave kernel (measured 11 % slower: off)
     int enc_diag = 0;         // diagnostics only: queue kernel without the field arithmetic (wrong output)
+    int enc_dyadic = 1;       // fixed-shape encode of dyadic codes (RS(8,12), RS(16,24)) by the
+                              // split-recursive product (fewer field multiplications)
     int dec_diag = 0;         // diagnostics only: wave reconstruct with one shared plan (wrong output)
     int dec_ipl = 0;          // wave-form reconstruct items per lane: 1; 2 loaded together; 3: 2 one
                               // after the other (one plan stage); 0: 2 for k <= 4, else 1

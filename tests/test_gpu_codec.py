@@ -291,7 +291,8 @@ def test_rs_recover_out_of_place(codec, oracle, torch, fec, k, m, slots):
 # ranges empty, partial and ragged (B * ceil(L/16) items vs 8 ranges of 256-item chunks).
 ENC_VARIANTS = {
     "generic": dict(enc_fixed=0),
-    "fixed_flat": dict(enc_fixed=1, enc_queue=0, enc_wpc=3),
+    "fixed_flat": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=1),
+    "fixed_flat_matrix": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=0),
     "queue_d0": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=0),
     "queue_d0_nodrain": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=-1),
     "queue_d1": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=1),

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Diagnostics: pick the RS(8,12) encode launch form by interleaved A/B in one process
-(flat fixed-shape grid at several residencies vs the ticket-queue kernel), many rounds."""
+"""Diagnostics: pick the fixed-shape encode form by interleaved A/B in one process (matrix vs
+dyadic split-recursive body, flat grid at several residencies, ticket queue), many rounds.
+usage: enc_select.py [k,m]   (8,4 default; 2^23 / k blocks)"""
 import importlib
 import json
 import os
@@ -12,19 +13,31 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     import torch
     fec = importlib.import_module("0xfec_amd")
-    B, k, m, L, S = 1 << 20, 8, 4, 1202, 1216
+    k, m = (int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "8,4").split(","))
+    B, L, S = (1 << 23) // k, 1202, 1216
     codec = fec.Codec(0).use_torch_stream()
     data = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device="cuda")
     par = torch.zeros((B, m, S), dtype=torch.uint8, device="cuda")
     dp, pp = data.data_ptr(), par.data_ptr()
-    variants = {
-        "flat wpc0": dict(enc_queue=0, enc_wpc=0), "flat wpc3": dict(enc_queue=0, enc_wpc=3),
-        "flat wpc4": dict(enc_queue=0, enc_wpc=4), "flat wpc5": dict(enc_queue=0, enc_wpc=5),
-        "queue d0 wpc2": dict(enc_queue=1, enc_qwpc=2, enc_qdepth=0),
-        "queue d0 wpc3": dict(enc_queue=1, enc_qwpc=3, enc_qdepth=0),
-        "queue d1 wpc2": dict(enc_queue=1, enc_qwpc=2, enc_qdepth=1),
-    }
-    base = codec.set_tuning(enc_queue=1, enc_wpc=3, enc_qwpc=2, enc_qdepth=0)
+    variants = {}
+    for w in (3, 4, 5):
+        variants["matrix flat wpc%d" % w] = dict(enc_queue=0, enc_wpc=w, enc_dyadic=0)
+    for w in (0, 3, 4, 5):
+        variants["dyadic flat wpc%d" % w] = dict(enc_queue=0, enc_wpc=w, enc_dyadic=1)
+    if k == 8:
+        variants["matrix queue d0 wpc2"] = dict(enc_queue=1, enc_qwpc=2, enc_qdepth=0, enc_dyadic=0)
+    base = codec.set_tuning(enc_queue=0, enc_wpc=4, enc_qwpc=2, enc_qdepth=0, enc_dyadic=1)
+    ref = None
+    for n, kv in variants.items():   # every form writes the same parity bytes
+        codec.set_tuning(**kv)
+        par.zero_()
+        codec.rs_encode_raw(k, m, L, B, dp, k * S, pp, m * S, S, fec.FEC_DEVICE)
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = par.clone()
+        assert torch.equal(par, ref), n
+        codec.set_tuning(**base)
+    del ref
 
     def t(iters=5):
         codec.rs_encode_raw(k, m, L, B, dp, k * S, pp, m * S, S, fec.FEC_DEVICE)
