@@ -1194,7 +1194,7 @@ hipError_t launch_rs_encode_fixed(EncodeArgs a, int ncu, hipStream_t s) {
     const uint32_t chunks = (a.total + kThreads - 1) / kThreads;
     if (chunks == 0) return hipSuccess;
     // Per shape (measured): RS(8,12) and RS(16,24) run the flat grid at
-    // g_tune.enc_wpc (4) workgroups per CU; RS(2,3) (2 loads per lane: little in flight per
+    // g_tune.enc_wpc (3) workgroups per CU; RS(2,3) (2 loads per lane: little in flight per
     // wave) at full residency. The ticket-queue form stays selectable (enc_queue).
     const bool queue = g_tune.enc_queue && a.ctr != nullptr && a.k == 8;
     int grid = (int)chunks;

@@ -115,7 +115,7 @@ struct Tuning {
     int rotate = 0;           // rotate chunk order so shard boundaries share a wave (measured: no gain)
     int xcd_swz = 1;          // encode / XOR: workgroups of one XCD take one contiguous range of the grid
     int dec_swz = 1;          // same for reconstruct
-    int enc_wpc = 4;          // resident workgroups per CU, fixed-shape encode (0: as many as fit)
+    int enc_wpc = 3;          // resident workgroups per CU, fixed-shape encode (0: as many as fit)
     int gen_wpc = 0;          // same for the generic encode and XOR encode
     int dec_wpc = 0;          // same for reconstruct
     int enc_fixed = 1;        // compile-time-shape encode for RS(2,3), RS(8,12), RS(16,24)
