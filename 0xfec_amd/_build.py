@@ -1,14 +1,29 @@
-"""Build lib0xfec_hip.so in-tree with hipcc for gfx950 (no JIT cache, no torch extension)."""
+"""Build lib0xfec_hip.so in-tree with hipcc for gfx950 (no JIT cache, no torch extension).
+
+Every source is compiled to its own object in parallel (the kernel translation units carry
+many template instances and dominate the build), then linked into one shared library. An
+object is rebuilt when its source or any shared header is newer than it.
+"""
 import os
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(HERE, "_obj")
+INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 LIB = os.path.join(HERE, "lib0xfec_hip.so")
 
-SOURCES = ["fec_kernels.hip", "fec_capi.cpp", "fec_scheme.cpp", "fec_batch.cpp", "fec_wire.cpp"]
-HEADERS = ["fec_kernels.hpp", "gf256.h", "rs_matrix.hpp"]
-PUBLIC = ["fec_hip.h", "fec_scheme.h", "fec_batch.h", "fec_batch.hpp", "fec_scheme.hpp", "fec_wire.h"]
+SOURCES = ["fec_encode.hip", "fec_decode.hip", "fec_xor.hip", "fec_kernels.hip", "fec_capi.cpp",
+           "fec_scheme.cpp", "fec_batch.cpp", "fec_wire.cpp", "fec_go.cpp"]
+HEADERS = ["fec_kernels.hpp", "fec_device.hpp", "gf256.h", "rs_matrix.hpp"]
+PUBLIC = ["fec_hip.h", "fec_scheme.h", "fec_batch.h", "fec_batch.hpp", "fec_scheme.hpp", "fec_wire.h", "fec_go.h"]
+
+# The atomic optimizer turns a single-lane atomicAdd (queue kernels' ticket draw) into a
+# wave-aggregated one whose result is consumed on the spot, which makes the draw a full HBM
+# round trip on the critical path; the tickets are consumed a stage later instead.
+CFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall",
+          "-mllvm", "-amdgpu-atomic-optimizer-strategy=None", "-I", INCLUDE]
 
 
 def _hipcc():
@@ -18,34 +33,59 @@ def _hipcc():
     return "hipcc"
 
 
-def _inputs():
-    inc = os.path.join(os.path.dirname(HERE), "include")
-    files = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(inc, h) for h in PUBLIC]
+def _sources():
+    return [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+
+
+def _headers():
+    files = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, h) for h in PUBLIC]
     return [f for f in files if os.path.exists(f)]
 
 
+def _obj(src):
+    return os.path.join(OBJ, src.rsplit(".", 1)[0] + ".o")
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
 def up_to_date():
-    if not os.path.exists(LIB):
+    hdrs = _headers()
+    srcs = _sources()
+    if any(_stale(_obj(s), [os.path.join(CSRC, s)] + hdrs) for s in srcs):
         return False
-    t = os.path.getmtime(LIB)
-    return all(os.path.getmtime(f) <= t for f in _inputs())
+    return not _stale(LIB, [_obj(s) for s in srcs])
 
 
-def build(force=False, verbose=False):
-    """Compile every HIP/C++ source of the codec into lib0xfec_hip.so (gfx950 only)."""
-    if not force and up_to_date():
-        return LIB
-    srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
-    # The atomic optimizer turns a single-lane atomicAdd (queue kernels' ticket draw) into a
-    # wave-aggregated one whose result is consumed on the spot, which makes the draw a full HBM
-    # round trip on the critical path; the tickets are consumed a stage later instead.
-    cmd = [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
-           "-I", os.path.join(os.path.dirname(HERE), "include"), "-o", LIB + ".tmp"] + srcs
+def _run(cmd, verbose):
     if verbose:
-        print(" ".join(cmd))
+        print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(LIB + ".tmp", LIB)
+
+
+def build(force=False, verbose=False, jobs=None):
+    """Compile every HIP/C++ source of the codec and link lib0xfec_hip.so (gfx950 only)."""
+    os.makedirs(OBJ, exist_ok=True)
+    hdrs = _headers()
+    srcs = _sources()
+    todo = [s for s in srcs if force or _stale(_obj(s), [os.path.join(CSRC, s)] + hdrs)]
+    # heaviest translation units first, so they start before the quick host sources
+    todo.sort(key=lambda s: not s.endswith(".hip"))
+    hipcc = _hipcc()
+    cmds = [[hipcc] + CFLAGS + ["-c", "-o", _obj(s), os.path.join(CSRC, s)] for s in todo]
+    if cmds:
+        jobs = jobs or min(len(cmds), max(1, (os.cpu_count() or 2)))
+        with ThreadPoolExecutor(max_workers=jobs) as ex:
+            for f in [ex.submit(_run, c, verbose) for c in cmds]:
+                f.result()
+    if force or todo or _stale(LIB, [_obj(s) for s in srcs]):
+        _run([hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB + ".tmp"] + [_obj(s) for s in srcs],
+             verbose)
+        os.replace(LIB + ".tmp", LIB)
     return LIB
 
 

@@ -105,8 +105,8 @@ struct XorArgs {
 // Kernel-selection knobs. Defaults are the measured best (tools/kbench.py A/Bs them through
 // the internal fec__set_tuning() entry point; results in DESIGN.md).
 struct Tuning {
-    int enc_nt = 3;           // encode/XOR cache policy: bit 0 non-temporal loads, bit 1 nt stores
-    int dec_nt = 3;           // reconstruct cache policy, same bits
+    int enc_nt = 3;           // encode/XOR cache policy: 0 plain, nonzero non-temporal loads and stores
+    int dec_nt = 3;           // reconstruct cache policy, same values
     int grid_mult = 1;        // persistent grids: workgroups = grid_mult * CUs * resident/CU
     int dec_max_rounds = 8;   // bound on item rounds per decode tile (pick_tile_blocks)
     int pad_zero = 1;         // tail chunks: zero-padded full 16-B stores instead of partial
@@ -167,5 +167,9 @@ uint32_t pick_tile_blocks(uint32_t cps, uint32_t k, uint32_t maxe, const PlanLay
 size_t recon_lds_bytes(uint32_t g, uint32_t k, uint32_t maxe, const PlanLayout& lay);
 // Resident workgroups on the device for kernel `which` (0 encode, 1 reconstruct, 2 XOR).
 int occupancy_grid(int device, int which, uint32_t m_or_maxe, size_t lds_bytes);
+// Host stubs of the kernels occupancy_grid() sizes against (one per translation unit).
+const void* encode_occupancy_kernel(uint32_t m);
+const void* recon_occupancy_kernel(uint32_t maxe);
+const void* xor_occupancy_kernel();
 
 }  // namespace fk
