@@ -68,6 +68,9 @@ lib.fec_rs_reconstruct_batch.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _
 lib.fec_rs_recover_batch.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _vp, _vp, _sz, _i, _vp, _i]
 lib.fec_xor_encode_batch.argtypes = [_vp, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _i]
 lib.fec_xor_reconstruct_batch.argtypes = [_vp, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _vp, _vp, _i]
+_u64 = ctypes.c_uint64
+lib.fec_synth_data.argtypes = [_vp, _u64, _u64, _sz, _i, _sz, _vp, _sz, _sz]
+lib.fec_synth_single_erasures.argtypes = [_vp, _u64, _u64, _sz, _i, _i, _vp, _vp]
 
 
 class FecError(RuntimeError):
@@ -169,6 +172,10 @@ class Codec:
     def sync(self):
         return _check(lib.fec_sync(self._h), "fec_sync")
 
+    def lib_sync_rc(self):
+        """fec_sync's return code (FEC_ERR_TOO_FEW_SHARDS after a failed block) without raising."""
+        return lib.fec_sync(self._h)
+
     # Kernel-selection knobs (diagnostics and tests; defaults are the measured best). Keys of
     # the library's internal fec__set_tuning(); the setting is process-wide.
     TUNING_KEYS = {"enc_nt": 0, "dec_nt": 1, "grid_mult": 2, "dec_max_rounds": 3, "pad_zero": 4,
@@ -264,6 +271,17 @@ class Codec:
         rc = self.rs_recover_raw(k, m, L, B, _addr(data)[0], k * S, _addr(parity)[0], m * S, S, _addr(masks)[0],
                                  _addr(out)[0], slots * S, slots, sa)
         return _check(rc, "fec_rs_recover_batch")
+
+    # ---- synthetic workload on the device (include/fec_synth.h; same bytes as shard.py)
+    def synth_data(self, seed, first_block, nblocks, k, payload_len, data, block_stride, shard_stride):
+        """Fill data shards of global blocks [first_block, first_block + nblocks) at the device
+        address `data` (asynchronous on the ctx stream)."""
+        return _check(lib.fec_synth_data(self._h, seed, first_block, nblocks, k, payload_len, data, block_stride,
+                                         shard_stride), "fec_synth_data")
+
+    def synth_single_erasures(self, seed, first_block, nblocks, k, m, masks, erased=None):
+        return _check(lib.fec_synth_single_erasures(self._h, seed, first_block, nblocks, k, m, masks, erased),
+                      "fec_synth_single_erasures")
 
     def xor_encode(self, k, shards, shard_len=None):
         B, n, S = _shape3(shards)

@@ -41,6 +41,8 @@ lib.fec_batch_encoder_staged.restype = _sz
 lib.fec_batch_encoder_staged.argtypes = [_vp]
 lib.fec_batch_encoder_in_flight.restype = _sz
 lib.fec_batch_encoder_in_flight.argtypes = [_vp]
+lib.fec_batch_encoder_backlog.restype = _sz
+lib.fec_batch_encoder_backlog.argtypes = [_vp]
 lib.fec_manager_add_source_symbol_frame_batched.argtypes = [_vp, _u64, ctypes.c_char_p, _sz, _sz, _vp, _vp]
 lib.fec_recovered_queue_new.restype = _vp
 lib.fec_recovered_queue_new.argtypes = []
@@ -160,6 +162,10 @@ class BatchEncoder:
     @property
     def in_flight(self):
         return lib.fec_batch_encoder_in_flight(self._h)
+
+    @property
+    def backlog(self):
+        return lib.fec_batch_encoder_backlog(self._h)
 
 
 def add_source_symbol_frame_batched(manager, ssid, payload, encoder, queue, cap=MAX_PACKET_BUFFER_SIZE):

@@ -50,6 +50,9 @@ size_t RepairQueue::Len() {
 
 namespace {
 constexpr size_t kSlotMax = (kMaxFECPacketBufferSize + kRepairPayloadMetadataLen + 15) & ~size_t(15);   // 1440
+// Receive side: a repair payload may be as long as a packet buffer (XOR recovery accepts up to
+// MaxPacketBufferSize, xor.go:76-86), so decoder slots hold 1452 bytes.
+constexpr size_t kDecSlotMax = (kMaxPacketBufferSize + 15) & ~size_t(15);   // 1456
 size_t round16(size_t x) { return (x + 15) & ~size_t(15); }
 Error hip_error(hipError_t e, const char* what) {
     (void)hipGetLastError();
@@ -121,25 +124,14 @@ Error BatchEncoder::Submit(Block& b, RepairQueue* q) {
                       : xor_->stageRepairInput(b, scratch.data(), kSlotMax, &L, &count);
         if (!e.ok()) return e;
         if (xor_ && count != k_) return Error::text("block does not match the encoder's source symbol count");
-        e = init();
-        if (!e.ok()) return e;
     }
-    Set* s = &sets_[cur_];
-    if (s->inFlight) {   // a retired batch whose frames did not fit their queue yet
-        Error e = waitSet(*s);
-        if (e.ok()) e = deliver(*s, nullptr);
-        if (!e.ok()) return e;
-    }
-    if (!s->blocks.empty() && (s->blocks.size() >= maxBlocks_ || std::max<size_t>(want, 16) > s->slot)) {
-        Error e = flushImpl(nullptr);
-        if (!e.ok()) return e;
-        s = &sets_[cur_];
-    }
-    if (s->blocks.empty()) s->slot = std::min(kSlotMax, std::max<size_t>(want, 16));
+    Set* s = nullptr;
+    Error e = slotFor(want, &s);
+    if (!e.ok()) return e;
     uint8_t* dst = s->h_in + s->blocks.size() * (size_t)k_ * s->slot;
     size_t L = 0;
     int count = 0;
-    Error e = rs_ ? rs_->stageRepairInput(b, dst, s->slot, &L) : xor_->stageRepairInput(b, dst, s->slot, &L, &count);
+    e = rs_ ? rs_->stageRepairInput(b, dst, s->slot, &L) : xor_->stageRepairInput(b, dst, s->slot, &L, &count);
     if (!e.ok()) return e;
     if (xor_ && count != k_) return Error::text("block does not match the encoder's source symbol count");
     s->blocks.push_back(Pending{q, b.id, L});
@@ -148,6 +140,7 @@ Error BatchEncoder::Submit(Block& b, RepairQueue* q) {
 }
 
 // The staging set to write the next block into, with slot >= want (flushes when needed).
+// Only device failures fail here: queue backpressure leaves frames in the backlog.
 Error BatchEncoder::slotFor(size_t want, Set** out) {
     if (!ready_) {
         Error e = init();
@@ -155,8 +148,7 @@ Error BatchEncoder::slotFor(size_t want, Set** out) {
     }
     Set* s = &sets_[cur_];
     if (s->inFlight) {
-        Error e = waitSet(*s);
-        if (e.ok()) e = deliver(*s, nullptr);
+        Error e = retire(*s);
         if (!e.ok()) return e;
     }
     if (!s->blocks.empty() && (s->blocks.size() >= maxBlocks_ || std::max<size_t>(want, 16) > s->slot)) {
@@ -202,9 +194,8 @@ Error BatchEncoder::Flush() { return flushImpl(nullptr); }
 
 Error BatchEncoder::flushImpl(size_t* delivered) {
     Set& s = sets_[cur_];
-    if (s.inFlight) {   // undelivered frames of a retired batch still hold this set
-        Error e = waitSet(s);
-        if (e.ok()) e = deliver(s, delivered);
+    if (s.inFlight) {
+        Error e = retire(s);
         if (!e.ok()) return e;
     }
     if (s.blocks.empty()) return Error::nil();
@@ -227,14 +218,13 @@ Error BatchEncoder::flushImpl(size_t* delivered) {
         return hip_error(h, "hipMemcpyAsync D2H");
     if ((h = hipEventRecord((hipEvent_t)s.done, st)) != hipSuccess) return hip_error(h, "hipEventRecord");
     s.inFlight = true;
-    s.delivered = 0;
     cur_ ^= 1;
     // the other set becomes the staging set: retire it if its batch is still out
     Set& next = sets_[cur_];
     if (next.inFlight) {
-        if ((e = waitSet(next)).ok()) e = deliver(next, delivered);
-        if (!e.ok()) return e;
+        if (!(e = retire(next)).ok()) return e;
     }
+    pump(delivered);   // a full queue is not a failure of this flush
     return Error::nil();
 }
 
@@ -243,26 +233,48 @@ Error BatchEncoder::waitSet(Set& s) {
     return h == hipSuccess ? Error::nil() : hip_error(h, "hipEventSynchronize");
 }
 
-Error BatchEncoder::deliver(Set& s, size_t* blocks) {
-    const size_t B = s.blocks.size();
-    for (; s.delivered < B; ++s.delivered) {
-        const Pending& p = s.blocks[s.delivered];
-        if (p.q->Len() + (size_t)m_ > p.q->MaxLen()) return Error::text("repair queue full");
-        for (int i = 0; i < m_; ++i) {
+Error BatchEncoder::retire(Set& s) {
+    Error e = waitSet(s);
+    if (!e.ok()) return e;
+    for (size_t i = 0; i < s.blocks.size(); ++i) {
+        const Pending& p = s.blocks[i];
+        Ready r{p.q, p.id, {}};
+        r.payloads.reserve((size_t)m_);
+        for (int j = 0; j < m_; ++j) {
             // repairSymbols makes RS payloads as make([]byte, 0, MaxPacketBufferSize)[:L']
             // (reed_solomon.go:44-49) and the XOR payload as make([]byte, L) (xor.go:28-33)
             Slice pl = rs_ ? Slice::make(0, kMaxPacketBufferSize).reslice(0, p.len) : Slice::make(p.len, p.len);
-            memcpy(pl.data(), s.h_out + (s.delivered * (size_t)m_ + i) * s.slot, p.len);
-            Error e = p.q->Add(RepairFrame{p.id, (ParityID)i, pl});
-            if (!e.ok()) return e;
+            memcpy(pl.data(), s.h_out + (i * (size_t)m_ + j) * s.slot, p.len);
+            r.payloads.push_back(pl);
         }
-        if (blocks) ++*blocks;
+        backlog_.push_back(std::move(r));
     }
     s.blocks.clear();
     s.maxLen = 0;
-    s.delivered = 0;
     s.inFlight = false;
     return Error::nil();
+}
+
+bool BatchEncoder::pump(size_t* blocks) {
+    std::vector<RepairQueue*> held;   // queues whose next block did not fit: keep their order
+    for (auto it = backlog_.begin(); it != backlog_.end();) {
+        if (std::find(held.begin(), held.end(), it->q) != held.end()) {
+            ++it;
+            continue;
+        }
+        if (it->q->Len() + it->payloads.size() > it->q->MaxLen()) {
+            held.push_back(it->q);
+            ++it;
+            continue;
+        }
+        bool ok = true;
+        for (size_t j = 0; j < it->payloads.size(); ++j)
+            if (!it->q->Add(RepairFrame{it->id, (ParityID)j, it->payloads[j]}).ok()) ok = false;   // closed queue
+        (void)ok;   // a closed queue drops its frames, as the reference's connection would
+        if (blocks) ++*blocks;
+        it = backlog_.erase(it);
+    }
+    return backlog_.empty();
 }
 
 Error BatchEncoder::Poll(size_t* blocks) {
@@ -274,35 +286,35 @@ Error BatchEncoder::Poll(size_t* blocks) {
         const hipError_t h = hipEventQuery((hipEvent_t)s.done);
         if (h == hipErrorNotReady) break;   // later batches complete later (one stream)
         if (h != hipSuccess) return hip_error(h, "hipEventQuery");
-        Error e = deliver(s, blocks);
+        Error e = retire(s);
         if (!e.ok()) return e;
     }
-    return Error::nil();
+    return pump(blocks) ? Error::nil() : Error::text("repair queue full");
 }
 
 Error BatchEncoder::Drain(size_t* blocks) {
-    size_t before = 0;
-    Error e = flushImpl(&before);   // may retire (and deliver) the older batch
     if (blocks) *blocks = 0;
+    size_t n = 0;
+    Error e = flushImpl(&n);
     if (!e.ok()) return e;
     for (int i = 1; i >= 0; --i) {
         Set& s = sets_[cur_ ^ i];
         if (!s.inFlight) continue;
-        if (!(e = waitSet(s)).ok()) return e;
-        size_t n = 0;
-        if (!(e = deliver(s, &n)).ok()) return e;
-        before += n;
+        if (!(e = retire(s)).ok()) return e;
     }
-    if (blocks) *blocks = before;
-    return Error::nil();
+    const bool empty = pump(&n);
+    if (blocks) *blocks = n;
+    return empty ? Error::nil() : Error::text("repair queue full");
 }
 
 size_t BatchEncoder::Staged() const { return sets_[cur_].blocks.size(); }
 
 size_t BatchEncoder::InFlight() const {
     const Set& o = sets_[cur_ ^ 1];
-    return o.inFlight ? o.blocks.size() - o.delivered : 0;
+    return o.inFlight ? o.blocks.size() : 0;
 }
+
+size_t BatchEncoder::Backlog() const { return backlog_.size(); }
 
 }  // namespace fec
 
@@ -366,7 +378,7 @@ Error BatchDecoder::init() {
     Error e = engine_->ctx(&ctx);
     if (!e.ok()) return e;
     const size_t n = (size_t)k_ + m_;
-    const size_t in_bytes = maxBlocks_ * n * kSlotMax, out_bytes = maxBlocks_ * (size_t)m_ * kSlotMax;
+    const size_t in_bytes = maxBlocks_ * n * kDecSlotMax, out_bytes = maxBlocks_ * (size_t)m_ * kDecSlotMax;
     for (Set& s : sets_) {
         hipError_t h;
         if ((h = hipHostMalloc(&s.h_in, in_bytes, hipHostMallocDefault)) != hipSuccess ||
@@ -414,13 +426,13 @@ Error BatchDecoder::Submit(Block& b, RecoveredQueue* q, bool* staged) {
     if (!q) return Error::text("nil recovered queue");
     size_t want = kRepairPayloadMetadataLen + (size_t)std::max(0, b.biggestSourceSymbolLenSoFar);
     for (auto& kv : b.pidToRepairPayload) want = std::max(want, kv.second.len);
-    want = std::min(kSlotMax, std::max<size_t>(16, round16(want)));
+    want = std::min(kDecSlotMax, std::max<size_t>(16, round16(want)));
     const size_t n = (size_t)k_ + m_;
     bool nothing = false;
     Pending p;
     if (!ready_) {   // validate before any device work
-        std::vector<uint8_t> scratch(n * kSlotMax);
-        Error e = stage(b, scratch.data(), kSlotMax, &p, &nothing);
+        std::vector<uint8_t> scratch(n * kDecSlotMax);
+        Error e = stage(b, scratch.data(), kDecSlotMax, &p, &nothing);
         if (!e.ok() || nothing) return e;
         if (!(e = init()).ok()) return e;
     }

@@ -408,8 +408,8 @@ static int host_reconstruct(fec_ctx* ctx, Code* code, int k, int m, size_t len, 
                             int32_t* block_status) {
     const size_t ssd = round16(len);
     const size_t n = (size_t)k + m;
-    const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
-    const uint32_t kmask = (1u << k) - 1u;
+    const uint32_t all = fk::low_mask((uint32_t)n);
+    const uint32_t kmask = fk::low_mask((uint32_t)k);
     const size_t chunk = host_chunk_blocks(n, ssd);
     int rc;
     if ((rc = grow_stage(ctx, std::min(chunk, nblocks) * n * ssd))) return rc;

@@ -46,9 +46,9 @@ __global__ __launch_bounds__(kPlanThreads) void rs_plan_kernel(PlanArgs a) {
     uint8_t* P = recs + threadIdx.x * lay.stride;
     const uint32_t k = a.k, m = a.m, n = k + m;
     if (b < a.nblocks) {
-        const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
+        const uint32_t all = low_mask(n);
         const uint32_t mask = a.masks[b] & all;
-        const uint32_t kmask = (1u << k) - 1u;   // k <= 31
+        const uint32_t kmask = low_mask(k);   // k = 32 when m = 0
         const uint32_t e = k - __popc(mask & kmask);
         int32_t st = a.max_out ? (int32_t)e : 0;   // recover reports the rebuilt count
         if (e == 0) {
@@ -64,7 +64,7 @@ __global__ __launch_bounds__(kPlanThreads) void rs_plan_kernel(PlanArgs a) {
         } else if (e == 1) {
             // one erasure: x_E = inv(A[R0][E0]) * (p_R0 ^ sum_j A[R0][j] x_j)
             const uint32_t E0 = __ffs(~mask & kmask) - 1;
-            const uint32_t R0 = __ffs(mask >> k) - 1;
+            const uint32_t R0 = __ffs(k < 32 ? mask >> k : 0u) - 1;
             const uint8_t* row = s_prows + R0 * k;
             const uint32_t inv = s_exp[255 - s_log[row[E0]]];
             for (uint32_t j = 0, pos = 0; j < k; ++j) {
@@ -392,8 +392,8 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
         uint8_t* Dt = plans + (size_t)kWaveBlocks * lay.stride;   // k bytes
         uint8_t* Nt = Dt + k;                                       // maxe bytes
         const uint32_t m = a.m, n = k + m;
-        const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
-        const uint32_t kmask = (1u << k) - 1u;
+        const uint32_t all = low_mask(n);
+        const uint32_t kmask = low_mask(k);
         auto mul = [&](uint32_t x, uint32_t y) -> uint32_t { return (x && y) ? s_exp[s_log[x] + s_log[y]] : 0u; };
         // the wave's (<= 3) masks in one load, then broadcast
         const uint32_t mine = lane < nb ? a.masks[bfirst + lane] : 0u;
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
                 uint8_t* C = P + lay.coef_off;
                 if (e == 1) {
                     const uint32_t E0 = __ffs(~mask & kmask) - 1;
-                    const uint32_t R0 = __ffs(mask >> k) - 1;
+                    const uint32_t R0 = __ffs(k < 32 ? mask >> k : 0u) - 1;
                     const uint8_t* row = s_prows + R0 * k;
                     const uint32_t inv = s_exp[255 - s_log[row[E0]]];
                     if (lane < k) {

@@ -38,6 +38,9 @@ struct EncodeArgs {
                                // form, dyadic_leaf_tables(), padded to m * k entries
 };
 
+// Bits [0, n) set, for n in [0, 32] (a present mask over n shards; 1u << 32 is undefined).
+__host__ __device__ inline uint32_t low_mask(uint32_t n) { return n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u); }
+
 constexpr int kCtrStride = 32;      // one 128-byte line per ticket counter
 constexpr int kCtrWords = 9 * kCtrStride;
 

@@ -252,16 +252,19 @@ Error ReedSolomonScheme::stageRecoverInput(Block& b, uint8_t* dst, size_t stride
     for (auto& sh : shards)
         if (!sh.nil() && sh.len) { L = sh.len; break; }
     if (L == 0) return codec_error(FEC_ERR_SHARD_NO_DATA);
-    uint32_t mask = 0;
     int present = 0;
     for (int i = 0; i < nsh; ++i) {
         if (shards[i].nil() || shards[i].len == 0) continue;
         if (shards[i].len != L) return codec_error(FEC_ERR_SHARD_SIZE);
-        mask |= 1u << i;
         ++present;
     }
     if (present < k_) return codec_error(FEC_ERR_TOO_FEW_SHARDS);
+    // the device decode takes uint32 present masks: n <= 32 (klauspost itself reconstructs up
+    // to 256 shards; every code the reference builds has n <= 30, manager.go:54-90)
     if (nsh > FEC_MAX_DECODE_SHARDS) return codec_error(FEC_ERR_MAX_SHARD_NUM);
+    uint32_t mask = 0;
+    for (int i = 0; i < nsh; ++i)
+        if (!shards[i].nil() && shards[i].len != 0) mask |= 1u << i;
     if (L > stride) return Error::text(fmt("shard len (%zu) exceeds the staging slot (%zu)", L, stride));
     for (int i = 0; i < nsh; ++i)
         if (mask >> i & 1u) {
@@ -955,6 +958,7 @@ int fec_batch_encoder_drain(fec_batch_encoder* e, size_t* blocks) {
 size_t fec_batch_encoder_staged(const fec_batch_encoder* e) { return e ? e->e->Staged() : 0; }
 
 size_t fec_batch_encoder_in_flight(const fec_batch_encoder* e) { return e ? e->e->InFlight() : 0; }
+size_t fec_batch_encoder_backlog(const fec_batch_encoder* e) { return e ? e->e->Backlog() : 0; }
 
 int fec_manager_add_source_symbol_frame_batched(fec_manager* m, uint64_t ssid, const uint8_t* p, size_t len,
                                                 size_t cap, fec_batch_encoder* e, fec_repair_queue* q) {

@@ -44,7 +44,7 @@ template <int POL, int KG>
 __global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
     constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     const uint32_t k = a.k, n = k + 1;
-    const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
+    const uint32_t all = low_mask(n);
     const uint32_t stride = gridDim.x * kThreads;
     for (uint32_t item = xcd_order(a.swz) * kThreads + threadIdx.x; item < a.total; item += stride) {
         const uint32_t b = fdiv(item, a.div_cps);
@@ -53,7 +53,7 @@ __global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
         const uint32_t nmiss = __popc(miss);
         const uint32_t mi = miss ? (uint32_t)__ffs(miss) - 1 : 0;
         const bool work = nmiss == 1 && mi < k;
-        const bool fail = nmiss > 1 && (miss & ((1u << k) - 1u));
+        const bool fail = nmiss > 1 && (miss & low_mask(k));
         if (c == 0) {
             if (a.status) a.status[b] = fail ? -4 : 0;
             if (fail) atomicOr(a.err, 1);

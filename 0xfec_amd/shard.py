@@ -44,3 +44,25 @@ def synth_payload_blocks(seed, lo, hi, k, payload_bytes, stride):
     out[:, :, payload_bytes] = (payload_bytes >> 8) & 0xFF
     out[:, :, payload_bytes + 1] = payload_bytes & 0xFF
     return out
+
+
+_GOLD = 0x9E3779B97F4A7C15
+_M64 = (1 << 64) - 1
+
+
+def _splitmix_fin(x):
+    x = (x + _GOLD) & _M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _M64
+    return x ^ (x >> 31)
+
+
+def synth_single_erasures(seed, lo, hi, k):
+    """Erased data shard of each global block [lo, hi): splitmix64 of a key no data word uses
+    (include/fec_synth.h fec_synth_single_erasures, restated)."""
+    import numpy as np
+    out = np.empty(hi - lo, dtype=np.int64)
+    base = (seed * _GOLD) & _M64
+    for i, b in enumerate(range(lo, hi)):
+        out[i] = _splitmix_fin(base ^ ((b << 24) & _M64) ^ 0xFFFFFF) % k
+    return out

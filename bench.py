@@ -74,25 +74,68 @@ def parse():
     return p.parse_args()
 
 
-def make_batch(torch, B, k, m, seed, device):
-    """Data shards [B, k, 1216] (random 1200-byte payloads + trailer 0x04 0xB0, zero pad) and
-    parity shards [B, m, 1216] in a separate buffer; one random erased data shard per block."""
-    n = k + m
-    g = torch.Generator(device=device)
-    g.manual_seed(seed)
-    data = torch.zeros((B, k, SHARD_STRIDE), dtype=torch.uint8, device=device)
-    for b0 in range(0, B, 1 << 16):      # chunked to bound the temporaries
-        b1 = min(B, b0 + (1 << 16))
-        data[b0:b1, :, :PAYLOAD] = torch.randint(0, 256, (b1 - b0, k, PAYLOAD), generator=g,
-                                                 device=device, dtype=torch.int16).to(torch.uint8)
-    data[:, :, PAYLOAD] = PAYLOAD >> 8
-    data[:, :, PAYLOAD + 1] = PAYLOAD & 0xFF
-    parity = torch.zeros((B, m, SHARD_STRIDE), dtype=torch.uint8, device=device)
-    erased = torch.randint(0, k, (B,), generator=g, device=device, dtype=torch.int64)
-    full = (1 << n) - 1
-    masks = (full - torch.bitwise_left_shift(torch.ones_like(erased), erased)).to(torch.int32)
-    recovered = torch.zeros((B, 1, SHARD_STRIDE), dtype=torch.uint8, device=device)
-    return data, parity, erased, masks, recovered
+class RankBatch:
+    """One rank's slice of the global batch, resident in HBM: data shards [B, k, 1216] and
+    parity shards [B, m, 1216] in separate buffers, one erased data shard per block (masks),
+    the recovered-shard buffer [B, 1, 1216]. Data and erasures come from the device generator
+    (include/fec_synth.h: splitmix64 keyed by (seed, global block, shard, word), BASELINE.md
+    §2), so any split over ranks codes the same global batch."""
+
+    def __init__(self, torch, codec, dev, B, k, m, seed, first_block):
+        self.B, self.k, self.m, self.first = B, k, m, first_block
+        self.data = torch.empty((B, k, SHARD_STRIDE), dtype=torch.uint8, device=dev)
+        codec.synth_data(seed, first_block, B, k, PAYLOAD, self.data.data_ptr(), k * SHARD_STRIDE, SHARD_STRIDE)
+        self.parity = torch.zeros((B, m, SHARD_STRIDE), dtype=torch.uint8, device=dev)
+        self.masks = torch.empty((B,), dtype=torch.int32, device=dev)
+        self.erased = torch.empty((B,), dtype=torch.int32, device=dev)
+        codec.synth_single_erasures(seed, first_block, B, k, m, self.masks.data_ptr(), self.erased.data_ptr())
+        self.recovered = torch.zeros((B, 1, SHARD_STRIDE), dtype=torch.uint8, device=dev)
+
+
+class RankStep:
+    """The hot path over one RankBatch: encode (fec_rs_encode_batch, reed_solomon.go:51) and
+    decode (fec_rs_recover_batch: ReconstructData + the copy-out of recoverSymbolPayloads,
+    reed_solomon.go:92-136), plus the in-place form (fec_rs_reconstruct_batch) timed beside."""
+
+    def __init__(self, fec, codec, batch):
+        self.fec, self.codec, self.b = fec, codec, batch
+
+    def encode(self):
+        b = self.b
+        self.codec.rs_encode_raw(b.k, b.m, SHARD_LEN, b.B, b.data.data_ptr(), b.k * SHARD_STRIDE,
+                                 b.parity.data_ptr(), b.m * SHARD_STRIDE, SHARD_STRIDE, self.fec.FEC_DEVICE)
+
+    def decode(self):
+        b = self.b
+        rc = self.codec.rs_recover_raw(b.k, b.m, SHARD_LEN, b.B, b.data.data_ptr(), b.k * SHARD_STRIDE,
+                                       b.parity.data_ptr(), b.m * SHARD_STRIDE, SHARD_STRIDE, b.masks.data_ptr(),
+                                       b.recovered.data_ptr(), SHARD_STRIDE, 1, None)
+        if rc != 0:
+            raise self.fec.FecError(rc, "decode")
+
+    def decode_inplace(self):
+        b = self.b
+        rc = self.codec.rs_reconstruct_raw(b.k, b.m, SHARD_LEN, b.B, b.data.data_ptr(), b.k * SHARD_STRIDE,
+                                           b.parity.data_ptr(), b.m * SHARD_STRIDE, SHARD_STRIDE,
+                                           b.masks.data_ptr(), None, self.fec.FEC_DEVICE)
+        if rc != 0:
+            raise self.fec.FecError(rc, "decode_inplace")
+
+    def check_full(self, torch):
+        """Outside the timed region: every recovered shard equals the erased original; then
+        wipe every erased shard, rebuild in place, compare the whole batch."""
+        b = self.b
+        rows = torch.arange(b.B, device=b.data.device)
+        er = b.erased.long()
+        ok = bool(torch.equal(b.recovered[:, 0, :SHARD_LEN], b.data[rows, er, :SHARD_LEN]))
+        ref = b.data[:, :, :SHARD_LEN].clone()
+        b.data[rows, er, :] = 0
+        self.decode_inplace()
+        self.codec.sync()
+        ok = ok and bool(torch.equal(b.data[:, :, :SHARD_LEN], ref))
+        del ref
+        torch.cuda.empty_cache()
+        return ok
 
 
 def host_threads():
@@ -160,42 +203,13 @@ def main():
     codec.use_torch_stream()
     stream = torch.cuda.current_stream(dev)
 
-    data, parity, erased, masks, recovered = make_batch(torch, B, k, m, args.seed + g_lo, dev)
-    torch.cuda.synchronize()
-    dptr, pptr, optr = data.data_ptr(), parity.data_ptr(), recovered.data_ptr()
-    dbs, pbs = k * SHARD_STRIDE, m * SHARD_STRIDE
-
-    def encode():
-        codec.rs_encode_raw(k, m, SHARD_LEN, B, dptr, dbs, pptr, pbs, SHARD_STRIDE, fec.FEC_DEVICE)
-
-    def decode():
-        rc = codec.rs_recover_raw(k, m, SHARD_LEN, B, dptr, dbs, pptr, pbs, SHARD_STRIDE, masks.data_ptr(),
-                                  optr, SHARD_STRIDE, 1, None)
-        if rc != 0:
-            raise fec.FecError(rc, "decode")
-
-    def decode_inplace():
-        rc = codec.rs_reconstruct_raw(k, m, SHARD_LEN, B, dptr, dbs, pptr, pbs, SHARD_STRIDE, masks.data_ptr(),
-                                      None, fec.FEC_DEVICE)
-        if rc != 0:
-            raise fec.FecError(rc, "decode_inplace")
-
+    batch = RankBatch(torch, codec, dev, B, k, m, args.seed, g_lo)
+    step = RankStep(fec, codec, batch)
+    encode, decode, decode_inplace = step.encode, step.decode, step.decode_inplace
     encode()
     decode()
     codec.sync()
-
-    # correctness at full size (before warmup, outside the timed region): the recovered shard
-    # of every block equals the erased original; then wipe every erased shard, rebuild in
-    # place, compare
-    rows = torch.arange(B, device=dev)
-    ok_recover = bool(torch.equal(recovered[:, 0, :SHARD_LEN], data[rows, erased, :SHARD_LEN]))
-    ref = data[:, :, :SHARD_LEN].clone()
-    data[rows, erased, :] = 0
-    decode_inplace()
-    codec.sync()
-    ok_roundtrip = bool(torch.equal(data[:, :, :SHARD_LEN], ref)) and ok_recover
-    del ref
-    torch.cuda.empty_cache()
+    ok_roundtrip = step.check_full(torch)
 
     for _ in range(args.warmup):
         encode()
@@ -246,7 +260,7 @@ def main():
             import numpy as np
             from oracle import oracle as orc
             pick = torch.randperm(B, device=dev)[:64]
-            sample = torch.cat([data[pick], parity[pick]], dim=1).cpu().numpy()
+            sample = torch.cat([batch.data[pick], batch.parity[pick]], dim=1).cpu().numpy()
             want = sample[:, :, :SHARD_LEN].copy()
             orc.rs_encode(k, m, want)
             ok_parity = bool(np.array_equal(sample[:, :, :SHARD_LEN], want))
@@ -280,7 +294,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (torch Philox bytes, seed 0x0FEC + first global block of the rank)",
+            "data": "synthetic: splitmix64 bytes keyed by (seed 0x0FEC, global block, shard, word), "
+                    "generated in HBM (include/fec_synth.h, BASELINE.md 2)",
             "config": {"workload": "RS(k=%d,n=%d) encode + random single-data-erasure decode" % (k, n),
                        "blocks_per_gpu": B, "payload_bytes": PAYLOAD, "shard_len": L,
                        "shard_stride": SHARD_STRIDE, "layout": "data [B][k][1216] + parity [B][m][1216] buffers",

@@ -63,6 +63,9 @@ int fec_batch_encoder_poll(fec_batch_encoder *e, size_t *blocks);
 int fec_batch_encoder_drain(fec_batch_encoder *e, size_t *blocks);
 size_t fec_batch_encoder_staged(const fec_batch_encoder *e);
 size_t fec_batch_encoder_in_flight(const fec_batch_encoder *e);
+/* Encoded blocks whose frames wait for room in their repair queue. Poll / drain return
+ * FEC_ERR_SCHEME "repair queue full" while this is nonzero; submit never fails for it. */
+size_t fec_batch_encoder_backlog(const fec_batch_encoder *e);
 
 int fec_manager_add_source_symbol_frame_batched(fec_manager *m, uint64_t ssid, const uint8_t *p, size_t len,
                                                 size_t cap, fec_batch_encoder *e, fec_repair_queue *q);

@@ -83,11 +83,16 @@ public:
     // Start encoding the staged blocks (asynchronous). No-op when nothing is staged.
     Error Flush();
     // Deliver the frames of every completed batch (non-blocking); *blocks = blocks delivered.
+    // Frames that do not fit their queue stay in the encoder's backlog (per queue in order)
+    // and go out on a later Poll / Drain; the call then returns "repair queue full".
+    // Backpressure never fails Submit: a staging set whose frames cannot be delivered yet
+    // moves them to the backlog and is reused.
     Error Poll(size_t* blocks = nullptr);
-    // Flush, wait for every batch and deliver.
+    // Flush, wait for every batch and deliver (backlog as Poll).
     Error Drain(size_t* blocks = nullptr);
     size_t Staged() const;     // blocks staged, not yet flushed
-    size_t InFlight() const;   // blocks flushed, not yet delivered
+    size_t InFlight() const;   // blocks flushed, not yet encoded and collected
+    size_t Backlog() const;    // blocks encoded whose frames wait for room in their queue
     int k() const { return k_; }
     int m() const { return m_; }
     DecoderFECScheme scheme() const { return scheme_; }
@@ -107,15 +112,23 @@ private:
         std::vector<Pending> blocks;
         size_t slot = 0;            // S of this batch (16-byte multiple)
         size_t maxLen = 0;          // largest L of this batch
-        size_t delivered = 0;       // blocks of a completed batch already delivered
         bool inFlight = false;
+    };
+    struct Ready {                  // an encoded block whose frames wait for queue room
+        RepairQueue* q;
+        BlockID id;
+        std::vector<Slice> payloads;   // m repair payloads, ParityID = index
     };
     BatchEncoder(DecoderFECScheme scheme, int k, int m, size_t maxBlocks, std::shared_ptr<Engine> e)
         : scheme_(scheme), k_(k), m_(m), maxBlocks_(maxBlocks), engine_(std::move(e)) {}
     Error init();
     Error flushImpl(size_t* delivered);
     Error waitSet(Set& s);
-    Error deliver(Set& s, size_t* blocks);
+    // Wait for a flushed set, move its blocks' payloads to the backlog and free the set.
+    Error retire(Set& s);
+    // Hand backlog frames to their queues in order; a queue that is full holds back its later
+    // blocks. *blocks += blocks delivered. True when the backlog is empty afterwards.
+    bool pump(size_t* blocks);
     Error slotFor(size_t want, Set** out);
 
     DecoderFECScheme scheme_;
@@ -127,6 +140,7 @@ private:
     Set sets_[2];
     int cur_ = 0;   // the set being staged
     bool ready_ = false;
+    std::deque<Ready> backlog_;
 };
 
 // Receive side: recovered payloads of one connection, in the order their
@@ -175,8 +189,8 @@ private:
         ReedSolomonScheme::RecoverPlan plan;   // RS: mask, length, missing indices
     };
     struct Set {
-        uint8_t* h_in = nullptr;    // pinned [maxBlocks][n][kSlotMax]
-        uint8_t* h_out = nullptr;   // pinned [maxBlocks][m][kSlotMax]
+        uint8_t* h_in = nullptr;    // pinned [maxBlocks][n][kDecSlotMax]
+        uint8_t* h_out = nullptr;   // pinned [maxBlocks][m][kDecSlotMax]
         uint32_t* h_masks = nullptr;
         int32_t* h_status = nullptr;
         uint8_t* d_in = nullptr;

@@ -261,13 +261,23 @@ def xor_recover_symbol_payloads(b):
         return None, "not enough present symbols to repair the missing ones"
     if b.is_complete():
         return None, None
+    # Where Go panics (index / slice bounds out of range on the 1452-byte buffer) the oracle
+    # returns the error text the product's mirror uses (fec_scheme.cpp XorScheme).
     acc = bytearray(MAX_PACKET_BUFFER_SIZE)
     for p in b.repairs.values():
+        if len(p) > MAX_PACKET_BUFFER_SIZE:
+            return None, "repair payload longer than the packet buffer"
         for i, v in enumerate(p.data):
             acc[i] ^= v
     for p in b.sources.values():
+        if b.biggest < 0 or b.biggest + 2 > MAX_PACKET_BUFFER_SIZE or len(p) > MAX_PACKET_BUFFER_SIZE:
+            return None, "source payload overruns the packet buffer"
         _xor_into(acc, p, b.biggest)
+    if b.biggest < 0 or b.biggest + 2 > MAX_PACKET_BUFFER_SIZE:
+        return None, "length trailer outside the packet buffer"
     ln = (acc[b.biggest] << 8) | acc[b.biggest + 1]
+    if ln > MAX_PACKET_BUFFER_SIZE:
+        return None, "recovered payload length exceeds the packet buffer"
     rec = bytes(acc[:ln])
     for ssid in range(b.smallest, b.largest + 1):
         if ssid not in b.sources:
@@ -285,3 +295,94 @@ def block_from_fixture(blk):
                  biggest=blk["biggestSourceSymbolLenSoFar"], smallest=blk["smallestSSID"],
                  largest=blk["largestSSID"], sources=pl(blk["ssidToSourcePayload"]),
                  repairs=pl(blk["pidToRepairPayload"]))
+
+
+# ---------------------------------------------------------------- manager layer (layer 3)
+
+class Manager:
+    """internal/fec/manager.go:41-227 restated over the scheme functions above, for one
+    connection (the sender and the receiver are the same type, manager.go:50-94). Frames are
+    (block_id, parity_id, payload bytes); source payloads arrive with the packet buffer's
+    capacity (1452, zeroed past len: packet_packer.go:984, fec_source_symbol_frame.go:34).
+
+    recover_on_source models the repo's optional receive-side extension (off in the
+    reference): a source symbol that makes its block recoverable, but not complete, recovers
+    it (the reference only recovers on a REPAIR arrival, manager.go:181 vs :221-226)."""
+
+    def __init__(self, scheme, k, m, recover_on_source=False):
+        if scheme not in ("rs", "xor"):
+            raise ValueError(scheme)
+        self.scheme, self.k, self.m = scheme, k, m
+        self.recover_on_source = recover_on_source
+        self.status = {}          # block id -> Block | "processed"  (manager.go:107, blockStatus)
+
+    def _status(self, bid):                       # newBlock, block.go:36-49
+        if bid not in self.status:
+            lo = bid * self.k
+            self.status[bid] = Block(id=bid, tot_src=self.k, tot_rep=self.m, biggest=0, smallest=lo,
+                                     largest=lo + self.k - 1)
+        return self.status[bid]
+
+    def _add_source(self, b, ssid, payload, cap):  # block.go:56-70
+        if ssid < b.smallest or ssid > b.largest:
+            return ("source symbol was provided to the wrong block. Expecting SID within the range [%d, %d] "
+                    "and got %d" % (b.smallest, b.largest, ssid))
+        if ssid not in b.sources:
+            b.sources[ssid] = Payload(payload, cap)
+            b.biggest = max(b.biggest, len(payload))
+        return None
+
+    def _recover(self, b):
+        if self.scheme == "rs":
+            return rs_recover_symbol_payloads(b, self.k, self.m)
+        return xor_recover_symbol_payloads(b)
+
+    def add_source_symbol_frame(self, ssid, payload, cap=MAX_PACKET_BUFFER_SIZE):   # manager.go:123-158
+        bid = ssid // self.k
+        b = self._status(bid)
+        if b == "processed":
+            return None, None
+        err = self._add_source(b, ssid, payload, cap)
+        if err:
+            return None, err
+        if b.is_complete():
+            frames, err = rs_repair_symbols(b, self.k, self.m) if self.scheme == "rs" else xor_repair_symbols(b)
+            if err:
+                return None, err
+            self.status[bid] = "processed"
+            return frames, None
+        return None, None
+
+    def handle_repair_frame(self, bid, pid, payload):   # manager.go:160-198
+        b = self._status(bid)
+        if b == "processed":
+            return None, None
+        if pid not in b.repairs:                        # block.go:73-85
+            b.repairs[pid] = Payload(payload)
+            b.biggest = len(payload) - REPAIR_PAYLOAD_METADATA_LEN
+        if b.is_recoverable():
+            rec, err = self._recover(b)
+            if err:
+                return None, err
+            self.status[bid] = "processed"
+            return rec, None
+        return None, None
+
+    def handle_source_symbol_frame(self, ssid, payload, cap=MAX_PACKET_BUFFER_SIZE):   # manager.go:200-227
+        """-> (payload | None, recovered | None, err)."""
+        bid = ssid // self.k
+        b = self._status(bid)
+        if b == "processed":
+            return None, None, None
+        err = self._add_source(b, ssid, payload, cap)
+        if err:
+            return None, None, err
+        rec = None
+        if b.is_complete():
+            self.status[bid] = "processed"
+        elif self.recover_on_source and b.is_recoverable():
+            rec, err = self._recover(b)
+            if err:
+                return None, None, err
+            self.status[bid] = "processed"
+        return bytes(payload), rec, None

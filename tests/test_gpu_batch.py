@@ -1,8 +1,9 @@
-"""GPU parity of the sender-side batching layer: the repair frames a connection's RepairQueue
-receives from the batched path equal, in order and byte for byte, the frames the per-block
-path (Manager.AddSourceSymbolFrame -> repairSymbols, manager.go:123-158) returns for the same
-source symbols — across batch boundaries, double-buffered batches, mixed symbol lengths and
-several connections sharing one encoder."""
+"""GPU parity of the batching layer against the CPU oracle (oracle.Manager: manager.go restated
+over the oracle's repairSymbols / recoverSymbolPayloads): the repair frames a connection's
+RepairQueue receives from the batched sender, and the payloads its RecoveredQueue receives from
+the batched receiver, equal in order and byte for byte what the oracle's manager returns for
+the same symbols — and what the per-block HIP path returns — across batch boundaries,
+double-buffered batches, mixed symbol lengths and several connections sharing one encoder."""
 import importlib
 
 import numpy as np
@@ -39,12 +40,22 @@ def _streams(rng, nconn, nblocks, k, lens):
     ("rs", 2, 1, 64, [1200, 1434]),
     ("xor", 2, 1, 3, [1, 100, 1200, 1434]),          # the reference's XOR factory code
 ])
-def test_batched_frames_equal_per_block_frames(B, S, scheme, k, m, max_blocks, lens):
+def test_batched_frames_equal_per_block_frames(B, S, oracle, scheme, k, m, max_blocks, lens):
     rng = np.random.default_rng(k * 100 + max_blocks)
     sid = S.XOR_FEC_SCHEME if scheme == "xor" else S.REED_SOLOMON_FEC_SCHEME
     nconn, nblocks = 3, 7
     streams = _streams(rng, nconn, nblocks, k, lens)
-    # per-block path
+    # the oracle's manager (CPU)
+    orc = []
+    for pl in streams:
+        mgr = oracle.Manager(scheme, k, m)
+        frames = []
+        for ssid, p in enumerate(pl):
+            fr, err = mgr.add_source_symbol_frame(ssid, p)
+            assert err is None
+            frames += fr or []
+        orc.append(frames)
+    # per-block HIP path
     want = []
     for pl in streams:
         mgr, err = S.new_manager(sid, k, m)
@@ -55,6 +66,7 @@ def test_batched_frames_equal_per_block_frames(B, S, scheme, k, m, max_blocks, l
             assert err is None
             frames += fr or []
         want.append(frames)
+    assert want == orc
     # batched path: one encoder for all connections, symbols interleaved across connections
     enc, err = B.BatchEncoder.new(sid, k, m, max_blocks=max_blocks)
     assert err is None
@@ -86,12 +98,41 @@ def test_full_queue_holds_frames_until_room(B, S):
     for ssid in range(2 * 4):
         assert mgr.add_source_symbol_frame_batched(ssid, bytes([ssid]) * 50, enc, q) is None
     n, err = enc.drain()
-    assert err == "repair queue full" and len(q) == 2
+    assert err == "repair queue full" and len(q) == 2 and enc.backlog == 2
     got = q.drain_frames()
     n, err = enc.drain()
-    assert err is None and len(q) == 2
+    assert err is None and len(q) == 2 and enc.backlog == 0
     got += q.drain_frames()
     assert [f[0] for f in got] == [0, 1, 2, 3]
+
+
+def test_submit_never_fails_on_a_full_queue(B, S, oracle):
+    """Backpressure from an earlier batch must not fail Submit (the block would never be
+    encoded: the manager drops complete blocks, manager.go:145-153): small batches flushed by
+    Submit itself while the connection's queue is full; every block's frames arrive, in order,
+    equal to the oracle's repairSymbols."""
+    k, m = 8, 4
+    enc, _ = B.BatchEncoder.new(S.REED_SOLOMON_FEC_SCHEME, k, m, max_blocks=2)
+    q = B.RepairQueue(max_len=m)          # room for one block's frames
+    mgr, _ = S.new_manager(S.REED_SOLOMON_FEC_SCHEME, k, m)
+    rng = np.random.default_rng(77)
+    nblocks = 9
+    pl = [rng.integers(0, 256, int(rng.integers(1, 1435)), dtype=np.uint8).tobytes() for _ in range(nblocks * k)]
+    got = []
+    for ssid, p in enumerate(pl):
+        # every Submit (on each block's k-th symbol) may flush and retire a batch into a full queue
+        assert mgr.add_source_symbol_frame_batched(ssid, p, enc, q) is None
+        if ssid % (3 * k) == 3 * k - 1:
+            got += q.drain_frames()
+    while True:
+        n, err = enc.drain()
+        got += q.drain_frames()
+        if err is None:
+            break
+        assert err == "repair queue full"
+    orc = oracle.Manager("rs", k, m)
+    want = sum((orc.add_source_symbol_frame(ssid, p)[0] or [] for ssid, p in enumerate(pl)), [])
+    assert len(want) == nblocks * m and got == want
 
 
 @pytest.mark.parametrize("scheme,k,m,max_blocks,lens,loss", [
@@ -100,7 +141,7 @@ def test_full_queue_holds_frames_until_room(B, S):
     ("rs", 2, 1, 64, [1200, 1434], 0.3),
     ("xor", 2, 1, 3, [1, 100, 1200, 1434], 0.3),
 ])
-def test_batched_recovery_equals_per_block_recovery(B, S, scheme, k, m, max_blocks, lens, loss):
+def test_batched_recovery_equals_per_block_recovery(B, S, oracle, scheme, k, m, max_blocks, lens, loss):
     """Receiver: the payloads HandleRepairFrame returns per block (manager.go:160-198) equal,
     in order, those the batched path delivers to the connection's RecoveredQueue, under random
     source and repair losses (some blocks unrecoverable, some complete before any repair)."""
@@ -141,6 +182,19 @@ def test_batched_recovery_equals_per_block_recovery(B, S, scheme, k, m, max_bloc
             assert err is None
         want.append(got)
     assert sum(len(w) for w in want) > 0
+    # the oracle's receivers (CPU)
+    for c, ev in enumerate(arrivals):
+        rcv = oracle.Manager(scheme, k, m)
+        got = []
+        for e in ev:
+            if e[0] == "src":
+                _, _, err = rcv.handle_source_symbol_frame(e[1], e[2])
+            else:
+                rec, err = rcv.handle_repair_frame(e[1], e[2], e[3])
+                if rec is not None:
+                    got.append((e[1], rec))
+            assert err is None
+        assert got == want[c], c
     # batched receivers sharing one decoder, arrivals interleaved across connections
     dec, err = B.BatchDecoder.new(sid, k, m, max_blocks=max_blocks)
     assert err is None
@@ -165,7 +219,7 @@ def test_batched_recovery_equals_per_block_recovery(B, S, scheme, k, m, max_bloc
 
 
 @pytest.mark.parametrize("scheme,k,m", [("rs", 20, 10), ("rs", 8, 4), ("xor", 2, 1)])
-def test_submit_payloads_equals_manager_path(B, S, scheme, k, m):
+def test_submit_payloads_equals_manager_path(B, S, oracle, scheme, k, m):
     """Zero-copy staging of source payloads (fec_wire.h) yields the frames the per-block
     manager path returns for the same symbols."""
     W = importlib.import_module("0xfec_amd.wire")
@@ -179,9 +233,44 @@ def test_submit_payloads_equals_manager_path(B, S, scheme, k, m):
         fr, err = mgr.add_source_symbol_frame(ssid, p)
         assert err is None
         want += fr or []
+    orc = oracle.Manager(scheme, k, m)
+    assert want == sum((orc.add_source_symbol_frame(ssid, p)[0] or [] for ssid, p in enumerate(pl)), [])
     enc, _ = B.BatchEncoder.new(sid, k, m, max_blocks=4)
     q = B.RepairQueue(max_len=nblocks * m)
     for blk in range(nblocks):
         assert W.submit_payloads(enc, blk, pl[blk * k:(blk + 1) * k], q) is None
     assert enc.drain()[1] is None
     assert q.drain_frames() == want
+
+
+@pytest.mark.parametrize("rlen", [1441, 1446, 1452])
+def test_long_repair_payload_batched_equals_per_block(B, S, oracle, rlen):
+    """XOR recovery accepts repair payloads up to a packet buffer (1452 B, xor.go:76-86): the
+    batched receiver must stage them like the per-block path and the oracle."""
+    k, m = 2, 1
+    rng = np.random.default_rng(rlen)
+    big = rlen - 2                       # the receiver's biggest = len(repair) - 2 (block.go:82)
+    src = rng.integers(0, 256, 700, dtype=np.uint8).tobytes()
+    lost = rng.integers(0, 256, big, dtype=np.uint8).tobytes()
+    rep = bytearray(rlen)                # xor framing of both payloads at `big` (xor.go:44-56)
+    for p in (src, lost):
+        for i, v in enumerate(p):
+            rep[i] ^= v
+        rep[big] ^= len(p) >> 8
+        rep[big + 1] ^= len(p) & 0xFF
+    rep = bytes(rep)
+    orc = oracle.Manager("xor", k, m)
+    orc.handle_source_symbol_frame(0, src)
+    want, err = orc.handle_repair_frame(0, 0, rep)
+    assert err is None and want == lost
+    rcv, _ = S.new_manager(S.XOR_FEC_SCHEME, k, m)
+    rcv.handle_source_symbol_frame(0, src)
+    got, err = rcv.handle_repair_frame(0, 0, rep)
+    assert err is None and got == want
+    dec, _ = B.BatchDecoder.new(S.XOR_FEC_SCHEME, k, m, max_blocks=4)
+    rcv2, _ = S.new_manager(S.XOR_FEC_SCHEME, k, m)
+    q = B.RecoveredQueue()
+    rcv2.handle_source_symbol_frame(0, src)
+    assert rcv2.handle_repair_frame_batched(0, 0, rep, dec, q) is None
+    assert dec.drain()[1] is None
+    assert q.drain() == [(0, want)]

@@ -364,3 +364,34 @@ def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, 
         assert np.array_equal(data.cpu().numpy()[:, :, :L], sh[:, :k, :L])
     finally:
         codec.set_tuning(**old)
+
+
+def test_rs_32_0_fully_present_is_untouched(codec, torch, fec):
+    """k = 32, m = 0 (n = 32: the widest present mask): a fully present block rebuilds nothing,
+    in place or out of place (klauspost ReconstructData with every shard present is a no-op)."""
+    k, m, B, L, S = 32, 0, 7, 100, 112
+    rng = np.random.default_rng(32)
+    data_np = rng.integers(0, 256, (B, k, S), dtype=np.uint8)
+    data = torch.from_numpy(data_np.copy()).cuda()
+    masks = torch.from_numpy(np.full(B, 0xFFFFFFFF, dtype=np.uint32).view(np.int32)).cuda()
+    st = torch.full((B,), 99, dtype=torch.int32, device="cuda")
+    rc = codec.rs_reconstruct_raw(k, m, L, B, data.data_ptr(), k * S, data.data_ptr(), k * S, S, masks.data_ptr(),
+                                  st.data_ptr(), fec.FEC_DEVICE)
+    assert rc == 0
+    codec.sync()
+    assert np.array_equal(data.cpu().numpy(), data_np) and not st.cpu().numpy().any()
+    out = torch.full((B, 1, S), 0xEE, dtype=torch.uint8, device="cuda")
+    st.fill_(99)
+    rc = codec.rs_recover_raw(k, m, L, B, data.data_ptr(), k * S, data.data_ptr(), k * S, S, masks.data_ptr(),
+                              out.data_ptr(), S, 1, st.data_ptr())
+    assert rc == 0
+    codec.sync()
+    assert (out.cpu().numpy() == 0xEE).all() and not st.cpu().numpy().any()
+    # one erasure with no parity: too few shards, data untouched
+    masks.fill_(np.uint32(0x7FFFFFFF).view(np.int32))
+    rc = codec.rs_reconstruct_raw(k, m, L, B, data.data_ptr(), k * S, data.data_ptr(), k * S, S, masks.data_ptr(),
+                                  st.data_ptr(), fec.FEC_DEVICE)
+    assert rc == 0
+    assert codec.lib_sync_rc() == fec.FEC_ERR_TOO_FEW_SHARDS
+    assert (st.cpu().numpy() == fec.FEC_ERR_TOO_FEW_SHARDS).all()
+    assert np.array_equal(data.cpu().numpy(), data_np)

@@ -68,13 +68,31 @@ def _model(events, payloads, k, on_source):
 CASES = [("rs", 20, 10, 6, 0.2), ("rs", 8, 4, 24, 0.15), ("rs", 2, 1, 40, 0.2), ("xor", 2, 1, 40, 0.25)]
 
 
+def _oracle_receiver(oracle, scheme, k, m, events, on):
+    """The same arrivals through the oracle's manager (manager.go restated, CPU)."""
+    rcv = oracle.Manager(scheme, k, m, recover_on_source=on)
+    got = []
+    for e in events:
+        if e[0] == "src":
+            _, rec, err = rcv.handle_source_symbol_frame(e[1], e[2])
+            blk = e[1] // k
+        else:
+            rec, err = rcv.handle_repair_frame(e[1], e[2], e[3])
+            blk = e[1]
+        assert err is None
+        if rec is not None:
+            got.append((blk, rec))
+    return got
+
+
 @pytest.mark.parametrize("scheme,k,m,nblocks,loss", CASES)
 @pytest.mark.parametrize("on", [False, True])
-def test_per_block_receiver(S, scheme, k, m, nblocks, loss, on):
+def test_per_block_receiver(S, oracle, scheme, k, m, nblocks, loss, on):
     rng = np.random.default_rng(1000 * k + m)
     sid = S.XOR_FEC_SCHEME if scheme == "xor" else S.REED_SOLOMON_FEC_SCHEME
     payloads, events = _arrivals(S, rng, sid, k, m, nblocks, loss)
     want = _model(events, payloads, k, on)
+    assert _oracle_receiver(oracle, scheme, k, m, events, on) == want
     if on:
         assert len(want) > len(_model(events, payloads, k, False))   # the extension matters here
     rcv, _ = S.new_manager(sid, k, m)
@@ -96,13 +114,14 @@ def test_per_block_receiver(S, scheme, k, m, nblocks, loss, on):
 
 
 @pytest.mark.parametrize("scheme,k,m,nblocks,loss", CASES)
-def test_batched_receiver(B, S, scheme, k, m, nblocks, loss):
+def test_batched_receiver(B, S, oracle, scheme, k, m, nblocks, loss):
     """Same arrivals through HandleSourceSymbolFrameBatched / HandleRepairFrameBatched with the
     flag on: the RecoveredQueue holds exactly the per-block path's recoveries, in order."""
     rng = np.random.default_rng(1000 * k + m)
     sid = S.XOR_FEC_SCHEME if scheme == "xor" else S.REED_SOLOMON_FEC_SCHEME
     payloads, events = _arrivals(S, rng, sid, k, m, nblocks, loss)
     want = _model(events, payloads, k, True)
+    assert _oracle_receiver(oracle, scheme, k, m, events, True) == want
     dec, err = B.BatchDecoder.new(sid, k, m, max_blocks=5)
     assert err is None
     rcv, _ = S.new_manager(sid, k, m)
