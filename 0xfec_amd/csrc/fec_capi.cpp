@@ -28,6 +28,9 @@ struct Code {
     uint8_t* d_prows = nullptr;    // m x k
     uint32_t* d_tabs = nullptr;    // m x k PermTabs
     uint32_t* d_dytabs = nullptr;  // dyadic codes: leaf PermTabs of the split-recursive encode
+    uint32_t* d_single = nullptr;  // single-erasure decode tables (fk::direct_table_words), when small
+    uint32_t* d_single_coef = nullptr;   // their coefficient bytes, (k*m) rows of ceil(k/4) dwords
+    std::vector<uint32_t> single_coef;   // host copy
 };
 
 // Parity row r, column j of a dyadic code is g(r ^ j), g = parity row 0 (fec_kernels.hip,
@@ -75,6 +78,8 @@ struct fec_ctx {
     std::map<std::pair<int, int>, Code> codes;
     uint8_t* d_plans = nullptr;
     size_t plans_cap = 0;
+    uint32_t* d_hard = nullptr;   // direct decode's multi-erasure worklist (fk::kHardList + waves words)
+    size_t hard_cap = 0;
     int* d_err = nullptr;    // [0] sticky device-path error, [1] host-path error
     uint32_t* d_ctr = nullptr;   // ticket counters of the queue kernels (fk::kCtrWords words)
     uint8_t* h_stage = nullptr;
@@ -128,6 +133,39 @@ static int get_code(fec_ctx* ctx, int k, int m, Code** out) {
         HIP_TRY(hipMalloc(&c.d_tabs, tabs.size() * 4));
         HIP_TRY(hipMemcpy(c.d_prows, c.matrix.data() + (size_t)k * k, (size_t)m * k, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(c.d_tabs, tabs.data(), tabs.size() * 4, hipMemcpyHostToDevice));
+        // single-erasure plans: data shard E0 lost, parity R0 the first present one; inputs are
+        // the other data shards in order, then parity R0 (the first k present shards):
+        // x_E0 = inv(A[R0][E0]) * (p_R0 ^ sum_{j != E0} A[R0][j] x_j)   (reed_solomon.go:124)
+        if (k + m <= FEC_MAX_DECODE_SHARDS && fk::direct_table_words((uint32_t)k, (uint32_t)m) * 4 <= 16 * 1024) {
+            std::vector<uint32_t> st(fk::direct_table_words((uint32_t)k, (uint32_t)m), 0);
+            for (int e0 = 0; e0 < k; ++e0)
+                for (int r0 = 0; r0 < m; ++r0) {
+                    const uint8_t* row = c.matrix.data() + (size_t)(k + r0) * k;
+                    const uint8_t inv = gf::inv(row[e0]);
+                    for (int j = 0, pos = 0; j <= k; ++j) {
+                        if (j == e0) continue;
+                        const uint8_t coef = j < k ? gf::mul(inv, row[j]) : inv;
+                        gf::PermTab t = gf::make_permtab(coef);
+                        memcpy(&st[(((size_t)e0 * m + r0) * k + pos) * 8], &t, sizeof(t));
+                        ++pos;
+                    }
+                }
+            HIP_TRY(hipMalloc(&c.d_single, st.size() * 4));
+            HIP_TRY(hipMemcpy(c.d_single, st.data(), st.size() * 4, hipMemcpyHostToDevice));
+            const size_t kw = ((size_t)k + 3) / 4;
+            std::vector<uint32_t> sc((size_t)k * m * kw, 0);
+            for (int e0 = 0; e0 < k; ++e0)
+                for (int r0 = 0; r0 < m; ++r0) {
+                    const uint8_t* row = c.matrix.data() + (size_t)(k + r0) * k;
+                    const uint8_t inv = gf::inv(row[e0]);
+                    uint8_t* dst = reinterpret_cast<uint8_t*>(&sc[((size_t)e0 * m + r0) * kw]);
+                    for (int j = 0, pos = 0; j <= k; ++j)
+                        if (j != e0) dst[pos++] = j < k ? gf::mul(inv, row[j]) : inv;
+                }
+            c.single_coef = sc;
+            HIP_TRY(hipMalloc(&c.d_single_coef, sc.size() * 4));
+            HIP_TRY(hipMemcpy(c.d_single_coef, sc.data(), sc.size() * 4, hipMemcpyHostToDevice));
+        }
         const std::vector<uint8_t> leaves = dyadic_leaves(c.matrix, k, m);
         if (!leaves.empty() && leaves.size() <= (size_t)m * k) {   // staged like m x k tables
             std::vector<uint32_t> dy((size_t)m * k * 8, 0);
@@ -152,6 +190,19 @@ static int grow_plans(fec_ctx* ctx, size_t bytes) {
     ctx->plans_cap = 0;
     HIP_TRY(hipMalloc(&ctx->d_plans, bytes));
     ctx->plans_cap = bytes;
+    return FEC_OK;
+}
+
+static int grow_hard(fec_ctx* ctx, size_t waves) {
+    const size_t words = fk::kHardList + waves;
+    if (words <= ctx->hard_cap) return FEC_OK;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (ctx->d_hard) HIP_TRY(hipFree(ctx->d_hard));
+    ctx->d_hard = nullptr;
+    ctx->hard_cap = 0;
+    HIP_TRY(hipMalloc(&ctx->d_hard, words * 4));
+    HIP_TRY(hipMemset(ctx->d_hard, 0, fk::kHardList * 4));   // count and done: rewound by the kernel after
+    ctx->hard_cap = words;
     return FEC_OK;
 }
 
@@ -253,10 +304,15 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
     const uint32_t maxe = std::max<uint32_t>(1, std::min(k, m));
     const uint32_t cps = (uint32_t)((len + fk::kChunk - 1) / fk::kChunk);
     const fk::PlanLayout lay = fk::plan_layout(k, maxe);
-    size_t per_launch = std::min<size_t>(kPlanBytes / lay.stride, (size_t)(kMaxItems / cps));
+    // direct form: no plan kernel (single-erasure tables of the code; multi-erasure waves plan
+    // in-wave), fec_recover.hip
+    const bool direct = code->d_single && fk::direct_recon_applies(k, m, cps, lay.stride);
+    size_t per_launch = std::min<size_t>(direct ? nblocks : kPlanBytes / lay.stride, (size_t)(kMaxItems / cps));
     per_launch = std::max<size_t>(1, std::min(per_launch, nblocks));
-    int rc = grow_plans(ctx, per_launch * lay.stride);
-    if (rc) return rc;
+    {
+        int rc = direct ? grow_hard(ctx, (per_launch * cps + 63) / 64) : grow_plans(ctx, per_launch * lay.stride);
+        if (rc) return rc;
+    }
     const uint32_t G = fk::pick_tile_blocks(cps, k, maxe, lay);
     const size_t lds = fk::recon_lds_bytes(G, k, maxe, lay);
     const bool wave = fk::wave_recon_applies(cps, k, maxe, lay.stride);
@@ -275,7 +331,7 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         p.maxe = maxe;
         p.lay = lay;
         p.max_out = out ? out_slots : 0;
-        if (!fused) HIP_TRY(fk::launch_rs_plan(p, ctx->stream));
+        if (!fused && !direct) HIP_TRY(fk::launch_rs_plan(p, ctx->stream));
         fk::ReconArgs a{};
         a.data = data + b0 * dbs;
         a.parity = parity + b0 * pbs;
@@ -298,6 +354,20 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         a.diag = (uint32_t)fk::g_tune.dec_diag;
         a.out = out ? out + b0 * out_bs : nullptr;
         a.out_bs = out_bs;
+        if (direct) {
+            a.masks = p.masks;
+            a.status = p.status;
+            a.err = p.err;
+            a.prows = p.prows;
+            a.m = m;
+            a.max_out = p.max_out;
+            a.single = code->d_single;
+            a.single_coef = code->d_single_coef;
+            a.single_coef_host = code->single_coef.data();
+            a.hard = ctx->d_hard;
+            HIP_TRY(fk::launch_rs_recover_direct(a, ctx->ncu, ctx->stream));
+            continue;
+        }
         if (fused) {
             a.masks = p.masks;
             a.status = p.status;
@@ -529,8 +599,11 @@ void fec_ctx_destroy(fec_ctx* ctx) {
         if (kv.second.d_prows) (void)hipFree(kv.second.d_prows);
         if (kv.second.d_tabs) (void)hipFree(kv.second.d_tabs);
         if (kv.second.d_dytabs) (void)hipFree(kv.second.d_dytabs);
+        if (kv.second.d_single) (void)hipFree(kv.second.d_single);
+        if (kv.second.d_single_coef) (void)hipFree(kv.second.d_single_coef);
     }
     if (ctx->d_plans) (void)hipFree(ctx->d_plans);
+    if (ctx->d_hard) (void)hipFree(ctx->d_hard);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->d_ctr) (void)hipFree(ctx->d_ctr);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
@@ -566,7 +639,7 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 16 ? &fk::g_tune.enc_qdepth : key == 17 ? &fk::g_tune.dec_wave
               : key == 18 ? &fk::g_tune.enc_diag : key == 19 ? &fk::g_tune.dec_fused
               : key == 20 ? &fk::g_tune.dec_ipl : key == 21 ? &fk::g_tune.dec_diag
-              : key == 22 ? &fk::g_tune.enc_dyadic : nullptr;
+              : key == 22 ? &fk::g_tune.enc_dyadic : key == 23 ? &fk::g_tune.dec_direct : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

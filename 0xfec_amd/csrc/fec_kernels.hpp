@@ -87,7 +87,16 @@ struct ReconArgs {
     int* err;
     const uint8_t* prows;
     uint32_t m, max_out;
+    // direct form (rs_recover_direct_kernel): single-erasure coefficient tables, k*m*k PermTabs,
+    // entry ((E0*m + R0)*k + j) = coefficient of input j (data shards != E0 in order, then
+    // parity R0) when data shard E0 is the only erasure and R0 the first present parity
+    const uint32_t* single;
+    const uint32_t* single_coef;   // the same plans' coefficient bytes: (k*m) rows of ceil(k/4) dwords
+    const uint32_t* single_coef_host;   // host copy of single_coef (passed as a kernel argument when small)
+    uint32_t* hard;            // multi-erasure worklist: [0] count, [kHardDone] done, [kHardList..] wave items
 };
+
+constexpr uint32_t kHardDone = 32, kHardList = 64;   // worklist words (own 128-byte lines)
 
 struct XorArgs {
     const uint8_t* in;         // data shard 0 of block 0
@@ -131,6 +140,9 @@ struct Tuning {
     int enc_dyadic = 1;       // fixed-shape encode of dyadic codes (RS(8,12), RS(16,24)) by the
                               // split-recursive product (fewer field multiplications)
     int dec_diag = 0;         // diagnostics only: wave reconstruct with one shared plan (wrong output)
+    int dec_direct = 1;       // single-erasure codes with small tables: no plan kernel, per-lane table
+                              // lookup (1: rows expanded from scalar-loaded coefficients, 2: PermTab rows
+                              // copied by a vector load); multi-erasure waves go to a worklist kernel
     int dec_ipl = 0;          // wave-form reconstruct items per lane: 1; 2 loaded together; 3: 2 one
                               // after the other (one plan stage); 0: 2 for k <= 4, else 1
 };
@@ -162,6 +174,10 @@ hipError_t launch_rs_reconstruct(const ReconArgs& a, int grid, hipStream_t s);
 bool wave_recon_applies(uint32_t cps, uint32_t k, uint32_t maxe, uint32_t stride);
 hipError_t launch_rs_reconstruct_wave(const ReconArgs& a, hipStream_t s);
 hipError_t launch_rs_recover_fused(const ReconArgs& a, hipStream_t s);
+// Direct form (fec_recover.hip): applies when the single-erasure tables of (k, m) fit in LDS.
+bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t stride);
+size_t direct_table_words(uint32_t k, uint32_t m);
+hipError_t launch_rs_recover_direct(const ReconArgs& a, int ncu, hipStream_t s);
 hipError_t launch_xor_encode(const XorArgs& a, int grid, hipStream_t s);
 hipError_t launch_xor_reconstruct(const XorArgs& a, int grid, hipStream_t s);
 

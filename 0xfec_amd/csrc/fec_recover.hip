@@ -1,0 +1,340 @@
+// fec_recover.hip — direct RS reconstruct for gfx950 (reed_solomon.go:124 ReconstructData, and the
+// copy-out of recoverSymbolPayloads, :126-135), for codes whose single-erasure coefficient tables
+// are small (k*m*k PermTabs <= 16 KiB: RS(2,3), RS(8,12), ...).
+//
+// A block with one erased data shard E0 is rebuilt from the first k present shards in index
+// order — the k-1 other data shards and the first present parity R0 — with the coefficients of
+// parity row R0 (x_E0 = inv(A[R0][E0]) * (p_R0 ^ sum_j A[R0][j] x_j)). Those coefficients depend
+// on (E0, R0) only, so every one of the k*m plans is expanded to PermTabs once per code on the
+// host (a table of k*m*k*32 bytes that stays in L2): a lane reads its block's present mask,
+// derives (E0, R0) and its input slots from it with a few scalar-width ops and issues its k loads
+// straight away, while its wave copies the <= 3 table rows it needs into LDS. No plan kernel, no
+// plan records in HBM, no PermTab expansion on the device.
+//
+// A wave holding a block with two or more erasures is put on a worklist instead; a second,
+// persistent kernel (rs_recover_hard_kernel) builds those waves' plans in-wave and rebuilds them
+// through the general path, so the single-erasure kernel keeps its small register footprint.
+#include <string.h>
+
+#include "fec_recon.hpp"
+
+namespace fk {
+
+// LDS of one direct wave (4 per workgroup, no workgroup-level staging, no barrier): the PermTab
+// rows of its <= 3 blocks.
+__host__ __device__ inline size_t direct_wave_bytes(uint32_t k) { return (size_t)kWaveBlocks * k * sizeof(gf::PermTab); }
+
+// LDS of one wave of the multi-erasure kernel: exp/log and the parity rows, then a fused slice
+// (PermTabs of <= 3 blocks' rows, their plan records, Lagrange scratch).
+__host__ __device__ inline size_t hard_head_bytes(uint32_t m, uint32_t k) { return (768 + (size_t)m * k + 15) & ~(size_t)15; }
+__host__ __device__ inline size_t hard_wave_bytes(uint32_t m, uint32_t k, uint32_t maxe, uint32_t stride) {
+    return hard_head_bytes(m, k) + fused_slice_bytes(k, maxe, stride);
+}
+
+constexpr size_t kDirectTableBytes = 16 * 1024;
+
+// The fetched 16-byte table pieces of a wave (NT per lane) into its LDS rows, then a wave barrier.
+template <int NT>
+__device__ __forceinline__ void rows_to_lds(gf::PermTab* wt, const uint4 (&tv)[NT], uint32_t lane, uint32_t n) {
+    uint4* w = reinterpret_cast<uint4*>(wt);
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+        if (lane + 64u * q < n) w[lane + 64u * q] = tv[q];
+    wave_sync();
+}
+
+// The single-erasure coefficient bytes of a small code ((k*m) rows of ceil(k/4) dwords), passed
+// by value: the kernel reads them from its argument segment with scalar loads.
+constexpr uint32_t kCoefWords = 128;
+struct CoefWords {
+    uint32_t w[kCoefWords];
+};
+
+// K: compile-time data shard count (0: runtime a.k). TAB: how a wave gets the PermTabs of its
+// blocks' rows: 0 copies them from the code's PermTab table (one vector load per wave, L1/L2
+// hits); 1 reads the rows' coefficient bytes from the kernel arguments (scalar loads, off the
+// vector memory path) and expands them on the lanes (gf::make_permtab).
+template <int K, int POL, int TAB>
+__global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a, CoefWords cwords) {
+    constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t k = K ? (uint32_t)K : a.k, m = a.m;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint8_t* slice = smem + (size_t)wave * direct_wave_bytes(k);
+    const uint32_t total = a.nblocks * a.cps;
+    const uint32_t i0 = xcd_order(a.swz) * kThreads + (wave << 6);
+    if (i0 >= total) return;
+    const uint32_t bfirst = fdiv(i0, a.div_cps);
+    const uint32_t nb = fdiv(min(i0 + 63u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
+    const uint32_t all = low_mask(k + m), kmask = low_mask(k);
+    const uint32_t mine = lane < nb ? a.masks[bfirst + lane] : 0u;   // the wave's masks in one load
+
+    // A block with two or more erasures (and enough shards) sends the whole wave to the
+    // worklist of rs_recover_hard_kernel; it writes that wave's statuses.
+    bool hard = false;
+    for (uint32_t g = 0; g < nb; ++g) {
+        const uint32_t mask = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)g) & all;
+        const uint32_t e = k - __popc(mask & kmask);
+        if (e >= 2 && (uint32_t)__popc(mask) >= k && !(a.max_out && e > a.max_out)) hard = true;
+    }
+    if (hard) {
+        if (lane == 0) a.hard[kHardList + atomicAdd(a.hard, 1u)] = i0;
+        return;
+    }
+    // Per block (uniform): status (recover: e rebuilt; in place: 0) and failures, as
+    // rs_plan_kernel reports them, and the table row (E0 * m + R0) of a single-erasure block.
+    uint32_t row[kWaveBlocks] = {0, 0, 0};
+#pragma unroll
+    for (uint32_t g = 0; g < kWaveBlocks; ++g) {
+        if (g >= nb) break;
+        const uint32_t mask = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)g) & all;
+        const uint32_t e = k - __popc(mask & kmask);
+        int32_t st = a.max_out ? (int32_t)e : 0;
+        if (e != 0 && (uint32_t)__popc(mask) < k) {
+            st = -4;   // FEC_ERR_TOO_FEW_SHARDS
+            if (lane == 0) atomicOr(a.err, 1);
+        } else if (a.max_out && e > a.max_out) {
+            st = -1;   // FEC_ERR_INVALID_ARG
+            if (lane == 0) atomicOr(a.err, 2);
+        } else if (e == 1) {
+            row[g] = (__ffs(~mask & kmask) - 1) * m + (__ffs(mask >> k) - 1);   // m >= 1 here: k < 32
+        }
+        if (lane == 0 && a.status) a.status[bfirst + g] = st;
+    }
+    // The PermTab rows of the wave's blocks into its LDS slice, prepared while the data loads are
+    // in flight (vector loads return in order: LDS writes that wait for a row load wait for that
+    // load only, and scalar loads are counted apart).
+    gf::PermTab* wt = reinterpret_cast<gf::PermTab*>(slice);
+    // TAB 0: pieces per lane: 3 blocks * 2k 16-byte pieces (<= 64 for k <= 10, the compile-time shapes)
+    constexpr int NT = (K > 0 && K <= 10) ? 1 : 3;
+    uint4 tv[NT];
+    if constexpr (TAB == 0) {
+        // unconditional loads (a lane past the wave's pieces re-reads a valid piece): no branch,
+        // so nothing makes the compiler wait for them before the data loads
+        const uint4* src = reinterpret_cast<const uint4*>(a.single);
+        const uint32_t np = nb * 2 * k;
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+            const uint32_t t = min(lane + 64u * q, np - 1u);
+            const uint32_t g = t / (2 * k), r = t - g * 2 * k;
+            const uint32_t rw = g == 0 ? row[0] : g == 1 ? row[1] : row[2];
+            tv[q] = src[(size_t)rw * 2 * k + r];
+        }
+    }
+    // TAB 1: the rows' coefficient words by scalar loads (uniform addresses, constant cache), then
+    // lane l < nb*k expands coefficient j = l % k of block g = l / k into wt[l]
+    constexpr uint32_t KW = K > 0 ? (K + 3) / 4 : 8;   // coefficient dwords per row (k <= 32)
+    uint32_t cw[kWaveBlocks][KW];
+    if constexpr (TAB == 1) {
+        const uint32_t* ct = cwords.w;   // a kernel argument: read with scalar loads
+        const uint32_t kw = (k + 3) / 4;
+#pragma unroll
+        for (uint32_t g = 0; g < kWaveBlocks; ++g)
+#pragma unroll
+            for (uint32_t q = 0; q < KW; ++q) {
+                // the index is wave-uniform; readfirstlane makes that visible, so the load is scalar
+                const uint32_t at = (uint32_t)__builtin_amdgcn_readfirstlane((int)(row[g] * kw + q));
+                cw[g][q] = q < kw ? ct[at] : 0u;
+            }
+    }
+    auto expand_rows = [&]() {
+        for (uint32_t l = lane; l < nb * k; l += 64) {
+            const uint32_t lg = l / k, lj = l - lg * k;
+            uint32_t coef = 0;
+#pragma unroll
+            for (uint32_t g = 0; g < kWaveBlocks; ++g)
+#pragma unroll
+                for (uint32_t q = 0; q < KW; ++q)
+                    if (lg == g && (lj >> 2) == q) coef = (cw[g][q] >> (8 * (lj & 3))) & 0xFFu;
+            wt[l] = gf::make_permtab((uint8_t)coef);
+        }
+        wave_sync();
+    };
+    const uint32_t item = i0 + lane;
+    const bool inr = item < total;
+    const uint32_t blk = inr ? fdiv(item, a.div_cps) : bfirst;
+    const uint32_t g = blk - bfirst;
+    const uint32_t c = item - blk * a.cps;
+    const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 0);
+    const uint32_t m1 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 1);
+    const uint32_t m2 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 2);
+    const uint32_t mask = (g == 0 ? m0 : g == 1 ? m1 : m2) & all;
+    const bool work = inr && k - __popc(mask & kmask) == 1 && (uint32_t)__popc(mask) >= k;
+    const uint32_t E0 = __ffs(~mask & kmask) - 1;
+    const uint32_t R0 = work ? __ffs(mask >> k) - 1 : 0;
+    const gf::PermTab* T = wt + g * k;
+    const uint8_t* dblk = a.data + (uint64_t)blk * a.dbs + (uint64_t)c * kChunk;
+    const uint8_t* par = a.parity + (uint64_t)blk * a.pbs + (uint64_t)R0 * a.ss + (uint64_t)c * kChunk;
+    uint32_t acc[4] = {0, 0, 0, 0};
+    if constexpr (K > 0) {
+        // unconditional loads (a lane with nothing to rebuild reads one L2-resident table line
+        // instead): no branch around them, so the row pieces' LDS writes wait for the row loads
+        // only (vmcnt counts in order), not for the data
+        const uint8_t* idle = reinterpret_cast<const uint8_t*>(a.single);
+        const uint64_t ss = work ? a.ss : 0;
+        const uint8_t* d0 = work ? dblk : idle;
+        const uint8_t* p0 = work ? par : idle;
+        uint4 x[K];
+#pragma unroll
+        for (int j = 0; j < K - 1; ++j) x[j] = ld16<NTL>(d0 + (uint64_t)(j + (j >= (int)E0)) * ss);
+        x[K - 1] = ld16<NTL>(p0);
+        if constexpr (TAB == 0) rows_to_lds(wt, tv, lane, nb * 2 * k);
+        else expand_rows();
+        if (!work) return;
+#pragma unroll
+        for (int j = 0; j < K; j += 2) {
+            Idx ia[4], ib[4];
+            split4(ia, x[j]);
+            if (j + 1 < K) {
+                split4(ib, x[j + 1]);
+                mac2(acc, ia, ib, T + j, T + j + 1);
+            } else {
+                mac1(acc, ia, T + j);
+            }
+        }
+    } else {
+        if constexpr (TAB == 0) rows_to_lds(wt, tv, lane, nb * 2 * k);
+        else expand_rows();
+        if (!work) return;
+        for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
+            uint4 x[kInGroup];
+#pragma unroll
+            for (int jj = 0; jj < kInGroup; ++jj) {
+                const uint32_t j = j0 + jj;
+                x[jj] = j + 1 < k ? ld16<NTL>(dblk + (uint64_t)(j + (j >= E0)) * a.ss)
+                                  : (j + 1 == k ? ld16<NTL>(par) : make_uint4(0, 0, 0, 0));
+            }
+#pragma unroll
+            for (int jj = 0; jj < kInGroup; jj += 2) {
+                const uint32_t j = j0 + jj;
+                if (j + 1 < k) {
+                    Idx ia[4], ib[4];
+                    split4(ia, x[jj]);
+                    split4(ib, x[jj + 1]);
+                    mac2(acc, ia, ib, T + j, T + j + 1);
+                } else if (j < k) {
+                    Idx ia[4];
+                    split4(ia, x[jj]);
+                    mac1(acc, ia, T + j);
+                }
+            }
+        }
+    }
+    uint8_t* dst = a.out ? a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk
+                         : const_cast<uint8_t*>(dblk) + (uint64_t)E0 * a.ss;
+    store_chunk<NTS>(dst, as_uint4(acc), a.len - c * kChunk, a.pad_zero);
+}
+
+// Waves the direct kernel found holding a multi-erasure block (worklist a.hard: [0] count,
+// [kHardDone] finished workgroups, [kHardList..] item bases): a persistent grid of waves takes them
+// in turn, builds the plans of each wave's blocks in-wave (build_wave_plans, the fused form of
+// fec_decode.hip) and rebuilds them through the general per-item path. With an empty list every
+// wave exits at once. The last workgroup to finish rewinds the worklist for the next launch.
+template <int MAXE, int POL>
+__global__ __launch_bounds__(kThreads) void rs_recover_hard_kernel(ReconArgs a) {
+    constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t k = a.k, m = a.m, maxe = a.maxe;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t count = __hip_atomic_load(a.hard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t W = gridDim.x * (kThreads / 64);
+    uint32_t t = blockIdx.x * (kThreads / 64) + wave;
+    if (t < count) {
+        uint8_t* f = smem + (size_t)wave * hard_wave_bytes(m, k, maxe, a.lay.stride);
+        for (uint32_t i = lane; i < 512; i += 64) f[i] = gf::kTables.exp[i];
+        for (uint32_t i = lane; i < 256; i += 64) f[512 + i] = gf::kTables.log[i];
+        for (uint32_t i = lane; i < m * k; i += 64) f[768 + i] = a.prows[i];
+        uint8_t* fs = f + hard_head_bytes(m, k);
+        gf::PermTab* wt = reinterpret_cast<gf::PermTab*>(fs);
+        uint8_t* plans = fs + (size_t)kWaveBlocks * maxe * k * sizeof(gf::PermTab);
+        const uint32_t total = a.nblocks * a.cps;
+        for (; t < count; t += W) {
+            const uint32_t i0 = a.hard[kHardList + t];
+            const uint32_t bfirst = fdiv(i0, a.div_cps);
+            const uint32_t nb = fdiv(min(i0 + 63u, total - 1u), a.div_cps) - bfirst + 1;
+            const uint32_t mine = lane < nb ? a.masks[bfirst + lane] : 0u;
+            wave_sync();   // the previous wave's reads of the slice are done; staging is visible
+            build_wave_plans(a, plans, bfirst, nb, lane, mine, f, f + 512, f + 768);   // statuses too
+            wave_sync();
+            const uint32_t ne = nb * maxe * k;
+            for (uint32_t i = lane; i < ne; i += 64) {
+                const uint32_t g = i / (maxe * k);
+                const uint32_t rem = i - g * maxe * k;
+                const uint32_t r = rem / k, j = rem - r * k;
+                const uint8_t* P = plans + g * a.lay.stride;
+                if (r < P[a.lay.nout_off]) wt[i] = gf::make_permtab(P[a.lay.coef_off + r * k + j]);
+            }
+            wave_sync();
+            const uint32_t item = i0 + lane;
+            const bool inr = item < total;
+            const uint32_t blk = inr ? fdiv(item, a.div_cps) : bfirst;
+            const uint32_t g = blk - bfirst;
+            const uint32_t c = item - blk * a.cps;
+            const uint8_t* P = plans + g * a.lay.stride;
+            const uint32_t nout = inr ? P[a.lay.nout_off] : 0;
+            const uint32_t rows = wave_rows<MAXE>(nout);
+            if (nout) recon_item<MAXE, NTL, NTS>(a, P, wt + g * maxe * k, blk, c, rows, nout);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(a.hard + kHardDone, 1u) == gridDim.x - 1) {
+            atomicExch(a.hard, 0u);
+            atomicExch(a.hard + kHardDone, 0u);
+        }
+    }
+}
+
+size_t direct_table_words(uint32_t k, uint32_t m) { return (size_t)k * m * k * 8; }
+
+bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t stride) {
+    if (!g_tune.dec_direct || m == 0 || k + m > 32 || cps < 32) return false;
+    if ((size_t)k * m * k * sizeof(gf::PermTab) > kDirectTableBytes) return false;
+    const uint32_t maxe = std::max<uint32_t>(1, std::min(k, m));
+    return 4 * hard_wave_bytes(m, k, maxe, stride) <= 64 * 1024;
+}
+
+template <int K, int POL, int TAB>
+static hipError_t direct_launch(const ReconArgs& a, const CoefWords& cw, hipStream_t s) {
+    const uint64_t total = (uint64_t)a.nblocks * a.cps;
+    const int grid = (int)((total + kThreads - 1) / kThreads);
+    if (grid == 0) return hipSuccess;
+    const size_t lds = occupancy_lds(g_tune.dec_wpc, 4 * direct_wave_bytes(a.k));
+    hipLaunchKernelGGL((rs_recover_direct_kernel<K, POL, TAB>), dim3(grid), dim3(kThreads), lds, s, a, cw);
+    return hipGetLastError();
+}
+
+template <int MAXE, int POL>
+static hipError_t hard_launch(const ReconArgs& a, int ncu, hipStream_t s) {
+    const size_t lds = 4 * hard_wave_bytes(a.m, a.k, a.maxe, a.lay.stride);
+    hipLaunchKernelGGL((rs_recover_hard_kernel<MAXE, POL>), dim3(ncu * 4), dim3(kThreads), lds, s, a);
+    return hipGetLastError();
+}
+
+template <int POL>
+static hipError_t direct_dispatch(const ReconArgs& a, int ncu, hipStream_t s) {
+    // the reference's benchmark shapes at compile time, the rest by runtime k
+    hipError_t e;
+    CoefWords cw{};
+    const size_t kw = (a.k + 3) / 4, words = (size_t)a.k * a.m * kw;
+    const bool by_arg = g_tune.dec_direct != 2 && a.single_coef_host && words <= kCoefWords;
+    if (by_arg) memcpy(cw.w, a.single_coef_host, words * 4);
+    if (!by_arg)
+        e = a.k == 2 ? direct_launch<2, POL, 0>(a, cw, s) : a.k == 8 ? direct_launch<8, POL, 0>(a, cw, s)
+                                                                     : direct_launch<0, POL, 0>(a, cw, s);
+    else
+        e = a.k == 2 ? direct_launch<2, POL, 1>(a, cw, s) : a.k == 8 ? direct_launch<8, POL, 1>(a, cw, s)
+                                                                     : direct_launch<0, POL, 1>(a, cw, s);
+    if (e != hipSuccess || a.m < 2) return e;   // m = 1: two erasures always leave too few shards
+    if (a.maxe <= 2) return hard_launch<2, POL>(a, ncu, s);
+    if (a.maxe <= 4) return hard_launch<4, POL>(a, ncu, s);
+    if (a.maxe <= 8) return hard_launch<8, POL>(a, ncu, s);
+    return hard_launch<16, POL>(a, ncu, s);
+}
+
+hipError_t launch_rs_recover_direct(const ReconArgs& a, int ncu, hipStream_t s) {
+    return (g_tune.dec_nt & 3) ? direct_dispatch<3>(a, ncu, s) : direct_dispatch<0>(a, ncu, s);
+}
+
+}  // namespace fk

@@ -68,6 +68,17 @@ int fo_xor_reconstruct_batch(int k, size_t len, size_t nblocks,
                              uint8_t *shards, size_t bs, size_t ss,
                              const uint32_t *present_mask, int32_t *status, int threads);
 
+/* fec_simd.c: klauspost's SIMD kernel methods restated (cpu_baseline of bench.py). isa: 0 scalar,
+ * 1 avx2 (PSHUFB nibble tables), 2 gfni-avx2, 3 gfni-avx512 (VGF2P8AFFINEQB). Same arguments and
+ * results as fo_rs_encode_batch / fo_rs_reconstruct_batch; -1 if the CPU lacks the ISA. */
+int fs_best_isa(void);
+int fs_isa_supported(int isa);
+const char *fs_isa_name(int isa);
+int fs_rs_encode_batch(int k, int m, size_t len, size_t nblocks, const uint8_t *data, size_t data_bs,
+                       uint8_t *parity, size_t parity_bs, size_t ss, int threads, int isa);
+int fs_rs_reconstruct_batch(int k, int m, size_t len, size_t nblocks, uint8_t *shards, size_t bs, size_t ss,
+                            const uint32_t *present_mask, int32_t *status, int threads, int isa);
+
 #ifdef __cplusplus
 }
 #endif

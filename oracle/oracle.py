@@ -53,6 +53,13 @@ def lib():
         L.fo_rs_reconstruct_batch.argtypes = [ctypes.c_int, ctypes.c_int, sz, sz, u8p, sz, sz, u8p, u8p, ctypes.c_int]
         L.fo_xor_encode_batch.argtypes = [ctypes.c_int, sz, sz, u8p, sz, u8p, sz, sz, ctypes.c_int]
         L.fo_xor_reconstruct_batch.argtypes = [ctypes.c_int, sz, sz, u8p, sz, sz, u8p, u8p, ctypes.c_int]
+        L.fs_isa_name.restype = ctypes.c_char_p
+        L.fs_isa_name.argtypes = [ctypes.c_int]
+        L.fs_isa_supported.argtypes = [ctypes.c_int]
+        L.fs_rs_encode_batch.argtypes = [ctypes.c_int, ctypes.c_int, sz, sz, u8p, sz, u8p, sz, sz, ctypes.c_int,
+                                         ctypes.c_int]
+        L.fs_rs_reconstruct_batch.argtypes = [ctypes.c_int, ctypes.c_int, sz, sz, u8p, sz, sz, u8p, u8p, ctypes.c_int,
+                                              ctypes.c_int]
         _lib = L
     return _lib
 
@@ -102,6 +109,44 @@ def rs_reconstruct(k, m, shards, masks, threads=0, length=None):
     status = np.zeros(B, dtype=np.int32)
     lib().fo_rs_reconstruct_batch(k, m, S if length is None else length, B, _ptr(shards), n * S, S,
                                   _ptr(masks), _ptr(status), threads)
+    return status
+
+
+# ---------------------------------------------------------------- SIMD forms (fec_simd.c)
+
+ISA_SCALAR, ISA_AVX2, ISA_GFNI_AVX2, ISA_GFNI_AVX512 = 0, 1, 2, 3
+
+
+def best_isa():
+    return lib().fs_best_isa()
+
+
+def isa_supported(isa):
+    return bool(lib().fs_isa_supported(isa))
+
+
+def isa_name(isa):
+    return lib().fs_isa_name(isa).decode()
+
+
+def rs_encode_simd(k, m, shards, isa, threads=0, length=None):
+    """As rs_encode, with klauspost's SIMD kernel method (isa: ISA_*)."""
+    B, n, S = shards.shape
+    assert n == k + m and shards.flags.c_contiguous
+    base = shards.ctypes.data
+    rc = lib().fs_rs_encode_batch(k, m, S if length is None else length, B, ctypes.c_void_p(base), n * S,
+                                  ctypes.c_void_p(base + k * S), n * S, S, threads, isa)
+    assert rc == 0, "ISA %d unsupported or bad shape" % isa
+    return shards
+
+
+def rs_reconstruct_simd(k, m, shards, masks, isa, threads=0, length=None):
+    B, n, S = shards.shape
+    assert n == k + m and shards.flags.c_contiguous
+    masks = np.ascontiguousarray(masks, dtype=np.uint32)
+    status = np.zeros(B, dtype=np.int32)
+    lib().fs_rs_reconstruct_batch(k, m, S if length is None else length, B, _ptr(shards), n * S, S, _ptr(masks),
+                                  _ptr(status), threads, isa)
     return status
 
 

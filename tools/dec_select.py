@@ -1,6 +1,10 @@
 #!/usr/bin/env python3
-"""Diagnostics: pick the RS(8,12) single-erasure recover launch form by interleaved A/B in one
-process (wave vs tile reconstruct, residency caps, XCD order), many rounds."""
+"""Diagnostics: pick the single-erasure recover launch form by interleaved A/B in one process
+(plan kernel + wave rebuild vs the direct form, residency caps, XCD order), many rounds.
+Every variant's output is checked against the default's first.
+
+usage: dec_select.py [--k 8 --m 4 --blocks 1048576] [--rounds 8]"""
+import argparse
 import importlib
 import json
 import os
@@ -10,9 +14,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--m", type=int, default=4)
+    ap.add_argument("--blocks", type=int, default=1 << 20)
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=5)
+    args = ap.parse_args()
     import torch
     fec = importlib.import_module("0xfec_amd")
-    B, k, m, L, S = 1 << 20, 8, 4, 1202, 1216
+    B, k, m, L, S = args.blocks, args.k, args.m, 1202, 1216
     codec = fec.Codec(0).use_torch_stream()
     data = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device="cuda")
     par = torch.randint(0, 256, (B, m, S), dtype=torch.uint8, device="cuda")
@@ -20,35 +31,26 @@ def main():
     erased = torch.randint(0, k, (B,), device="cuda")
     masks = ((1 << (k + m)) - 1 - (1 << erased)).to(torch.int32)
     dp, pp, op = data.data_ptr(), par.data_ptr(), out.data_ptr()
-    D = dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=1, dec_ipl=0)
-    # name -> (tuning, output slots per block: the recover plans min(k, m, slots) rows). With
-    # one erasure per block only slot 0 is written, so the 4-slot runs use the same one-slot
-    # buffer (block stride S): identical stores, only the planned row count differs.
-    variants = {"wave, 1 slot": (dict(D, dec_swz=0), 1),
-                "wave, 4 slots": (dict(D, dec_swz=0), 4),
-                "wave swz, 1 slot (default)": (D, 1),
-                "wave swz, 4 slots": (D, 4),
-                "wave fused swz, 1 slot": (dict(D, dec_fused=1, dec_swz=1), 1),
-                "wave ipl2 swz, 1 slot": (dict(D, dec_ipl=2, dec_swz=1), 1)}
-    for w in (4, 5, 6):
-        variants["wave swz wpc%d, 1 slot" % w] = (dict(D, dec_swz=1, dec_wpc=w), 1)
-    for w in (0, 4, 5):
-        variants["wave swz seq2 wpc%d, 1 slot" % w] = (dict(D, dec_ipl=3, dec_wpc=w), 1)
-    # diagnostics (wrong output): every wave stages block 0's plan, an L2-resident load
-    variants["DIAG shared plan"] = (dict(D, dec_diag=1), 1)
-    variants["DIAG shared plan wpc4"] = (dict(D, dec_diag=1, dec_wpc=4), 1)
+    D = dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=1, dec_ipl=0, dec_direct=1)
+    variants = {"direct (default)": D,
+                "direct, PermTab rows by vector load": dict(D, dec_direct=2),
+                "direct noswz": dict(D, dec_swz=0),
+                "plan + wave": dict(D, dec_direct=0),
+                "plan + wave ipl2": dict(D, dec_direct=0, dec_ipl=2)}
+    for w in (4, 6):
+        variants["direct wpc%d" % w] = dict(D, dec_wpc=w)
     base = codec.set_tuning(**D)
 
-    def run(slots=1):
-        codec.rs_recover_raw(k, m, L, B, dp, k * S, pp, m * S, S, masks.data_ptr(), op, S, slots, None)
+    def run():
+        codec.rs_recover_raw(k, m, L, B, dp, k * S, pp, m * S, S, masks.data_ptr(), op, S, 1, None)
 
-    def t(slots, iters=5):
-        run(slots)
+    def t(iters):
+        run()
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         for _ in range(iters):
-            run(slots)
+            run()
         e.record()
         torch.cuda.synchronize()
         return s.elapsed_time(e) / iters / 1e3
@@ -56,20 +58,24 @@ def main():
     run()
     torch.cuda.synchronize()
     ref = out.clone()
-    for n, (kv, slots) in variants.items():
+    for n, kv in variants.items():
         codec.set_tuning(**kv)
         out.zero_()
-        run(slots)
+        run()
         torch.cuda.synchronize()
-        assert n.startswith("DIAG") or torch.equal(out, ref), n
+        assert torch.equal(out, ref), n
         codec.set_tuning(**base)
     res = {n: [] for n in variants}
-    for _ in range(8):
-        for n, (kv, slots) in variants.items():
+    for _ in range(args.rounds):
+        for n, kv in variants.items():
             codec.set_tuning(**kv)
-            res[n].append(B * (k + 1) * L / t(slots) / 1e9)
+            res[n].append(t(args.iters))
             codec.set_tuning(**base)
-    print(json.dumps({n: [round(sorted(v)[len(v) // 2], 1), round(max(v), 1)] for n, v in res.items()}))
+    byts = B * (k + 1) * L
+    print(json.dumps({"shape": "RS(%d,%d) x %d" % (k, k + m, B),
+                      "median_us_TBps_best": {n: [round(sorted(v)[len(v) // 2] * 1e6, 1),
+                                                  round(byts / sorted(v)[len(v) // 2] / 1e12, 3),
+                                                  round(byts / min(v) / 1e12, 3)] for n, v in res.items()}}))
 
 
 if __name__ == "__main__":
