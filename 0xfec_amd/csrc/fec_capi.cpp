@@ -31,6 +31,7 @@ struct Code {
     uint32_t* d_single = nullptr;  // single-erasure decode tables (fk::direct_table_words), when small
     uint32_t* d_single_coef = nullptr;   // their coefficient bytes, (k*m) rows of ceil(k/4) dwords
     std::vector<uint32_t> single_coef;   // host copy
+    uint8_t* d_dall = nullptr;     // n bytes: sum_{t != s} log(s ^ t) mod 255 (sorted plans)
 };
 
 // Parity row r, column j of a dyadic code is g(r ^ j), g = parity row 0 (fec_kernels.hip,
@@ -165,6 +166,17 @@ static int get_code(fec_ctx* ctx, int k, int m, Code** out) {
             c.single_coef = sc;
             HIP_TRY(hipMalloc(&c.d_single_coef, sc.size() * 4));
             HIP_TRY(hipMemcpy(c.d_single_coef, sc.data(), sc.size() * 4, hipMemcpyHostToDevice));
+        }
+        if (k + m <= FEC_MAX_DECODE_SHARDS) {
+            uint8_t dall[FEC_MAX_DECODE_SHARDS] = {};
+            for (int sidx = 0; sidx < k + m; ++sidx) {
+                unsigned d = 0;
+                for (int t = 0; t < k + m; ++t)
+                    if (t != sidx) d += gf::kTables.log[sidx ^ t];
+                dall[sidx] = (uint8_t)(d % 255u);
+            }
+            HIP_TRY(hipMalloc(&c.d_dall, FEC_MAX_DECODE_SHARDS));
+            HIP_TRY(hipMemcpy(c.d_dall, dall, FEC_MAX_DECODE_SHARDS, hipMemcpyHostToDevice));
         }
         const std::vector<uint8_t> leaves = dyadic_leaves(c.matrix, k, m);
         if (!leaves.empty() && leaves.size() <= (size_t)m * k) {   // staged like m x k tables
@@ -303,10 +315,14 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
     const uint32_t k = (uint32_t)code->k, m = (uint32_t)code->m;
     const uint32_t maxe = std::max<uint32_t>(1, std::min(k, m));
     const uint32_t cps = (uint32_t)((len + fk::kChunk - 1) / fk::kChunk);
-    const fk::PlanLayout lay = fk::plan_layout(k, maxe);
+    const fk::PlanLayout lay0 = fk::plan_layout(k, maxe);
     // direct form: no plan kernel (single-erasure tables of the code; multi-erasure waves plan
     // in-wave), fec_recover.hip
-    const bool direct = code->d_single && fk::direct_recon_applies(k, m, cps, lay.stride);
+    const bool direct = code->d_single && fk::direct_recon_applies(k, m, cps, lay0.stride);
+    // sorted parallel plans for the plan + wave path (fec_plan.hip)
+    const bool sorted = !direct && fk::g_tune.dec_sorted && !fk::g_tune.dec_fused && !fk::g_tune.dec_diag &&
+                        fk::wave_recon_applies(cps, k, maxe, fk::plan_layout(k, maxe, true).stride);
+    const fk::PlanLayout lay = sorted ? fk::plan_layout(k, maxe, true) : lay0;
     size_t per_launch = std::min<size_t>(direct ? nblocks : kPlanBytes / lay.stride, (size_t)(kMaxItems / cps));
     per_launch = std::max<size_t>(1, std::min(per_launch, nblocks));
     {
@@ -331,7 +347,9 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         p.maxe = maxe;
         p.lay = lay;
         p.max_out = out ? out_slots : 0;
-        if (!fused && !direct) HIP_TRY(fk::launch_rs_plan(p, ctx->stream));
+        p.dall = code->d_dall;
+        if (sorted) HIP_TRY(fk::launch_rs_plan_sorted(p, ctx->stream));
+        else if (!fused && !direct) HIP_TRY(fk::launch_rs_plan(p, ctx->stream));
         fk::ReconArgs a{};
         a.data = data + b0 * dbs;
         a.parity = parity + b0 * pbs;
@@ -352,6 +370,7 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         a.rot = fk::g_tune.rotate ? fk::line_rotation(ss, cps) : 0;
         a.swz = (uint32_t)fk::g_tune.dec_swz;
         a.diag = (uint32_t)fk::g_tune.dec_diag;
+        a.sorted = sorted ? 1u : 0u;
         a.out = out ? out + b0 * out_bs : nullptr;
         a.out_bs = out_bs;
         if (direct) {
@@ -601,6 +620,7 @@ void fec_ctx_destroy(fec_ctx* ctx) {
         if (kv.second.d_dytabs) (void)hipFree(kv.second.d_dytabs);
         if (kv.second.d_single) (void)hipFree(kv.second.d_single);
         if (kv.second.d_single_coef) (void)hipFree(kv.second.d_single_coef);
+        if (kv.second.d_dall) (void)hipFree(kv.second.d_dall);
     }
     if (ctx->d_plans) (void)hipFree(ctx->d_plans);
     if (ctx->d_hard) (void)hipFree(ctx->d_hard);
@@ -639,7 +659,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 16 ? &fk::g_tune.enc_qdepth : key == 17 ? &fk::g_tune.dec_wave
               : key == 18 ? &fk::g_tune.enc_diag : key == 19 ? &fk::g_tune.dec_fused
               : key == 20 ? &fk::g_tune.dec_ipl : key == 21 ? &fk::g_tune.dec_diag
-              : key == 22 ? &fk::g_tune.enc_dyadic : key == 23 ? &fk::g_tune.dec_direct : nullptr;
+              : key == 22 ? &fk::g_tune.enc_dyadic : key == 23 ? &fk::g_tune.dec_direct
+              : key == 24 ? &fk::g_tune.dec_sorted : key == 25 ? &fk::g_tune.dec_fixk : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

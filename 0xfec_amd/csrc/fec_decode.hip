@@ -253,7 +253,8 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
     }
 }
 
-template <int MAXE, int POL, bool FUSED, int IPL>
+// K: compile-time data shard count for the IPL = 1 body (0: runtime a.k).
+template <int MAXE, int POL, bool FUSED, int IPL, int K = 0>
 __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs a) {
     constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -297,13 +298,16 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
     }
     wave_sync();
     {
-        const uint32_t ne = nb * maxe * k;
-        for (uint32_t i = lane; i < ne; i += 64) {
-            const uint32_t g = i / (maxe * k);
-            const uint32_t rem = i - g * maxe * k;
+        // expand only the rows the blocks rebuild: entry i of c0 + c1 + c2 (c_g = nout_g * k)
+        const uint32_t c0 = plans[lay.nout_off] * k;
+        const uint32_t c1 = nb > 1 ? plans[lay.stride + lay.nout_off] * k : 0u;
+        const uint32_t c2 = nb > 2 ? plans[2 * lay.stride + lay.nout_off] * k : 0u;
+        for (uint32_t i = lane; i < c0 + c1 + c2; i += 64) {
+            const uint32_t g = (i >= c0) + (i >= c0 + c1);
+            const uint32_t rem = i - (g == 0 ? 0u : g == 1 ? c0 : c0 + c1);
             const uint32_t r = rem / k, j = rem - r * k;
             const uint8_t* P = plans + g * lay.stride;
-            if (r < P[lay.nout_off]) tabs[i] = gf::make_permtab(P[lay.coef_off + r * k + j]);
+            tabs[g * maxe * k + rem] = gf::make_permtab(P[lay.coef_off + r * k + j]);
         }
     }
     wave_sync();
@@ -318,7 +322,8 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
             const uint8_t* P = plans + g * lay.stride;
             const uint32_t nout = inr ? P[lay.nout_off] : 0;
             const uint32_t rows = wave_rows<MAXE>(nout);
-            if (nout) recon_item<MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, blk, c, rows, nout);
+            const uint32_t rb = a.sorted ? *reinterpret_cast<const uint32_t*>(P + lay.blk_off) : blk;
+            if (nout) recon_item<MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
         }
     } else if constexpr (IPL == 1) {
         const uint32_t item = i0 + lane;
@@ -330,7 +335,9 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
         const uint32_t nout = inr ? P[lay.nout_off] : 0;
         const uint32_t rows = wave_rows<MAXE>(nout);
         if (nout == 0) return;
-        recon_item<MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, blk, c, rows, nout);
+        const uint32_t rb = a.sorted ? *reinterpret_cast<const uint32_t*>(P + lay.blk_off) : blk;
+        if constexpr (K > 0) recon_item_k<K, MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
+        else recon_item<MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
     } else {
         const uint32_t itA = i0 + lane, itB = itA + 64;
         const bool inA = itA < total, inB = itB < total;
@@ -341,8 +348,10 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
         const uint32_t nA = inA ? PA[lay.nout_off] : 0, nB = inB ? PB[lay.nout_off] : 0;
         const uint32_t rA = wave_rows<MAXE>(nA), rB = wave_rows<MAXE>(nB);
         if ((nA | nB) == 0) return;
-        recon_pair<MAXE, NTL, NTS>(a, PA, tabs + (bA - bfirst) * maxe * k, bA, itA - bA * a.cps, rA, nA, PB,
-                                   tabs + (bB - bfirst) * maxe * k, bB, itB - bB * a.cps, rB, nB);
+        const uint32_t rbA = a.sorted ? *reinterpret_cast<const uint32_t*>(PA + lay.blk_off) : bA;
+        const uint32_t rbB = a.sorted ? *reinterpret_cast<const uint32_t*>(PB + lay.blk_off) : bB;
+        recon_pair<MAXE, NTL, NTS>(a, PA, tabs + (bA - bfirst) * maxe * k, rbA, itA - bA * a.cps, rA, nA, PB,
+                                   tabs + (bB - bfirst) * maxe * k, rbB, itB - bB * a.cps, rB, nB);
     }
 }
 
@@ -389,6 +398,14 @@ static hipError_t recon_wave_dispatch(const ReconArgs& a, hipStream_t s) {
     const size_t lds = occupancy_lds(g_tune.dec_wpc, own);
 #define FEC_WAVE_LAUNCH(E) \
     hipLaunchKernelGGL((rs_reconstruct_wave_kernel<E, POL, FUSED, IPL>), dim3(grid), dim3(kThreads), lds, s, a)
+    // the benchmark's multi-erasure code RS(16,24) with its K known at compile time
+    if constexpr (IPL == 1 && !FUSED) {
+        if (a.k == 16 && a.maxe == 8 && g_tune.dec_fixk) {
+            hipLaunchKernelGGL((rs_reconstruct_wave_kernel<8, POL, false, 1, 16>), dim3(grid), dim3(kThreads), lds,
+                               s, a);
+            return hipGetLastError();
+        }
+    }
     if (a.maxe <= 1) FEC_WAVE_LAUNCH(1);
     else if (a.maxe <= 2) FEC_WAVE_LAUNCH(2);
     else if (a.maxe <= 4) FEC_WAVE_LAUNCH(4);

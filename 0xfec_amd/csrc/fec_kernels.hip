@@ -34,12 +34,13 @@ FastDiv make_fastdiv(uint32_t d) {
     return f;
 }
 
-PlanLayout plan_layout(uint32_t k, uint32_t maxe) {
+PlanLayout plan_layout(uint32_t k, uint32_t maxe, bool sorted) {
     PlanLayout l;
     l.in_off = 0;
     l.out_off = (k + 7) & ~7u;                       // in slots, read 8 at a time
     l.nout_off = l.out_off + maxe;
-    l.coef_off = (l.nout_off + 1 + 3) & ~3u;
+    l.blk_off = sorted ? (l.nout_off + 1 + 3) & ~3u : 0;
+    l.coef_off = sorted ? l.blk_off + 4 : (l.nout_off + 1 + 3) & ~3u;
     l.stride = (l.coef_off + maxe * k + 15) & ~15u;
     return l;
 }

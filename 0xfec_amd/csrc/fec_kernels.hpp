@@ -49,10 +49,12 @@ constexpr int kCtrWords = 9 * kCtrStride;
 //   [out_off,  +maxe)     erased data shard slots (ascending)
 //   [nout_off]            number of erased data shards to rebuild (0: nothing / failed)
 //   [coef_off, +maxe*k)   GF coefficients, row r = output r, column j = input j
+//   [blk_off,  +4)        sorted plans only: the block the record belongs to (uint32)
 struct PlanLayout {
     uint32_t in_off, out_off, nout_off, coef_off, stride;
+    uint32_t blk_off;          // 0: records are in block order (no block field)
 };
-PlanLayout plan_layout(uint32_t k, uint32_t maxe);
+PlanLayout plan_layout(uint32_t k, uint32_t maxe, bool sorted = false);
 
 struct PlanArgs {
     const uint32_t* masks;
@@ -63,7 +65,15 @@ struct PlanArgs {
     uint32_t k, m, nblocks, maxe;
     PlanLayout lay;
     uint32_t max_out;          // recover: output slots per block (0: in place, unlimited)
+    const uint8_t* dall;       // sorted plans: per shard index s < n, sum_{t < n, t != s} log(s ^ t) mod 255
 };
+
+// Sorted plans (fec_plan.hip): lanes per block and blocks per 256-thread workgroup for k.
+inline uint32_t plan_lanes(uint32_t k) {
+    uint32_t l = 2;
+    while (l < k) l <<= 1;
+    return l;
+}
 
 struct ReconArgs {
     uint8_t* data;             // data shard 0 of block 0 (rebuilt shards are written here)
@@ -81,6 +91,7 @@ struct ReconArgs {
     uint64_t out_bs;           //          (nullptr: rebuild in place into the data region)
     uint32_t swz;
     uint32_t diag;             // diagnostics (knob dec_diag): every wave stages block 0's plan (wrong output)
+    uint32_t sorted;           // plans from rs_plan_sorted_kernel: the block of a record is its blk field
     // fused form (plans built in the reconstruct kernel, no rs_plan_kernel): as PlanArgs
     const uint32_t* masks;
     int32_t* status;
@@ -143,6 +154,8 @@ struct Tuning {
     int dec_direct = 1;       // single-erasure codes with small tables: no plan kernel, per-lane table
                               // lookup (1: rows expanded from scalar-loaded coefficients, 2: PermTab rows
                               // copied by a vector load); multi-erasure waves go to a worklist kernel
+    int dec_fixk = 1;         // RS(16,24) rebuild with k = 16 at compile time (all 16 loads in flight)
+    int dec_sorted = 1;       // multi-erasure codes (plan path, shards of 32+ chunks): sorted parallel plans
     int dec_ipl = 0;          // wave-form reconstruct items per lane: 1; 2 loaded together; 3: 2 one
                               // after the other (one plan stage); 0: 2 for k <= 4, else 1
 };
@@ -170,6 +183,11 @@ hipError_t launch_rs_encode(const EncodeArgs& a, int grid, hipStream_t s);
 bool fixed_encode_applies(uint32_t k, uint32_t m);
 hipError_t launch_rs_encode_fixed(EncodeArgs a, int ncu, hipStream_t s);
 hipError_t launch_rs_plan(const PlanArgs& a, hipStream_t s);
+// Sorted plans (fec_plan.hip): lanes of a wave cooperate on one block's plan; within each
+// workgroup's segment of blocks the records are stored ordered by erasure count, each naming
+// its block (layout from plan_layout(k, maxe, true)), so a rebuild wave meets blocks of equal
+// row counts.
+hipError_t launch_rs_plan_sorted(const PlanArgs& a, hipStream_t s);
 hipError_t launch_rs_reconstruct(const ReconArgs& a, int grid, hipStream_t s);
 bool wave_recon_applies(uint32_t cps, uint32_t k, uint32_t maxe, uint32_t stride);
 hipError_t launch_rs_reconstruct_wave(const ReconArgs& a, hipStream_t s);

@@ -61,6 +61,76 @@ __device__ __forceinline__ void recon_item(const ReconArgs& a, const uint8_t* P,
                              nb, a.pad_zero);
 }
 
+// recon_item with the data shard count K known at compile time: all K input loads are issued
+// before any is folded (the runtime-k form issues them 8 at a time, and the second group's
+// loads wait for the first group's arithmetic), and the wave-uniform row count selects a
+// straight-line body per count (per-row branches inside the fold make the compiler copy the
+// accumulators through every branch).
+template <int K, int ROWS, bool NTS>
+__device__ __forceinline__ void recon_rows_k(const ReconArgs& a, const uint8_t* P, const gf::PermTab* T,
+                                             const uint4 (&x)[K], uint8_t* dblk, uint8_t* oblk, uint32_t c,
+                                             uint32_t nout) {
+    uint32_t acc[ROWS][4];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0;
+#pragma unroll
+    for (int j = 0; j < K; j += 2) {
+        // opaque zero per input pair: keeps the table reads next to their use (hoisted, every
+        // pair's tables would be held at once)
+        uint32_t toff = 0;
+        asm volatile("" : "+s"(toff));
+        const gf::PermTab* t = T + toff;
+        // the pair's inputs pass through an opaque step here, so their splits are not hoisted
+        // ahead of earlier pairs (all splits at once would hold 3 words per input dword)
+        uint4 xa = x[j], xb = x[j + 1];
+        asm volatile("" : "+v"(xa.x), "+v"(xa.y), "+v"(xa.z), "+v"(xa.w), "+v"(xb.x), "+v"(xb.y), "+v"(xb.z), "+v"(xb.w));
+        Idx ia[4], ib[4];
+        split4(ia, xa);
+        split4(ib, xb);
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) mac2(acc[r], ia, ib, t + r * K + j, t + r * K + j + 1);
+    }
+    const uint32_t nb = a.len - c * kChunk;
+    const uint8_t* out_idx = P + a.lay.out_off;
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r)
+        if (r < (int)nout)
+            store_chunk<NTS>(oblk ? oblk + (uint64_t)r * a.ss : dblk + (uint64_t)out_idx[r] * a.ss, as_uint4(acc[r]),
+                             nb, a.pad_zero);
+}
+
+template <int K, int MAXE, bool NTL, bool NTS>
+__device__ __forceinline__ void recon_item_k(const ReconArgs& a, const uint8_t* P, const gf::PermTab* T,
+                                             uint32_t blk, uint32_t c, uint32_t rows, uint32_t nout) {
+    static_assert(K % 8 == 0, "slot words are read 8 at a time");
+    const PlanLayout& lay = a.lay;
+    uint8_t* dblk = a.data + (uint64_t)blk * a.dbs + (uint64_t)c * kChunk;
+    const uint8_t* pblk = a.parity + (uint64_t)blk * a.pbs + (uint64_t)c * kChunk;
+    uint4 x[K];
+#pragma unroll
+    for (int j0 = 0; j0 < K; j0 += 8) {
+        const uint2 sl = *reinterpret_cast<const uint2*>(P + lay.in_off + j0);
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+            const uint32_t slot = ((jj < 4 ? sl.x : sl.y) >> (8 * (jj & 3))) & 0xFFu;
+            x[j0 + jj] = ld16<NTL>(slot < (uint32_t)K ? dblk + (uint64_t)slot * a.ss
+                                                      : pblk + (uint64_t)(slot - K) * a.ss);
+        }
+    }
+    uint8_t* oblk = a.out ? a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk : nullptr;
+    static_assert(MAXE <= 8, "row bodies 1..8");
+    switch (rows) {   // wave-uniform
+        case 1: recon_rows_k<K, 1, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 2: recon_rows_k<K, 2, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 3: recon_rows_k<K, 3, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 4: recon_rows_k<K, 4, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 5: if constexpr (MAXE >= 5) recon_rows_k<K, 5, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 6: if constexpr (MAXE >= 6) recon_rows_k<K, 6, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 7: if constexpr (MAXE >= 7) recon_rows_k<K, 7, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+        default: if constexpr (MAXE >= 8) recon_rows_k<K, 8, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+    }
+}
+
 template <int MAXE>
 __device__ __forceinline__ uint32_t wave_rows(uint32_t nout) {
     uint32_t rows = 0;

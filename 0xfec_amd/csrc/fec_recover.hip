@@ -84,6 +84,7 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
     // Per block (uniform): status (recover: e rebuilt; in place: 0) and failures, as
     // rs_plan_kernel reports them, and the table row (E0 * m + R0) of a single-erasure block.
     uint32_t row[kWaveBlocks] = {0, 0, 0};
+    int32_t stg[kWaveBlocks] = {0, 0, 0};
 #pragma unroll
     for (uint32_t g = 0; g < kWaveBlocks; ++g) {
         if (g >= nb) break;
@@ -99,8 +100,13 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
         } else if (e == 1) {
             row[g] = (__ffs(~mask & kmask) - 1) * m + (__ffs(mask >> k) - 1);   // m >= 1 here: k < 32
         }
-        if (lane == 0 && a.status) a.status[bfirst + g] = st;
+        stg[g] = st;
     }
+    // statuses: lane g < nb writes block g's, one store, issued after the data loads (a store
+    // before them would make the loads wait for its completion)
+    auto store_status = [&]() {
+        if (a.status && lane < nb) a.status[bfirst + lane] = lane == 0 ? stg[0] : lane == 1 ? stg[1] : stg[2];
+    };
     // The PermTab rows of the wave's blocks into its LDS slice, prepared while the data loads are
     // in flight (vector loads return in order: LDS writes that wait for a row load wait for that
     // load only, and scalar loads are counted apart).
@@ -178,6 +184,7 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
 #pragma unroll
         for (int j = 0; j < K - 1; ++j) x[j] = ld16<NTL>(d0 + (uint64_t)(j + (j >= (int)E0)) * ss);
         x[K - 1] = ld16<NTL>(p0);
+        store_status();
         if constexpr (TAB == 0) rows_to_lds(wt, tv, lane, nb * 2 * k);
         else expand_rows();
         if (!work) return;
@@ -193,6 +200,7 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
             }
         }
     } else {
+        store_status();
         if constexpr (TAB == 0) rows_to_lds(wt, tv, lane, nb * 2 * k);
         else expand_rows();
         if (!work) return;

@@ -21,7 +21,7 @@
 
 namespace gf {
 
-struct Tables {
+struct alignas(16) Tables {   // aligned: kernels stage exp | log into LDS as dwords
     uint8_t exp[512];
     uint8_t log[256];
 };

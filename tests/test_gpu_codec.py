@@ -331,8 +331,9 @@ def test_rs_encode_kernel_variants_match_oracle(codec, oracle, torch, variant, k
 # wave 2: plans built in-kernel; 3, 4: as 1, 2 with two items per lane loaded together (shards
 # of 64+ chunks, at most 4 erasures per block); 5, 6: as 1, 2 with two items one after the other;
 # 7: the direct form (fec_recover.hip: single-erasure tables, in-wave plans for waves holding a
-# multi-erasure block) where the code's tables fit, else as 1
-@pytest.mark.parametrize("wave", [0, 1, 2, 3, 4, 5, 6, 7])
+# multi-erasure block) where the code's tables fit, else as 1; 1, 3, 5 use the sorted parallel
+# plans (fec_plan.hip), 8 is 1 with the one-lane-per-block plan kernel in block order
+@pytest.mark.parametrize("wave", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10)])
 @pytest.mark.parametrize("L", [513, 1202, 1436])
 def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, wave, k, m, L):
@@ -350,7 +351,8 @@ def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, 
     par = torch.from_numpy(np.ascontiguousarray(sh[:, k:])).cuda()
     dm = torch.from_numpy(masks.view(np.int32)).cuda()
     old = codec.set_tuning(dec_wave=1 if wave else 0, dec_fused=1 if wave in (2, 4, 6) else 0,
-                           dec_ipl={3: 2, 4: 2, 5: 3, 6: 3}.get(wave, 1), dec_direct=1 if wave == 7 else 0)
+                           dec_ipl={3: 2, 4: 2, 5: 3, 6: 3}.get(wave, 1), dec_direct=1 if wave == 7 else 0,
+                           dec_sorted=0 if wave == 8 else 1)
     try:
         out = torch.full((B, m, S), 0xEE, dtype=torch.uint8, device="cuda")
         data = torch.from_numpy(data_np).cuda()

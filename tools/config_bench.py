@@ -67,11 +67,18 @@ def run_rs(torch, fec, codec, k, m, B, multi, iters, seed):
     out = torch.zeros((B, max(slots, 1), S), dtype=torch.uint8, device="cuda")
     status = torch.zeros((B,), dtype=torch.int32, device="cuda")
 
+    # raw C-ABI calls with the arguments precomputed: the shapes whose launches take tens of
+    # microseconds (RS(2,3)) are otherwise timed at the Python call rate, not the device's
+    dp, pp, op, mp, sp = data.data_ptr(), parity.data_ptr(), out.data_ptr(), masks.data_ptr(), status.data_ptr()
+    slots_ = out.shape[1]
+
     def enc():
-        codec.rs_encode_split(k, m, data, parity, shard_len=L)
+        codec.rs_encode_raw(k, m, L, B, dp, k * S, pp, m * S, S, fec.FEC_DEVICE)
 
     def dec():
-        codec.rs_recover_split(k, m, data, parity, masks, out, status=status, shard_len=L)
+        rc = codec.rs_recover_raw(k, m, L, B, dp, k * S, pp, m * S, S, mp, op, slots_ * S, slots_, sp)
+        if rc:
+            raise fec.FecError(rc, "recover")
 
     enc()
     dec()
@@ -111,11 +118,19 @@ def run_xor(torch, fec, codec, k, B, iters, seed):
     masks = (((1 << (k + 1)) - 1) - torch.bitwise_left_shift(torch.ones_like(which), which)).to(torch.int32)
     ref = None
 
+    shp, mp = sh.data_ptr(), masks.data_ptr()
+    n = k + 1
+
     def enc():
-        codec.xor_encode(k, sh, shard_len=L)
+        rc = fec.lib.fec_xor_encode_batch(codec.handle, k, L, B, shp, n * S, shp + k * S, n * S, S, fec.FEC_DEVICE)
+        if rc:
+            raise fec.FecError(rc, "xor encode")
 
     def dec():
-        codec.xor_reconstruct(k, sh, masks, shard_len=L)
+        rc = fec.lib.fec_xor_reconstruct_batch(codec.handle, k, L, B, shp, n * S, shp + k * S, n * S, S, mp, None,
+                                               fec.FEC_DEVICE)
+        if rc:
+            raise fec.FecError(rc, "xor reconstruct")
 
     enc()
     codec.sync()
