@@ -43,6 +43,7 @@ FEC_ERR_NOMEM = -9
 FEC_ERR_NO_DEVICE = -10
 FEC_DEVICE = 0
 FEC_HOST = 1
+FEC_HOST_PINNED = 2
 FEC_MAX_DECODE_SHARDS = 32
 
 _vp = ctypes.c_void_p
@@ -112,7 +113,9 @@ def _addr(x):
     if mod.startswith("numpy"):
         return x.ctypes.data, FEC_HOST
     if mod.startswith("torch"):
-        return x.data_ptr(), (FEC_DEVICE if x.is_cuda else FEC_HOST)
+        if x.is_cuda:
+            return x.data_ptr(), FEC_DEVICE
+        return x.data_ptr(), (FEC_HOST_PINNED if x.is_pinned() else FEC_HOST)
     raise TypeError("unsupported buffer type %r" % type(x))
 
 
@@ -127,8 +130,9 @@ def _shape3(shards):
 
 class Codec:
     """One device context (one HIP stream). Batch entry points over [B, n, S] uint8 arrays:
-    numpy arrays run the FEC_HOST path (staged through pinned memory), CUDA tensors the
-    FEC_DEVICE path (asynchronous on the ctx stream; call sync())."""
+    numpy arrays and pageable CPU tensors run the FEC_HOST path (staged through pinned memory),
+    pinned CPU tensors the FEC_HOST_PINNED path (direct DMA), CUDA tensors the FEC_DEVICE path
+    (asynchronous on the ctx stream; call sync())."""
 
     def __init__(self, device=0):
         h = _vp()
@@ -182,7 +186,7 @@ class Codec:
                    "items_per_thread": 5, "tiles_per_wg": 6, "rotate": 7, "xcd_swz": 8, "enc_wpc": 9,
                    "dec_wpc": 10, "enc_fixed": 11, "dec_swz": 12, "gen_wpc": 13, "enc_queue": 14,
                    "enc_qwpc": 15, "enc_qdepth": 16, "dec_wave": 17, "enc_diag": 18, "dec_fused": 19, "dec_ipl": 20, "dec_diag": 21,
-                   "enc_dyadic": 22, "dec_direct": 23, "dec_sorted": 24, "dec_fixk": 25}
+                   "enc_dyadic": 22, "dec_direct": 23, "dec_sorted": 24, "dec_fixk": 25, "host_chunk": 26}
 
     def set_tuning(self, **knobs):
         """Set kernel-selection knobs; returns the previous values (pass them back to restore)."""
@@ -227,7 +231,7 @@ class Codec:
 
     def _recon(self, fn, what, k, m, B, S, d, dbs, p, pbs, kind, masks, status, shard_len):
         ma, mkind = _addr(masks)
-        assert mkind == kind, "masks must live where the shards live"
+        assert (mkind == FEC_DEVICE) == (kind == FEC_DEVICE), "masks must live where the shards live"
         sa = _addr(status)[0] if status is not None else None
         L = S if shard_len is None else shard_len
         rc = fn(B, L, d, dbs, p, pbs, S, ma, sa, kind)

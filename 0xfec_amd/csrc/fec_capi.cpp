@@ -72,6 +72,22 @@ constexpr uint64_t kMaxItems = uint64_t(1) << 31;
 
 }  // namespace
 
+// One staging set of the host-resident path (pinned host + device buffers, a stream, an event):
+// with two, chunk c+1 is staged and copied up while chunk c is coded and copied down.
+struct HostSet {
+    uint8_t* h_in = nullptr;
+    uint8_t* h_out = nullptr;
+    uint8_t* d_in = nullptr;
+    uint8_t* d_out = nullptr;
+    uint32_t* h_masks = nullptr;
+    uint32_t* d_masks = nullptr;
+    int32_t* h_status = nullptr;
+    int32_t* d_status = nullptr;
+    size_t in_cap = 0, out_cap = 0, blk_cap = 0;
+    hipStream_t s = nullptr;
+    hipEvent_t done = nullptr;
+};
+
 struct fec_ctx {
     int device = 0;
     hipStream_t own = nullptr;
@@ -91,6 +107,7 @@ struct fec_ctx {
     size_t masks_cap = 0;
     int grid_cache[3][6] = {};
     int ncu = 256;           // compute units of the device
+    HostSet hs[2];           // host-resident path: two staging sets, each with its own stream
 };
 
 #define HIP_TRY(expr)                      \
@@ -311,7 +328,8 @@ static int rs_encode_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks
 static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks, uint8_t* data,
                                  size_t dbs, const uint8_t* parity, size_t pbs, size_t ss, const uint32_t* masks,
                                  int32_t* status, int* err, uint8_t* out = nullptr, size_t out_bs = 0,
-                                 uint32_t out_slots = 0) {
+                                 uint32_t out_slots = 0, size_t pss = 0) {
+    if (pss == 0) pss = ss;
     const uint32_t k = (uint32_t)code->k, m = (uint32_t)code->m;
     const uint32_t maxe = std::max<uint32_t>(1, std::min(k, m));
     const uint32_t cps = (uint32_t)((len + fk::kChunk - 1) / fk::kChunk);
@@ -356,6 +374,7 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         a.dbs = dbs;
         a.pbs = pbs;
         a.ss = ss;
+        a.pss = pss;
         a.plans = ctx->d_plans;
         a.k = k;
         a.len = (uint32_t)len;
@@ -483,48 +502,269 @@ static int check_device_layout(const void* p, size_t bs, size_t ss, size_t len) 
     return FEC_OK;
 }
 
-// Blocks per FEC_HOST chunk for `slots` staged shard slots per block of `ssd` bytes.
-static size_t host_chunk_blocks(size_t slots, size_t ssd) {
-    const size_t per_block = slots * ssd;
-    return std::max<size_t>(1, kStageBytes / per_block);
+// ---------------------------------------------------------------- host-resident path
+// FEC_HOST (pageable host memory): each chunk of blocks is staged by the calling thread into a
+// pinned buffer, copied up with one hipMemcpyAsync, coded, copied down with one, and its results
+// copied out once the set comes round again. FEC_HOST_PINNED (the caller's buffers are pinned or
+// registered): no staging copies at all; each shard column is moved with one 2D hipMemcpyAsync
+// straight between the caller's layout and the device staging. Only what the code needs crosses
+// PCIe: encode sends the k data shards and returns the m parity shards; reconstruct sends the data
+// shards and the parity planes up to the highest parity any block of the chunk reads, and
+// returns only the rebuilt shards. Two staging sets alternate on two streams, so the staging
+// copies and PCIe transfers of one chunk overlap the kernels of the other.
+
+static size_t host_chunk_blocks(size_t bytes_per_block) {
+    if (fk::g_tune.host_chunk > 0) return (size_t)fk::g_tune.host_chunk;   // tests: many small chunks
+    return std::max<size_t>(1, kStageBytes / std::max<size_t>(1, bytes_per_block));
 }
 
-// FEC_HOST reconstruct (RS when code != nullptr, else XOR(k,1)): stage the present shards of
-// each chunk of blocks into pinned memory as [block][n][ssd], run the device path, copy the
-// rebuilt data shards back.
-static int host_reconstruct(fec_ctx* ctx, Code* code, int k, int m, size_t len, size_t nblocks, uint8_t* data,
-                            size_t dbs, const uint8_t* parity, size_t pbs, size_t ss, const uint32_t* masks,
-                            int32_t* block_status) {
+static int host_set_grow(fec_ctx* ctx, HostSet& s, size_t in_bytes, size_t out_bytes, size_t blocks) {
+    if (!s.s) {
+        HIP_TRY(hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    }
+    if (in_bytes > s.in_cap) {
+        if (s.h_in) HIP_TRY(hipHostFree(s.h_in));
+        if (s.d_in) HIP_TRY(hipFree(s.d_in));
+        s.h_in = s.d_in = nullptr;
+        s.in_cap = 0;
+        HIP_TRY(hipHostMalloc(&s.h_in, in_bytes, hipHostMallocDefault));
+        HIP_TRY(hipMalloc(&s.d_in, in_bytes));
+        s.in_cap = in_bytes;
+    }
+    if (out_bytes > s.out_cap) {
+        if (s.h_out) HIP_TRY(hipHostFree(s.h_out));
+        if (s.d_out) HIP_TRY(hipFree(s.d_out));
+        s.h_out = s.d_out = nullptr;
+        s.out_cap = 0;
+        HIP_TRY(hipHostMalloc(&s.h_out, out_bytes, hipHostMallocDefault));
+        HIP_TRY(hipMalloc(&s.d_out, out_bytes));
+        s.out_cap = out_bytes;
+    }
+    if (blocks > s.blk_cap) {
+        for (void* q : {(void*)s.h_masks, (void*)s.h_status})
+            if (q) HIP_TRY(hipHostFree(q));
+        for (void* q : {(void*)s.d_masks, (void*)s.d_status})
+            if (q) HIP_TRY(hipFree(q));
+        s.h_masks = s.d_masks = nullptr;
+        s.h_status = s.d_status = nullptr;
+        s.blk_cap = 0;
+        HIP_TRY(hipHostMalloc(&s.h_masks, blocks * 4, hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(&s.h_status, blocks * 4, hipHostMallocDefault));
+        HIP_TRY(hipMalloc(&s.d_masks, blocks * 4));
+        HIP_TRY(hipMalloc(&s.d_status, blocks * 4));
+        s.blk_cap = blocks;
+    }
+    (void)ctx;
+    return FEC_OK;
+}
+
+// Run `fn` with the ctx's kernels enqueued on `s` (the host path's set stream).
+template <class F>
+static int on_stream(fec_ctx* ctx, hipStream_t s, F fn) {
+    hipStream_t keep = ctx->stream;
+    ctx->stream = s;
+    const int rc = fn();
+    ctx->stream = keep;
+    return rc;
+}
+
+// Column j of a chunk: nb rows of len bytes, host pitch hp, device pitch dp.
+static int copy_cols(void* dst, size_t dpitch, const void* src, size_t spitch, size_t len, size_t rows,
+                     hipMemcpyKind kind, hipStream_t s) {
+    HIP_TRY(hipMemcpy2DAsync(dst, dpitch, src, spitch, len, rows, kind, s));
+    return FEC_OK;
+}
+
+// Encode (RS when code != nullptr, else XOR(k, 1)): host data -> host parity.
+static int host_encode(fec_ctx* ctx, Code* code, int k, int m, size_t len, size_t nblocks, const uint8_t* data,
+                       size_t dbs, uint8_t* parity, size_t pbs, size_t ss, bool pinned) {
+    const size_t ssd = round16(len);
+    const size_t chunk = std::min(nblocks, host_chunk_blocks((size_t)k * ssd));
+    struct Pending {
+        size_t b0 = 0, nb = 0;
+        bool live = false;
+    } pend[2];
+    int rc;
+    auto finish = [&](int i) -> int {
+        HostSet& s = ctx->hs[i];
+        HIP_TRY(hipEventSynchronize(s.done));
+        if (!pinned)
+            for (size_t b = 0; b < pend[i].nb; ++b)
+                for (int r = 0; r < m; ++r)
+                    memcpy(parity + (pend[i].b0 + b) * pbs + r * ss, s.h_out + (b * m + r) * ssd, len);
+        pend[i].live = false;
+        return FEC_OK;
+    };
+    size_t c = 0;
+    for (size_t b0 = 0; b0 < nblocks; b0 += chunk, ++c) {
+        const int i = (int)(c & 1);
+        const size_t nb = std::min(chunk, nblocks - b0);
+        if (pend[i].live && (rc = finish(i))) return rc;
+        HostSet& s = ctx->hs[i];
+        if ((rc = host_set_grow(ctx, s, chunk * k * ssd, chunk * m * ssd, 1))) return rc;
+        if (pinned) {
+            for (int j = 0; j < k; ++j)
+                if ((rc = copy_cols(s.d_in + j * ssd, (size_t)k * ssd, data + b0 * dbs + j * ss, dbs, len, nb,
+                                    hipMemcpyHostToDevice, s.s)))
+                    return rc;
+        } else {
+            for (size_t b = 0; b < nb; ++b)
+                for (int j = 0; j < k; ++j) memcpy(s.h_in + (b * k + j) * ssd, data + (b0 + b) * dbs + j * ss, len);
+            HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, nb * k * ssd, hipMemcpyHostToDevice, s.s));
+        }
+        rc = on_stream(ctx, s.s, [&] {
+            return code ? rs_encode_device(ctx, code, len, nb, s.d_in, (size_t)k * ssd, s.d_out, (size_t)m * ssd, ssd)
+                        : xor_encode_device(ctx, k, len, nb, s.d_in, (size_t)k * ssd, s.d_out, ssd, ssd);
+        });
+        if (rc) return rc;
+        if (pinned) {
+            for (int r = 0; r < m; ++r)
+                if ((rc = copy_cols(parity + b0 * pbs + r * ss, pbs, s.d_out + r * ssd, (size_t)m * ssd, len, nb,
+                                    hipMemcpyDeviceToHost, s.s)))
+                    return rc;
+        } else {
+            HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, nb * m * ssd, hipMemcpyDeviceToHost, s.s));
+        }
+        HIP_TRY(hipEventRecord(s.done, s.s));
+        pend[i] = {b0, nb, true};
+    }
+    for (size_t t = 0; t < 2; ++t) {   // older chunk first
+        const int i = (int)((c + t) & 1);
+        if (pend[i].live && (rc = finish(i))) return rc;
+    }
+    return FEC_OK;
+}
+
+// RS reconstruct, in place in the caller's data slots: per chunk, the data shards and the parity
+// planes [0, P) (P = 1 + the highest parity index any block of the chunk reads among its first k
+// present shards) go up; the recover kernel rebuilds each block's erased data shards into
+// [block][slot] outputs (slots = the chunk's largest erasure count); only those come down and are
+// scattered into the erased slots.
+static int host_reconstruct_rs(fec_ctx* ctx, Code* code, int k, int m, size_t len, size_t nblocks, uint8_t* data,
+                               size_t dbs, const uint8_t* parity, size_t pbs, size_t ss, const uint32_t* masks,
+                               int32_t* block_status, bool pinned) {
     const size_t ssd = round16(len);
     const size_t n = (size_t)k + m;
-    const uint32_t all = fk::low_mask((uint32_t)n);
-    const uint32_t kmask = fk::low_mask((uint32_t)k);
-    const size_t chunk = host_chunk_blocks(n, ssd);
+    const uint32_t all = fk::low_mask((uint32_t)n), kmask = fk::low_mask((uint32_t)k);
+    const size_t maxe = (size_t)std::max(1, std::min(k, m));
+    const size_t chunk = std::min(nblocks, host_chunk_blocks(n * ssd));
+    struct Pending {
+        size_t b0 = 0, nb = 0, slots = 0;
+        bool live = false;
+    } pend[2];
+    bool failed = false;
     int rc;
-    if ((rc = grow_stage(ctx, std::min(chunk, nblocks) * n * ssd))) return rc;
-    if ((rc = grow_masks(ctx, std::min(chunk, nblocks)))) return rc;
+    auto finish = [&](int i) -> int {
+        HostSet& s = ctx->hs[i];
+        HIP_TRY(hipEventSynchronize(s.done));
+        for (size_t b = 0; b < pend[i].nb; ++b) {
+            const int32_t st = s.h_status[b];
+            if (block_status) block_status[pend[i].b0 + b] = st < 0 ? st : 0;
+            if (st < 0) {
+                failed = true;
+                continue;
+            }
+            const uint32_t mask = s.h_masks[b];
+            for (int j = 0, r = 0; j < k && r < st; ++j)
+                if (!((mask >> j) & 1u))
+                    memcpy(data + (pend[i].b0 + b) * dbs + j * ss, s.h_out + (b * pend[i].slots + r++) * ssd, len);
+        }
+        pend[i].live = false;
+        return FEC_OK;
+    };
+    size_t c = 0;
+    for (size_t b0 = 0; b0 < nblocks; b0 += chunk, ++c) {
+        const int i = (int)(c & 1);
+        const size_t nb = std::min(chunk, nblocks - b0);
+        if (pend[i].live && (rc = finish(i))) return rc;
+        HostSet& s = ctx->hs[i];
+        if ((rc = host_set_grow(ctx, s, chunk * n * ssd, chunk * maxe * ssd, chunk))) return rc;
+        // per block: the parity planes its first k present shards reach, its erasure count
+        size_t P = 0, slots = 1;
+        for (size_t b = 0; b < nb; ++b) {
+            const uint32_t mask = masks[b0 + b] & all;
+            s.h_masks[b] = mask;
+            const uint32_t e = (uint32_t)k - (uint32_t)__builtin_popcount(mask & kmask);
+            if (e == 0 || (uint32_t)__builtin_popcount(mask) < (uint32_t)k) continue;
+            uint32_t need = e;   // parities among the first k present: the first e present ones
+            for (int r = 0; r < m && need; ++r)
+                if ((mask >> (k + r)) & 1u) {
+                    --need;
+                    P = std::max(P, (size_t)r + 1);
+                }
+            slots = std::max(slots, (size_t)e);
+        }
+        uint8_t* d_par = s.d_in + nb * k * ssd;   // parity planes [P][nb][ssd]
+        if (pinned) {
+            for (int j = 0; j < k; ++j)
+                if ((rc = copy_cols(s.d_in + j * ssd, (size_t)k * ssd, data + b0 * dbs + j * ss, dbs, len, nb,
+                                    hipMemcpyHostToDevice, s.s)))
+                    return rc;
+            for (size_t r = 0; r < P; ++r)
+                if ((rc = copy_cols(d_par + r * nb * ssd, ssd, parity + b0 * pbs + r * ss, pbs, len, nb,
+                                    hipMemcpyHostToDevice, s.s)))
+                    return rc;
+        } else {
+            for (size_t b = 0; b < nb; ++b) {
+                const uint32_t mask = s.h_masks[b];
+                if ((mask & kmask) == kmask) continue;   // nothing to rebuild: nothing read
+                for (int j = 0; j < k; ++j)
+                    if ((mask >> j) & 1u) memcpy(s.h_in + (b * k + j) * ssd, data + (b0 + b) * dbs + j * ss, len);
+                for (size_t r = 0; r < P; ++r)
+                    if ((mask >> (k + r)) & 1u)
+                        memcpy(s.h_in + nb * k * ssd + (r * nb + b) * ssd, parity + (b0 + b) * pbs + r * ss, len);
+            }
+            HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, (nb * k + P * nb) * ssd, hipMemcpyHostToDevice, s.s));
+        }
+        HIP_TRY(hipMemcpyAsync(s.d_masks, s.h_masks, nb * 4, hipMemcpyHostToDevice, s.s));
+        rc = on_stream(ctx, s.s, [&] {
+            return rs_reconstruct_device(ctx, code, len, nb, s.d_in, (size_t)k * ssd, d_par, ssd, ssd, s.d_masks,
+                                         s.d_status, ctx->d_err + 1, s.d_out, slots * ssd, (uint32_t)slots, nb * ssd);
+        });
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, nb * slots * ssd, hipMemcpyDeviceToHost, s.s));
+        HIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, nb * 4, hipMemcpyDeviceToHost, s.s));
+        HIP_TRY(hipEventRecord(s.done, s.s));
+        pend[i] = {b0, nb, slots, true};
+    }
+    for (size_t t = 0; t < 2; ++t) {
+        const int i = (int)((c + t) & 1);
+        if (pend[i].live && (rc = finish(i))) return rc;
+    }
+    // the sticky device word of the host path is not used: statuses say it all
+    return failed ? FEC_ERR_TOO_FEW_SHARDS : FEC_OK;
+}
+
+// FEC_HOST XOR(k,1) reconstruct (the scheme mirror's per-block recovery): the present shards of
+// each chunk as [block][k+1][ssd], rebuilt in place on the device, the data slots copied back.
+static int host_reconstruct_xor(fec_ctx* ctx, int k, size_t len, size_t nblocks, uint8_t* data, size_t dbs,
+                                const uint8_t* parity, size_t pbs, size_t ss, const uint32_t* masks,
+                                int32_t* block_status) {
+    const size_t ssd = round16(len);
+    const size_t n = (size_t)k + 1;
+    const uint32_t all = fk::low_mask((uint32_t)n), kmask = fk::low_mask((uint32_t)k);
+    const size_t chunk = std::min(nblocks, host_chunk_blocks(n * ssd));
+    int rc;
+    if ((rc = grow_stage(ctx, chunk * n * ssd))) return rc;
+    if ((rc = grow_masks(ctx, chunk))) return rc;
     HIP_TRY(hipMemsetAsync(ctx->d_err + 1, 0, sizeof(int), ctx->stream));
     std::vector<int32_t> st;
-    auto slot = [&](size_t b, size_t i) -> const uint8_t* {
-        return i < (size_t)k ? data + b * dbs + i * ss : parity + b * pbs + (i - k) * ss;
-    };
     for (size_t b0 = 0; b0 < nblocks; b0 += chunk) {
         const size_t nb = std::min(chunk, nblocks - b0);
         for (size_t b = 0; b < nb; ++b) {
             const uint32_t mask = masks[b0 + b] & all;
-            if ((mask & kmask) == kmask) continue;   // nothing to rebuild: skip the copy
+            if ((mask & kmask) == kmask) continue;
             for (size_t i = 0; i < n; ++i)
-                if ((mask >> i) & 1u) memcpy(ctx->h_stage + (b * n + i) * ssd, slot(b0 + b, i), len);
+                if ((mask >> i) & 1u)
+                    memcpy(ctx->h_stage + (b * n + i) * ssd,
+                           i < (size_t)k ? data + (b0 + b) * dbs + i * ss : parity + (b0 + b) * pbs, len);
         }
         HIP_TRY(hipMemcpyAsync(ctx->d_masks, masks + b0, nb * 4, hipMemcpyHostToDevice, ctx->stream));
         HIP_TRY(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, nb * n * ssd, hipMemcpyHostToDevice, ctx->stream));
-        if (code)
-            rc = rs_reconstruct_device(ctx, code, len, nb, ctx->d_stage, n * ssd, ctx->d_stage + k * ssd, n * ssd,
-                                       ssd, ctx->d_masks, ctx->d_status, ctx->d_err + 1);
-        else
-            rc = xor_reconstruct_device(ctx, k, len, nb, ctx->d_stage, n * ssd, ctx->d_stage + k * ssd, n * ssd,
-                                        ssd, ctx->d_masks, ctx->d_status, ctx->d_err + 1);
-        if (rc) return rc;
+        if ((rc = xor_reconstruct_device(ctx, k, len, nb, ctx->d_stage, n * ssd, ctx->d_stage + k * ssd, n * ssd, ssd,
+                                         ctx->d_masks, ctx->d_status, ctx->d_err + 1)))
+            return rc;
         st.resize(nb);
         HIP_TRY(hipMemcpyAsync(st.data(), ctx->d_status, nb * 4, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(hipMemcpyAsync(ctx->h_stage, ctx->d_stage, nb * n * ssd, hipMemcpyDeviceToHost, ctx->stream));
@@ -534,8 +774,7 @@ static int host_reconstruct(fec_ctx* ctx, Code* code, int k, int m, size_t len, 
             if (st[b] != 0) continue;
             const uint32_t mask = masks[b0 + b] & all;
             for (int i = 0; i < k; ++i)
-                if (!((mask >> i) & 1u))
-                    memcpy(data + (b0 + b) * dbs + i * ss, ctx->h_stage + (b * n + i) * ssd, len);
+                if (!((mask >> i) & 1u)) memcpy(data + (b0 + b) * dbs + i * ss, ctx->h_stage + (b * n + i) * ssd, len);
         }
     }
     int err = 0;
@@ -630,6 +869,15 @@ void fec_ctx_destroy(fec_ctx* ctx) {
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
     if (ctx->d_masks) (void)hipFree(ctx->d_masks);
     if (ctx->d_status) (void)hipFree(ctx->d_status);
+    for (HostSet& s : ctx->hs) {
+        if (s.s) (void)hipStreamSynchronize(s.s);
+        for (void* q : {(void*)s.h_in, (void*)s.h_out, (void*)s.h_masks, (void*)s.h_status})
+            if (q) (void)hipHostFree(q);
+        for (void* q : {(void*)s.d_in, (void*)s.d_out, (void*)s.d_masks, (void*)s.d_status})
+            if (q) (void)hipFree(q);
+        if (s.done) (void)hipEventDestroy(s.done);
+        if (s.s) (void)hipStreamDestroy(s.s);
+    }
     if (ctx->own) (void)hipStreamDestroy(ctx->own);
     (void)hipGetLastError();
     delete ctx;
@@ -660,7 +908,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 18 ? &fk::g_tune.enc_diag : key == 19 ? &fk::g_tune.dec_fused
               : key == 20 ? &fk::g_tune.dec_ipl : key == 21 ? &fk::g_tune.dec_diag
               : key == 22 ? &fk::g_tune.enc_dyadic : key == 23 ? &fk::g_tune.dec_direct
-              : key == 24 ? &fk::g_tune.dec_sorted : key == 25 ? &fk::g_tune.dec_fixk : nullptr;
+              : key == 24 ? &fk::g_tune.dec_sorted : key == 25 ? &fk::g_tune.dec_fixk
+              : key == 26 ? &fk::g_tune.host_chunk : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;
@@ -711,7 +960,7 @@ int fec_rs_encode_batch(fec_ctx* ctx, int k, int m, size_t shard_len, size_t nbl
                         size_t shard_stride, int flags) {
     if (k <= 0 || m < 0) return FEC_ERR_INV_SHARD_NUM;
     if (k + m > 256) return FEC_ERR_MAX_SHARD_NUM;
-    if (flags != FEC_DEVICE && flags != FEC_HOST) return FEC_ERR_INVALID_ARG;
+    if (flags != FEC_DEVICE && flags != FEC_HOST && flags != FEC_HOST_PINNED) return FEC_ERR_INVALID_ARG;
     if (shard_len == 0) return FEC_ERR_SHARD_NO_DATA;
     if (shard_len > (size_t(1) << 30)) return FEC_ERR_INVALID_ARG;
     int rc = select_device(ctx);
@@ -726,29 +975,8 @@ int fec_rs_encode_batch(fec_ctx* ctx, int k, int m, size_t shard_len, size_t nbl
         return rs_encode_device(ctx, code, shard_len, nblocks, data, data_block_stride, parity,
                                 parity_block_stride, shard_stride);
     }
-    // FEC_HOST: stage [chunk][n][ssd] through pinned memory.
-    const size_t ssd = round16(shard_len);
-    const size_t n = (size_t)k + m;
-    const size_t chunk = host_chunk_blocks(n, ssd);
-    if ((rc = grow_stage(ctx, std::min(chunk, nblocks) * n * ssd))) return rc;
-    for (size_t b0 = 0; b0 < nblocks; b0 += chunk) {
-        const size_t nb = std::min(chunk, nblocks - b0);
-        for (size_t b = 0; b < nb; ++b)
-            for (int j = 0; j < k; ++j)
-                memcpy(ctx->h_stage + (b * n + j) * ssd, data + (b0 + b) * data_block_stride + j * shard_stride,
-                       shard_len);
-        HIP_TRY(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, nb * n * ssd, hipMemcpyHostToDevice, ctx->stream));
-        if ((rc = rs_encode_device(ctx, code, shard_len, nb, ctx->d_stage, n * ssd, ctx->d_stage + k * ssd,
-                                   n * ssd, ssd)))
-            return rc;
-        HIP_TRY(hipMemcpyAsync(ctx->h_stage, ctx->d_stage, nb * n * ssd, hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
-        for (size_t b = 0; b < nb; ++b)
-            for (int i = 0; i < m; ++i)
-                memcpy(parity + (b0 + b) * parity_block_stride + i * shard_stride,
-                       ctx->h_stage + (b * n + k + i) * ssd, shard_len);
-    }
-    return FEC_OK;
+    return host_encode(ctx, code, k, m, shard_len, nblocks, data, data_block_stride, parity, parity_block_stride,
+                       shard_stride, flags == FEC_HOST_PINNED);
 }
 
 int fec_rs_reconstruct_batch(fec_ctx* ctx, int k, int m, size_t shard_len, size_t nblocks, uint8_t* data,
@@ -756,7 +984,7 @@ int fec_rs_reconstruct_batch(fec_ctx* ctx, int k, int m, size_t shard_len, size_
                              size_t shard_stride, const uint32_t* present_mask, int32_t* block_status, int flags) {
     if (k <= 0 || m < 0) return FEC_ERR_INV_SHARD_NUM;
     if (k + m > FEC_MAX_DECODE_SHARDS) return FEC_ERR_MAX_SHARD_NUM;
-    if (flags != FEC_DEVICE && flags != FEC_HOST) return FEC_ERR_INVALID_ARG;
+    if (flags != FEC_DEVICE && flags != FEC_HOST && flags != FEC_HOST_PINNED) return FEC_ERR_INVALID_ARG;
     if (shard_len == 0) return FEC_ERR_SHARD_NO_DATA;
     if (shard_len > (size_t(1) << 30)) return FEC_ERR_INVALID_ARG;
     int rc = select_device(ctx);
@@ -772,8 +1000,8 @@ int fec_rs_reconstruct_batch(fec_ctx* ctx, int k, int m, size_t shard_len, size_
         return rs_reconstruct_device(ctx, code, shard_len, nblocks, data, data_block_stride, parity,
                                      parity_block_stride, shard_stride, present_mask, block_status, ctx->d_err);
     }
-    return host_reconstruct(ctx, code, k, m, shard_len, nblocks, data, data_block_stride, parity,
-                            parity_block_stride, shard_stride, present_mask, block_status);
+    return host_reconstruct_rs(ctx, code, k, m, shard_len, nblocks, data, data_block_stride, parity,
+                               parity_block_stride, shard_stride, present_mask, block_status, flags == FEC_HOST_PINNED);
 }
 
 int fec_rs_recover_batch(fec_ctx* ctx, int k, int m, size_t shard_len, size_t nblocks, const uint8_t* data,
@@ -805,7 +1033,7 @@ int fec_xor_encode_batch(fec_ctx* ctx, int k, size_t shard_len, size_t nblocks, 
                          int flags) {
     if (k <= 0) return FEC_ERR_INV_SHARD_NUM;
     if (k + 1 > 256) return FEC_ERR_MAX_SHARD_NUM;
-    if (flags != FEC_DEVICE && flags != FEC_HOST) return FEC_ERR_INVALID_ARG;
+    if (flags != FEC_DEVICE && flags != FEC_HOST && flags != FEC_HOST_PINNED) return FEC_ERR_INVALID_ARG;
     if (shard_len == 0) return FEC_ERR_SHARD_NO_DATA;
     if (shard_len > (size_t(1) << 30)) return FEC_ERR_INVALID_ARG;
     int rc = select_device(ctx);
@@ -818,26 +1046,8 @@ int fec_xor_encode_batch(fec_ctx* ctx, int k, size_t shard_len, size_t nblocks, 
         return xor_encode_device(ctx, k, shard_len, nblocks, data, data_block_stride, parity, parity_block_stride,
                                  shard_stride);
     }
-    const size_t ssd = round16(shard_len);
-    const size_t n = (size_t)k + 1;
-    const size_t chunk = host_chunk_blocks(n, ssd);
-    if ((rc = grow_stage(ctx, std::min(chunk, nblocks) * n * ssd))) return rc;
-    for (size_t b0 = 0; b0 < nblocks; b0 += chunk) {
-        const size_t nb = std::min(chunk, nblocks - b0);
-        for (size_t b = 0; b < nb; ++b)
-            for (int j = 0; j < k; ++j)
-                memcpy(ctx->h_stage + (b * n + j) * ssd, data + (b0 + b) * data_block_stride + j * shard_stride,
-                       shard_len);
-        HIP_TRY(hipMemcpyAsync(ctx->d_stage, ctx->h_stage, nb * n * ssd, hipMemcpyHostToDevice, ctx->stream));
-        if ((rc = xor_encode_device(ctx, k, shard_len, nb, ctx->d_stage, n * ssd, ctx->d_stage + k * ssd, n * ssd,
-                                    ssd)))
-            return rc;
-        HIP_TRY(hipMemcpyAsync(ctx->h_stage, ctx->d_stage, nb * n * ssd, hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
-        for (size_t b = 0; b < nb; ++b)
-            memcpy(parity + (b0 + b) * parity_block_stride, ctx->h_stage + (b * n + k) * ssd, shard_len);
-    }
-    return FEC_OK;
+    return host_encode(ctx, nullptr, k, 1, shard_len, nblocks, data, data_block_stride, parity, parity_block_stride,
+                       shard_stride, flags == FEC_HOST_PINNED);
 }
 
 int fec_xor_reconstruct_batch(fec_ctx* ctx, int k, size_t shard_len, size_t nblocks, uint8_t* data,
@@ -845,7 +1055,7 @@ int fec_xor_reconstruct_batch(fec_ctx* ctx, int k, size_t shard_len, size_t nblo
                               size_t shard_stride, const uint32_t* present_mask, int32_t* block_status, int flags) {
     if (k <= 0) return FEC_ERR_INV_SHARD_NUM;
     if (k + 1 > FEC_MAX_DECODE_SHARDS) return FEC_ERR_MAX_SHARD_NUM;
-    if (flags != FEC_DEVICE && flags != FEC_HOST) return FEC_ERR_INVALID_ARG;
+    if (flags != FEC_DEVICE && flags != FEC_HOST && flags != FEC_HOST_PINNED) return FEC_ERR_INVALID_ARG;
     if (shard_len == 0) return FEC_ERR_SHARD_NO_DATA;
     if (shard_len > (size_t(1) << 30)) return FEC_ERR_INVALID_ARG;
     int rc = select_device(ctx);
@@ -858,8 +1068,8 @@ int fec_xor_reconstruct_batch(fec_ctx* ctx, int k, size_t shard_len, size_t nblo
         return xor_reconstruct_device(ctx, k, shard_len, nblocks, data, data_block_stride, parity,
                                       parity_block_stride, shard_stride, present_mask, block_status, ctx->d_err);
     }
-    return host_reconstruct(ctx, nullptr, k, 1, shard_len, nblocks, data, data_block_stride, parity,
-                            parity_block_stride, shard_stride, present_mask, block_status);
+    return host_reconstruct_xor(ctx, k, shard_len, nblocks, data, data_block_stride, parity, parity_block_stride,
+                                shard_stride, present_mask, block_status);
 }
 
 }  // extern "C"

@@ -79,6 +79,8 @@ struct ReconArgs {
     uint8_t* data;             // data shard 0 of block 0 (rebuilt shards are written here)
     const uint8_t* parity;     // parity shard 0 of block 0
     uint64_t dbs, pbs, ss;
+    uint64_t pss;              // parity shard stride (parity i of block b at parity + b*pbs + i*pss; = ss
+                               // in the ABI's layouts, parity-major in the host path's staging)
     const uint8_t* plans;
     uint32_t k, len, cps, nblocks, maxe;
     PlanLayout lay;
@@ -154,6 +156,7 @@ struct Tuning {
     int dec_direct = 1;       // single-erasure codes with small tables: no plan kernel, per-lane table
                               // lookup (1: rows expanded from scalar-loaded coefficients, 2: PermTab rows
                               // copied by a vector load); multi-erasure waves go to a worklist kernel
+    int host_chunk = 0;       // host-resident path: blocks per staging chunk (0: 128 MiB worth)
     int dec_fixk = 1;         // RS(16,24) rebuild with k = 16 at compile time (all 16 loads in flight)
     int dec_sorted = 1;       // multi-erasure codes (plan path, shards of 32+ chunks): sorted parallel plans
     int dec_ipl = 0;          // wave-form reconstruct items per lane: 1; 2 loaded together; 3: 2 one

@@ -29,7 +29,7 @@ __device__ __forceinline__ void recon_item(const ReconArgs& a, const uint8_t* P,
             const uint32_t w = jj < 4 ? sl.x : sl.y;
             const uint32_t slot = (w >> (8 * (jj & 3))) & 0xFFu;
             x[jj] = j0 + jj < k   // uniform predicate: no loads past input k-1
-                        ? ld16<NTL>(slot < k ? dblk + (uint64_t)slot * a.ss : pblk + (uint64_t)(slot - k) * a.ss)
+                        ? ld16<NTL>(slot < k ? dblk + (uint64_t)slot * a.ss : pblk + (uint64_t)(slot - k) * a.pss)
                         : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
@@ -114,7 +114,7 @@ __device__ __forceinline__ void recon_item_k(const ReconArgs& a, const uint8_t* 
         for (int jj = 0; jj < 8; ++jj) {
             const uint32_t slot = ((jj < 4 ? sl.x : sl.y) >> (8 * (jj & 3))) & 0xFFu;
             x[j0 + jj] = ld16<NTL>(slot < (uint32_t)K ? dblk + (uint64_t)slot * a.ss
-                                                      : pblk + (uint64_t)(slot - K) * a.ss);
+                                                      : pblk + (uint64_t)(slot - K) * a.pss);
         }
     }
     uint8_t* oblk = a.out ? a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk : nullptr;

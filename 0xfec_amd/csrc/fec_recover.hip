@@ -170,7 +170,7 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
     const uint32_t R0 = work ? __ffs(mask >> k) - 1 : 0;
     const gf::PermTab* T = wt + g * k;
     const uint8_t* dblk = a.data + (uint64_t)blk * a.dbs + (uint64_t)c * kChunk;
-    const uint8_t* par = a.parity + (uint64_t)blk * a.pbs + (uint64_t)R0 * a.ss + (uint64_t)c * kChunk;
+    const uint8_t* par = a.parity + (uint64_t)blk * a.pbs + (uint64_t)R0 * a.pss + (uint64_t)c * kChunk;
     uint32_t acc[4] = {0, 0, 0, 0};
     if constexpr (K > 0) {
         // unconditional loads (a lane with nothing to rebuild reads one L2-resident table line

@@ -37,7 +37,15 @@
  *               ctx stream; per-block decode failures are reported through `block_status`
  *               (if given) and, sticky, by fec_sync().
  *   FEC_HOST    pointers are host memory with any layout; the ctx stages the batch
- *               through pinned buffers (H2D -> kernel -> D2H) and returns when done.
+ *               through pinned buffers (H2D -> kernel -> D2H) and returns when done. Chunks
+ *               of the batch alternate between two staging sets on two streams, so staging,
+ *               transfers and kernels of neighbouring chunks overlap; only the shards the code
+ *               needs cross PCIe (encode: k up, m down; reconstruct: the data shards and the
+ *               parity planes the blocks read up, the rebuilt shards down).
+ *   FEC_HOST_PINNED  as FEC_HOST, but the caller's buffers are pinned (hipHostMalloc) or
+ *               registered (hipHostRegister): no staging copies, each shard column moves with
+ *               one 2D DMA between the caller's layout and the device. fec_rs_recover_batch
+ *               is FEC_DEVICE only.
  *
  * Threading: a ctx has one HIP stream and is used by one caller at a time (the
  * reference's manager is per connection and not thread-safe either: manager.go:41-48).
@@ -68,6 +76,7 @@ extern "C" {
 
 #define FEC_DEVICE 0
 #define FEC_HOST 1
+#define FEC_HOST_PINNED 2
 
 /* Largest n = k + m the reconstruct path accepts (present masks are uint32). */
 #define FEC_MAX_DECODE_SHARDS 32

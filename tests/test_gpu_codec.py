@@ -399,3 +399,65 @@ def test_rs_32_0_fully_present_is_untouched(codec, torch, fec):
     assert codec.lib_sync_rc() == fec.FEC_ERR_TOO_FEW_SHARDS
     assert (st.cpu().numpy() == fec.FEC_ERR_TOO_FEW_SHARDS).all()
     assert np.array_equal(data.cpu().numpy(), data_np)
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("chunk", [0, 7])
+@pytest.mark.parametrize("k,m,L", [(2, 1, 1202), (8, 4, 1202), (16, 8, 700), (20, 10, 1436), (8, 4, 33)])
+def test_rs_host_pipeline_matches_oracle(codec, oracle, torch, fec, pinned, chunk, k, m, L):
+    """FEC_HOST (pageable, staged) and FEC_HOST_PINNED (direct 2D DMA) through the two-set
+    pipeline, with many small chunks (chunk = 7 blocks) so consecutive chunks alternate sets and
+    overlap: encode, then in-place reconstruct of random erasures (some blocks unrecoverable, some
+    complete) with split data / parity buffers of a padded host layout, against the oracle."""
+    rng = np.random.default_rng(k * 100 + L + chunk + pinned)
+    n, B, S = k + m, 97, L + 5                           # unaligned host stride: any layout
+    full = np.zeros((B, n, L), dtype=np.uint8)
+    full[:, :k] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    oracle.rs_encode(k, m, full)
+    mk = (lambda a: torch.from_numpy(a).pin_memory()) if pinned else (lambda a: a)
+    get = (lambda t: t.numpy()) if pinned else (lambda a: a)
+    data = np.zeros((B, k, S), dtype=np.uint8)
+    data[:, :, :L] = full[:, :k]
+    data = mk(data)
+    par = mk(np.full((B, m, S), 0x77, dtype=np.uint8))
+    old = codec.set_tuning(host_chunk=chunk)
+    try:
+        codec.rs_encode_split(k, m, data, par, shard_len=L)
+        assert np.array_equal(get(par)[:, :, :L], full[:, k:])
+        assert (get(par)[:, :, L:] == 0x77).all()        # exactly shard_len bytes written
+        masks = _random_masks(rng, B, k, m, max_loss=m + 1)
+        dmg = get(data).copy()
+        for b in range(B):
+            for i in range(k):
+                if not (masks[b] >> i) & 1:
+                    dmg[b, i, :L] = 0xA1
+        want = np.zeros((B, n, L), dtype=np.uint8)
+        want[:, :k] = dmg[:, :, :L]
+        want[:, k:] = full[:, k:]
+        st_want = oracle.rs_reconstruct(k, m, want, masks)
+        d2 = mk(dmg)
+        st = np.full(B, 7, dtype=np.int32)
+        rc = codec.rs_reconstruct_split(k, m, d2, par, masks, status=st, shard_len=L)
+        assert rc == (fec.FEC_ERR_TOO_FEW_SHARDS if (st_want != 0).any() else fec.FEC_OK)
+        assert np.array_equal(st != 0, st_want != 0)
+        assert np.array_equal(get(d2)[:, :, :L], want[:, :k])
+        assert (get(d2)[:, :, L:] == dmg[:, :, L:]).all()
+    finally:
+        codec.set_tuning(**old)
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_xor_host_pipeline_matches_oracle(codec, oracle, torch, fec, pinned):
+    rng = np.random.default_rng(5 + pinned)
+    k, B, L = 3, 61, 1202
+    sh = np.zeros((B, k + 1, L), dtype=np.uint8)
+    sh[:, :k] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    ref = oracle.xor_encode(k, sh.copy())
+    buf = torch.from_numpy(sh.copy()).pin_memory() if pinned else sh.copy()
+    old = codec.set_tuning(host_chunk=5)
+    try:
+        codec.xor_encode(k, buf)
+    finally:
+        codec.set_tuning(**old)
+    got = buf.numpy() if pinned else buf
+    assert np.array_equal(got, ref)
