@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <functional>
 #include <map>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -83,7 +84,8 @@ struct HostSet {
     uint32_t* d_masks = nullptr;
     int32_t* h_status = nullptr;
     int32_t* d_status = nullptr;
-    size_t in_cap = 0, out_cap = 0, blk_cap = 0;
+    uint8_t* d_raw = nullptr;   // FEC_HOST_PINNED: the caller's span, copied linearly (fec_pack.hip)
+    size_t in_cap = 0, out_cap = 0, blk_cap = 0, raw_cap = 0;
     hipStream_t s = nullptr;
     hipEvent_t done = nullptr;
 };
@@ -518,6 +520,73 @@ static size_t host_chunk_blocks(size_t bytes_per_block) {
     return std::max<size_t>(1, kStageBytes / std::max<size_t>(1, bytes_per_block));
 }
 
+// fn(lo, hi) over [0, n) on up to 8 threads: the staging and scatter copies of FEC_HOST
+// (one core copies ~10 GB/s, a fifth of PCIe).
+template <class F>
+static void parallel_for(size_t n, F fn) {
+    const unsigned T = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+    if (n < 512 || T == 1) {
+        fn((size_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (n + T - 1) / T;
+    for (size_t lo = 0; lo < n; lo += per) th.emplace_back(fn, lo, std::min(n, lo + per));
+    for (auto& t : th) t.join();
+}
+
+static int host_raw_grow(HostSet& s, size_t bytes) {
+    if (bytes <= s.raw_cap) return FEC_OK;
+    if (s.d_raw) HIP_TRY(hipFree(s.d_raw));
+    s.d_raw = nullptr;
+    s.raw_cap = 0;
+    HIP_TRY(hipMalloc(&s.d_raw, bytes));
+    s.raw_cap = bytes;
+    return FEC_OK;
+}
+
+// Bytes of the caller's span of nb blocks (shards of len bytes, cols per block).
+static size_t span_bytes(size_t nb, size_t cols, size_t bs, size_t ss, size_t len) {
+    return (nb - 1) * bs + (cols - 1) * ss + len;
+}
+
+// A span worth one linear copy: at most a quarter more bytes than the shards themselves.
+static bool dense_span(size_t nb, size_t cols, size_t bs, size_t ss, size_t len) {
+    return span_bytes(nb, cols, bs, ss, len) * 4 <= nb * cols * len * 5;
+}
+
+// Caller's columns [0, cols) of nb blocks into the device stage [nb][st_bs/st_ss]: one linear DMA
+// of the span of all span_cols >= cols columns and a device repack when that span is dense (a
+// few unneeded columns ride along: one linear DMA beats narrow 2D rows), else one 2D DMA per
+// column.
+static int pinned_up(HostSet& s, uint8_t* stage, size_t st_bs, size_t st_ss, const uint8_t* src, size_t bs, size_t ss,
+                     size_t nb, size_t cols, size_t len, uint8_t* raw, size_t span_cols) {
+    if (dense_span(nb, span_cols, bs, ss, len)) {
+        HIP_TRY(hipMemcpyAsync(raw, src, span_bytes(nb, span_cols, bs, ss, len), hipMemcpyHostToDevice, s.s));
+        HIP_TRY(fk::launch_span_to_stage(stage, st_bs, st_ss, raw, bs, ss, (uint32_t)nb, (uint32_t)cols, (uint32_t)len,
+                                         s.s));
+        return FEC_OK;
+    }
+    for (size_t j = 0; j < cols; ++j)
+        HIP_TRY(hipMemcpy2DAsync(stage + j * st_ss, st_bs, src + j * ss, bs, len, nb, hipMemcpyHostToDevice, s.s));
+    return FEC_OK;
+}
+
+// Device stage [nb][st_bs/st_ss] columns back to the caller: for a packed caller layout (no
+// bytes between shards) a device repack and one linear DMA; else one 2D DMA per column, which
+// writes exactly len bytes per shard.
+static int pinned_down(HostSet& s, uint8_t* dst, size_t bs, size_t ss, const uint8_t* stage, size_t st_bs,
+                       size_t st_ss, size_t nb, size_t cols, size_t len, uint8_t* raw) {
+    if (ss == len && bs == cols * len) {
+        HIP_TRY(fk::launch_stage_to_packed(raw, stage, st_bs, st_ss, (uint32_t)nb, (uint32_t)cols, (uint32_t)len, s.s));
+        HIP_TRY(hipMemcpyAsync(dst, raw, nb * cols * len, hipMemcpyDeviceToHost, s.s));
+        return FEC_OK;
+    }
+    for (size_t j = 0; j < cols; ++j)
+        HIP_TRY(hipMemcpy2DAsync(dst + j * ss, bs, stage + j * st_ss, st_bs, len, nb, hipMemcpyDeviceToHost, s.s));
+    return FEC_OK;
+}
+
 static int host_set_grow(fec_ctx* ctx, HostSet& s, size_t in_bytes, size_t out_bytes, size_t blocks) {
     if (!s.s) {
         HIP_TRY(hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking));
@@ -569,13 +638,6 @@ static int on_stream(fec_ctx* ctx, hipStream_t s, F fn) {
     return rc;
 }
 
-// Column j of a chunk: nb rows of len bytes, host pitch hp, device pitch dp.
-static int copy_cols(void* dst, size_t dpitch, const void* src, size_t spitch, size_t len, size_t rows,
-                     hipMemcpyKind kind, hipStream_t s) {
-    HIP_TRY(hipMemcpy2DAsync(dst, dpitch, src, spitch, len, rows, kind, s));
-    return FEC_OK;
-}
-
 // Encode (RS when code != nullptr, else XOR(k, 1)): host data -> host parity.
 static int host_encode(fec_ctx* ctx, Code* code, int k, int m, size_t len, size_t nblocks, const uint8_t* data,
                        size_t dbs, uint8_t* parity, size_t pbs, size_t ss, bool pinned) {
@@ -590,9 +652,11 @@ static int host_encode(fec_ctx* ctx, Code* code, int k, int m, size_t len, size_
         HostSet& s = ctx->hs[i];
         HIP_TRY(hipEventSynchronize(s.done));
         if (!pinned)
-            for (size_t b = 0; b < pend[i].nb; ++b)
-                for (int r = 0; r < m; ++r)
-                    memcpy(parity + (pend[i].b0 + b) * pbs + r * ss, s.h_out + (b * m + r) * ssd, len);
+            parallel_for(pend[i].nb, [&](size_t lo, size_t hi) {
+                for (size_t b = lo; b < hi; ++b)
+                    for (int r = 0; r < m; ++r)
+                        memcpy(parity + (pend[i].b0 + b) * pbs + r * ss, s.h_out + (b * m + r) * ssd, len);
+            });
         pend[i].live = false;
         return FEC_OK;
     };
@@ -604,13 +668,15 @@ static int host_encode(fec_ctx* ctx, Code* code, int k, int m, size_t len, size_
         HostSet& s = ctx->hs[i];
         if ((rc = host_set_grow(ctx, s, chunk * k * ssd, chunk * m * ssd, 1))) return rc;
         if (pinned) {
-            for (int j = 0; j < k; ++j)
-                if ((rc = copy_cols(s.d_in + j * ssd, (size_t)k * ssd, data + b0 * dbs + j * ss, dbs, len, nb,
-                                    hipMemcpyHostToDevice, s.s)))
-                    return rc;
+            if ((rc = host_raw_grow(s, chunk * std::max(dbs, pbs) + 16))) return rc;
+            if ((rc = pinned_up(s, s.d_in, (size_t)k * ssd, ssd, data + b0 * dbs, dbs, ss, nb, k, len, s.d_raw, k)))
+                return rc;
         } else {
-            for (size_t b = 0; b < nb; ++b)
-                for (int j = 0; j < k; ++j) memcpy(s.h_in + (b * k + j) * ssd, data + (b0 + b) * dbs + j * ss, len);
+            parallel_for(nb, [&](size_t lo, size_t hi) {
+                for (size_t b = lo; b < hi; ++b)
+                    for (int j = 0; j < k; ++j)
+                        memcpy(s.h_in + (b * k + j) * ssd, data + (b0 + b) * dbs + j * ss, len);
+            });
             HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, nb * k * ssd, hipMemcpyHostToDevice, s.s));
         }
         rc = on_stream(ctx, s.s, [&] {
@@ -619,10 +685,8 @@ static int host_encode(fec_ctx* ctx, Code* code, int k, int m, size_t len, size_
         });
         if (rc) return rc;
         if (pinned) {
-            for (int r = 0; r < m; ++r)
-                if ((rc = copy_cols(parity + b0 * pbs + r * ss, pbs, s.d_out + r * ssd, (size_t)m * ssd, len, nb,
-                                    hipMemcpyDeviceToHost, s.s)))
-                    return rc;
+            if ((rc = pinned_down(s, parity + b0 * pbs, pbs, ss, s.d_out, (size_t)m * ssd, ssd, nb, m, len, s.d_raw)))
+                return rc;
         } else {
             HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, nb * m * ssd, hipMemcpyDeviceToHost, s.s));
         }
@@ -661,15 +725,17 @@ static int host_reconstruct_rs(fec_ctx* ctx, Code* code, int k, int m, size_t le
         for (size_t b = 0; b < pend[i].nb; ++b) {
             const int32_t st = s.h_status[b];
             if (block_status) block_status[pend[i].b0 + b] = st < 0 ? st : 0;
-            if (st < 0) {
-                failed = true;
-                continue;
-            }
-            const uint32_t mask = s.h_masks[b];
-            for (int j = 0, r = 0; j < k && r < st; ++j)
-                if (!((mask >> j) & 1u))
-                    memcpy(data + (pend[i].b0 + b) * dbs + j * ss, s.h_out + (b * pend[i].slots + r++) * ssd, len);
+            if (st < 0) failed = true;
         }
+        parallel_for(pend[i].nb, [&](size_t lo, size_t hi) {
+            for (size_t b = lo; b < hi; ++b) {
+                const int32_t st = s.h_status[b];
+                const uint32_t mask = s.h_masks[b];
+                for (int j = 0, r = 0; j < k && r < st; ++j)
+                    if (!((mask >> j) & 1u))
+                        memcpy(data + (pend[i].b0 + b) * dbs + j * ss, s.h_out + (b * pend[i].slots + r++) * ssd, len);
+            }
+        });
         pend[i].live = false;
         return FEC_OK;
     };
@@ -697,24 +763,26 @@ static int host_reconstruct_rs(fec_ctx* ctx, Code* code, int k, int m, size_t le
         }
         uint8_t* d_par = s.d_in + nb * k * ssd;   // parity planes [P][nb][ssd]
         if (pinned) {
-            for (int j = 0; j < k; ++j)
-                if ((rc = copy_cols(s.d_in + j * ssd, (size_t)k * ssd, data + b0 * dbs + j * ss, dbs, len, nb,
-                                    hipMemcpyHostToDevice, s.s)))
-                    return rc;
-            for (size_t r = 0; r < P; ++r)
-                if ((rc = copy_cols(d_par + r * nb * ssd, ssd, parity + b0 * pbs + r * ss, pbs, len, nb,
-                                    hipMemcpyHostToDevice, s.s)))
-                    return rc;
+            const size_t draw = span_bytes(nb, k, dbs, ss, len);
+            if ((rc = host_raw_grow(s, draw + span_bytes(nb, m, pbs, ss, len) + 16))) return rc;
+            if ((rc = pinned_up(s, s.d_in, (size_t)k * ssd, ssd, data + b0 * dbs, dbs, ss, nb, k, len, s.d_raw, k)))
+                return rc;
+            if (P && (rc = pinned_up(s, d_par, ssd, nb * ssd, parity + b0 * pbs, pbs, ss, nb, P, len,
+                                     s.d_raw + ((draw + 15) & ~size_t(15)), m)))
+                return rc;
         } else {
-            for (size_t b = 0; b < nb; ++b) {
-                const uint32_t mask = s.h_masks[b];
-                if ((mask & kmask) == kmask) continue;   // nothing to rebuild: nothing read
-                for (int j = 0; j < k; ++j)
-                    if ((mask >> j) & 1u) memcpy(s.h_in + (b * k + j) * ssd, data + (b0 + b) * dbs + j * ss, len);
-                for (size_t r = 0; r < P; ++r)
-                    if ((mask >> (k + r)) & 1u)
-                        memcpy(s.h_in + nb * k * ssd + (r * nb + b) * ssd, parity + (b0 + b) * pbs + r * ss, len);
-            }
+            parallel_for(nb, [&](size_t lo, size_t hi) {
+                for (size_t b = lo; b < hi; ++b) {
+                    const uint32_t mask = s.h_masks[b];
+                    if ((mask & kmask) == kmask) continue;   // nothing to rebuild: nothing read
+                    for (int j = 0; j < k; ++j)
+                        if ((mask >> j) & 1u)
+                            memcpy(s.h_in + (b * k + j) * ssd, data + (b0 + b) * dbs + j * ss, len);
+                    for (size_t r = 0; r < P; ++r)
+                        if ((mask >> (k + r)) & 1u)
+                            memcpy(s.h_in + nb * k * ssd + (r * nb + b) * ssd, parity + (b0 + b) * pbs + r * ss, len);
+                }
+            });
             HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, (nb * k + P * nb) * ssd, hipMemcpyHostToDevice, s.s));
         }
         HIP_TRY(hipMemcpyAsync(s.d_masks, s.h_masks, nb * 4, hipMemcpyHostToDevice, s.s));
@@ -873,7 +941,7 @@ void fec_ctx_destroy(fec_ctx* ctx) {
         if (s.s) (void)hipStreamSynchronize(s.s);
         for (void* q : {(void*)s.h_in, (void*)s.h_out, (void*)s.h_masks, (void*)s.h_status})
             if (q) (void)hipHostFree(q);
-        for (void* q : {(void*)s.d_in, (void*)s.d_out, (void*)s.d_masks, (void*)s.d_status})
+        for (void* q : {(void*)s.d_in, (void*)s.d_out, (void*)s.d_masks, (void*)s.d_status, (void*)s.d_raw})
             if (q) (void)hipFree(q);
         if (s.done) (void)hipEventDestroy(s.done);
         if (s.s) (void)hipStreamDestroy(s.s);

@@ -202,6 +202,13 @@ hipError_t launch_rs_recover_direct(const ReconArgs& a, int ncu, hipStream_t s);
 hipError_t launch_xor_encode(const XorArgs& a, int grid, hipStream_t s);
 hipError_t launch_xor_reconstruct(const XorArgs& a, int grid, hipStream_t s);
 
+// Host-resident path layout conversion (fec_pack.hip): caller's span -> 16-byte stage slots, and
+// stage slots -> packed [nb][cols][len] image (written rounded up to 4 bytes).
+hipError_t launch_span_to_stage(uint8_t* stage, uint64_t st_bs, uint64_t st_ss, const uint8_t* span, uint64_t src_bs,
+                                uint64_t src_ss, uint32_t nb, uint32_t cols, uint32_t len, hipStream_t s);
+hipError_t launch_stage_to_packed(uint8_t* packed, const uint8_t* stage, uint64_t st_bs, uint64_t st_ss, uint32_t nb,
+                                  uint32_t cols, uint32_t len, hipStream_t s);
+
 // Blocks per decode tile for shard chunk count `cps`, bounded by LDS.
 uint32_t pick_tile_blocks(uint32_t cps, uint32_t k, uint32_t maxe, const PlanLayout& lay);
 size_t recon_lds_bytes(uint32_t g, uint32_t k, uint32_t maxe, const PlanLayout& lay);

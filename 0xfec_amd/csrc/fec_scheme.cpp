@@ -646,7 +646,12 @@ struct fec_bytes {
 
 static thread_local std::string t_last_error;
 
-static int report(const fec::Error& e) {
+namespace fec {
+namespace cabi {
+// Shared by the C ABIs of this library (fec_scheme.h, fec_batch.h, fec_go.h): a nil error is 0;
+// otherwise the Go text goes to fec_last_error() and the code (FEC_ERR_SCHEME for Go-level
+// errors) is returned.
+int report(const fec::Error& e) {
     if (e.ok()) {
         t_last_error.clear();
         return FEC_OK;
@@ -655,13 +660,18 @@ static int report(const fec::Error& e) {
     return e.code ? e.code : FEC_ERR_SCHEME;
 }
 
-static std::shared_ptr<fec::Engine> engine_for(int device) {
+std::shared_ptr<fec::Engine> engine_for(int device) {
     // one engine (one fec_ctx, created lazily) per device per thread
     static thread_local std::map<int, std::shared_ptr<fec::Engine>> engines;
     auto& e = engines[device];
     if (!e) e = std::make_shared<fec::Engine>(device);
     return e;
 }
+}  // namespace cabi
+}  // namespace fec
+
+using fec::cabi::engine_for;
+using fec::cabi::report;
 
 extern "C" {
 

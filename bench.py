@@ -70,7 +70,8 @@ def parse():
     p.add_argument("--seed", type=int, default=0x0FEC)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-blocks", type=int, default=1 << 15)
-    p.add_argument("--host-path", action="store_true", help="also time the pinned H2D/D2H path")
+    p.add_argument("--host-blocks", type=int, default=1 << 17,
+                   help="blocks of the host-resident (PCIe-inclusive) measurement, rank 0 at N=1; 0: skip")
     return p.parse_args()
 
 
@@ -195,6 +196,71 @@ def cpu_baseline(k, m, blocks, seed, budget_s=12.0):
                                                            ", ".join(orc.isa_name(i) for i in isas)),
             "scalar_value": round(scalar, 3),
             "scalar_sample": "%d reps, pure-Go mulTable form (oracle/fec_oracle.c)" % sreps}
+
+
+def host_resident(torch, fec, codec, k, m, blocks, seed, reps=3):
+    """The path as the reference runs it, from host packet buffers to host packet buffers:
+    fec_rs_encode_batch + single-erasure fec_rs_reconstruct_batch on host memory, PCIe copies
+    included (pinned hipMemcpyAsync, two staging sets overlapping chunks). Two forms: buffers the
+    caller pinned (FEC_HOST_PINNED: direct 2D DMA) and pageable buffers (FEC_HOST: staged by the
+    library). Packed host layout, stride = shard length. Reported beside the device-resident
+    value, never as it."""
+    import numpy as np
+    n, L = k + m, SHARD_LEN
+    shard = importlib.import_module("0xfec_amd.shard")
+    rng = np.random.default_rng(seed)
+    src = np.zeros((blocks, k, L), dtype=np.uint8)
+    src[:, :, :PAYLOAD] = rng.integers(0, 256, (blocks, k, PAYLOAD), dtype=np.uint8)
+    src[:, :, PAYLOAD] = PAYLOAD >> 8
+    src[:, :, PAYLOAD + 1] = PAYLOAD & 0xFF
+    erased = shard.synth_single_erasures(seed, 0, blocks, k)
+    masks = (((1 << n) - 1) & ~(1 << erased)).astype(np.uint32)
+    # PCIe bytes of a step: encode k up + m down; reconstruct k data shards + the parity planes
+    # read up (pinned: the whole parity span rides one linear DMA), the rebuilt shard down
+    out = {"blocks": blocks, "layout": "packed host [B][k][1202] + [B][m][1202]",
+           "pcie_bytes_per_step": blocks * (k + m + k + 1 + 1) * L,
+           "pcie_bytes_note": "pageable: k+m+k+1+1 shards per block; pinned: k+m+k+m+1 (whole parity span up)"}
+    for form in ("pinned", "pageable"):
+        if form == "pinned":
+            data = torch.from_numpy(src.copy()).pin_memory()
+            par = torch.zeros((blocks, m, L), dtype=torch.uint8).pin_memory()
+            dnp, pnp = data.numpy(), par.numpy()
+            flags, dp, pp = fec.FEC_HOST_PINNED, data.data_ptr(), par.data_ptr()
+        else:
+            dnp, pnp = src.copy(), np.zeros((blocks, m, L), dtype=np.uint8)
+            flags, dp, pp = fec.FEC_HOST, dnp.ctypes.data, pnp.ctypes.data
+        rows = np.arange(blocks)
+
+        def step():
+            codec.rs_encode_raw(k, m, L, blocks, dp, k * L, pp, m * L, L, flags)
+            rc = codec.rs_reconstruct_raw(k, m, L, blocks, dp, k * L, pp, m * L, L, masks.ctypes.data, None, flags)
+            if rc:
+                raise fec.FecError(rc, "host reconstruct")
+
+        codec.rs_encode_raw(k, m, L, blocks, dp, k * L, pp, m * L, L, flags)
+        dnp[rows, erased] = 0                       # the erased shards, wiped once (checked below)
+        rc = codec.rs_reconstruct_raw(k, m, L, blocks, dp, k * L, pp, m * L, L, masks.ctypes.data, None, flags)
+        ok = rc == 0 and bool(np.array_equal(dnp, src))
+        t = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            step()
+            t.append(time.perf_counter() - t0)
+        best = min(t)
+        out[form] = {"value": round(blocks * k * PAYLOAD / 2**30 / best, 2), "unit": "GiB/s",
+                     "ms_per_step": round(best * 1e3, 2), "pcie_GBps": round(out["pcie_bytes_per_step"] / best / 1e9, 2),
+                     "check": ok and bool(np.array_equal(pnp[:64], oracle_parity(k, m, src[:64])))}
+    return out
+
+
+def oracle_parity(k, m, data):
+    """Parity of host data blocks [B, k, L] by the CPU oracle (checker only)."""
+    import numpy as np
+    from oracle import oracle as orc
+    sh = np.zeros((data.shape[0], k + m, data.shape[2]), dtype=np.uint8)
+    sh[:, :k] = data
+    orc.rs_encode(k, m, sh)
+    return sh[:, k:]
 
 
 def main():
@@ -334,6 +400,10 @@ def main():
             },
             "check": {"roundtrip_full_batch": ok_roundtrip, "encode_vs_oracle_64_blocks": ok_parity},
         }
+        if world == 1 and args.host_blocks > 0:
+            del batch, step, encode, decode, decode_inplace   # free the device batch first
+            torch.cuda.empty_cache()
+            out["host_resident"] = host_resident(torch, fec, codec, k, m, args.host_blocks, args.seed)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(k, m, args.cpu_sample_blocks, args.seed)
         print(json.dumps(out), flush=True)

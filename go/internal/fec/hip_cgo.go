@@ -1,0 +1,71 @@
+//go:build fechip
+
+// Package fec additions that bind the MI355X engine (lib0xfec_hip.so). These files are dropped
+// into the reference's internal/fec directory (INTEGRATION.md); they use its unexported
+// block type and helpers, and build only with `-tags fechip`, so the default build is unchanged.
+//
+// cgo pointer rules, as applied throughout:
+//   - A Go pointer passed to C may point only to memory without Go pointers ([]byte payloads
+//     qualify); C must not keep it after the call. Every entry point of fec_hip.h / fec_go.h
+//     copies its inputs before returning (FEC_HOST stages through the library's pinned
+//     memory; fec_go_*_add copies the payload).
+//   - An array of Go pointers (fec_go_encoder_submit) must itself be C memory, and the Go
+//     memory it points to must be pinned (runtime.Pinner, Go 1.21 — go.mod:3) until the call
+//     returns.
+package fec
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../third_party/0xfec/include
+#cgo LDFLAGS: -L${SRCDIR}/../../third_party/0xfec/lib -l0xfec_hip -Wl,-rpath,${SRCDIR}/../../third_party/0xfec/lib
+#include <stdlib.h>
+#include "fec_hip.h"
+#include "fec_scheme.h"
+#include "fec_go.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"os"
+	"runtime"
+	"strconv"
+)
+
+// hipDevice is the GPU the schemes bind (FEC_HIP_DEVICE, default 0).
+func hipDevice() int {
+	if v, err := strconv.Atoi(os.Getenv("FEC_HIP_DEVICE")); err == nil {
+		return v
+	}
+	return 0
+}
+
+// useHIP selects the GPU schemes in NewSender / NewReceiver (manager.go:50-94) when
+// FEC_HIP=1, so the default stays the CPU path.
+func useHIP() bool { return os.Getenv("FEC_HIP") == "1" }
+
+// hipErr turns a fec_hip.h return code into an error (nil for 0).
+func hipErr(rc C.int) error {
+	if rc == 0 {
+		return nil
+	}
+	return errors.New(C.GoString(C.fec_strerror(rc)))
+}
+
+// lockThread keeps the goroutine on its OS thread from a C call to the fec_last_error read in
+// goErr (the message is thread-local): `defer lockThread()()`.
+func lockThread() func() {
+	runtime.LockOSThread()
+	return runtime.UnlockOSThread
+}
+
+// goErr turns a fec_go.h / fec_scheme.h return code into an error: FEC_ERR_SCHEME carries the
+// reference's own error text (fec_last_error, thread-local: the caller holds lockThread).
+func goErr(rc C.int) error {
+	if rc == 0 {
+		return nil
+	}
+	if msg := C.GoString(C.fec_last_error()); msg != "" {
+		return errors.New(msg)
+	}
+	return hipErr(rc)
+}

@@ -1,0 +1,465 @@
+/*
+ * fec_go_harness.c — issues exactly the C call sequence of the Go binding
+ * (go/internal/fec/{reed_solomon_hip,xor_hip,batch_hip}.go) over lib0xfec_hip.so, block by
+ * block, for the cases in a fixture file written by tests/test_go_harness.py from the reference's
+ * own test tables (tests/golden/reference_cases.json). The Go toolchain is absent from this image,
+ * so this file stands in for `go test -tags fechip`: every check, buffer layout, stride, mask and
+ * flag below is the Go file's, line for line in C, and the python test compares what it prints
+ * with the reference's expected frames / payloads / errors.
+ *
+ *   usage: fec_go_harness <fixture> direct|batch
+ *
+ * Fixture (one token list per line):
+ *   case <kind> <k> <m> <id> <smallest> <largest> <biggest> <tot_src> <tot_rep>
+ *   src <ssid> <cap> <hex|->        present source payload (cap = its Go capacity)
+ *   rep <pid> <cap> <hex|->         present repair payload
+ *   end
+ * kind: rs_repair rs_recover xor_repair xor_recover. Output per case:
+ *   result <n> err <text> | result <n> ok, then "frame <pid> <hex>" lines or "bytes <hex|->"
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "fec_go.h"
+#include "fec_hip.h"
+#include "fec_scheme.h"
+
+enum { MAX_PACKET = 1452, MAX_FEC_PAYLOAD = 1434, META = 2, MAX_SYM = 64 };
+
+typedef struct {
+    int present;
+    uint64_t id;
+    size_t len, cap;
+    uint8_t *p;
+} Sym;
+
+typedef struct {
+    char kind[32];
+    int k, m, tot_src, tot_rep, biggest;
+    uint64_t id, smallest, largest;
+    Sym src[MAX_SYM], rep[MAX_SYM];   /* in fixture order: Go map iteration order is arbitrary */
+    int nsrc, nrep;
+} Case;
+
+static char g_err[512];
+
+static int fail(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+#include <stdarg.h>
+static int fail(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return -1;
+}
+/* hipErr / goErr (hip_cgo.go) */
+static int hip_err(int rc) { return rc ? fail("%s", fec_strerror(rc)) : 0; }
+static int go_err(int rc) {
+    if (!rc) return 0;
+    const char *m = fec_last_error();
+    return m && *m ? fail("%s", m) : hip_err(rc);
+}
+
+static void print_hex(const uint8_t *p, size_t n) {
+    if (!n) {
+        fputs("-", stdout);
+        return;
+    }
+    for (size_t i = 0; i < n; ++i) printf("%02x", p[i]);
+}
+
+/* block.go:88-95 */
+static int is_complete(const Case *c) { return c->nsrc == c->tot_src; }
+static int is_recoverable(const Case *c) { return c->nsrc + c->nrep >= c->tot_src; }
+static Sym *source(Case *c, uint64_t ssid) {
+    for (int i = 0; i < c->nsrc; ++i)
+        if (c->src[i].id == ssid) return &c->src[i];
+    return NULL;
+}
+static Sym *repair(Case *c, uint64_t pid) {
+    for (int i = 0; i < c->nrep; ++i)
+        if (c->rep[i].id == pid) return &c->rep[i];
+    return NULL;
+}
+
+/* reed_solomon.go:70-89, as called by reed_solomon_hip.go */
+static int add_length(Case *c, uint64_t ssid, uint8_t *dst) {
+    Sym *s = source(c, ssid);
+    if (!s) return fail("block [%llu, %llu] is complete but SID %llu does not exist", (unsigned long long)c->smallest,
+                        (unsigned long long)c->largest, (unsigned long long)ssid);
+    const size_t L = META + (size_t)c->biggest;
+    if (L > s->cap) return fail("shard len (%zu) is greater than capacity of payload (%zu)", L, s->cap);
+    memset(dst, 0, L);
+    memcpy(dst, s->p, s->len < L ? s->len : L);
+    dst[c->biggest] = (uint8_t)(s->len >> 8);
+    dst[c->biggest + 1] = (uint8_t)(s->len & 0xFF);
+    return 0;
+}
+
+/* ---------------------------------------------------------------- reed_solomon_hip.go */
+
+static int rs_repair_direct(fec_ctx *ctx, Case *c) {
+    if (!is_complete(c)) return fail("block does not have enough source symbols to generate repair symbols");
+    if (c->biggest > MAX_FEC_PAYLOAD)
+        return fail("source symbol payload len is greater is too big for FEC headers. Max %d and got %d",
+                    MAX_FEC_PAYLOAD, c->biggest);
+    const size_t L = META + (size_t)c->biggest;
+    const int k = c->tot_src, n = c->tot_src + c->tot_rep;
+    uint8_t *buf = malloc((size_t)n * L);
+    for (int i = 0; i < k; ++i)
+        if (add_length(c, c->smallest + (uint64_t)i, buf + (size_t)i * L)) {
+            free(buf);
+            return -1;
+        }
+    int rc = fec_rs_encode_batch(ctx, k, c->tot_rep, L, 1, buf, (size_t)n * L, buf + (size_t)k * L, (size_t)n * L, L,
+                                 FEC_HOST);
+    if (rc) {
+        free(buf);
+        return fail("unable to make parity shards: %s", fec_strerror(rc));
+    }
+    printf("ok\n");
+    for (int i = 0; i < c->tot_rep; ++i) {
+        printf("frame %d ", i);
+        print_hex(buf + (size_t)(k + i) * L, L);
+        printf("\n");
+    }
+    free(buf);
+    return 0;
+}
+
+static int rs_recover_direct(fec_ctx *ctx, Case *c) {
+    if (!is_recoverable(c)) return fail("not enough present symbols to repair the missing ones");
+    if (is_complete(c)) {
+        printf("ok\nbytes -\n");
+        return 0;
+    }
+    const size_t L = META + (size_t)c->biggest;
+    const int k = c->tot_src, n = c->tot_src + c->tot_rep;
+    if (n > FEC_MAX_DECODE_SHARDS) return fail("too many shards for the GPU decoder");
+    uint8_t *buf = malloc((size_t)n * L);
+    uint32_t mask = 0;
+    int missing[MAX_SYM], nmiss = 0;
+    for (int i = 0; i < k; ++i) {
+        const uint64_t ssid = c->smallest + (uint64_t)i;
+        if (!source(c, ssid)) {
+            missing[nmiss++] = i;
+            continue;
+        }
+        if (add_length(c, ssid, buf + (size_t)i * L)) {
+            free(buf);
+            return -1;
+        }
+        mask |= 1u << i;
+    }
+    for (int r = 0; r < c->nrep; ++r) {
+        const int i = k + (int)c->rep[r].id;
+        if (c->rep[r].len != L) {
+            free(buf);
+            return fail("shard sizes do not match");
+        }
+        memcpy(buf + (size_t)i * L, c->rep[r].p, L);
+        mask |= 1u << i;
+    }
+    int32_t status = 0;
+    int rc = fec_rs_reconstruct_batch(ctx, k, c->tot_rep, L, 1, buf, (size_t)n * L, buf + (size_t)k * L,
+                                      (size_t)n * L, L, &mask, &status, FEC_HOST);
+    if (rc) {
+        free(buf);
+        return hip_err(rc);
+    }
+    uint8_t *out = malloc((size_t)nmiss * L + 1);
+    size_t total = 0;
+    for (int j = 0; j < nmiss; ++j) {   /* the payloads concatenated, each cut to its trailer */
+        const uint8_t *sh = buf + (size_t)missing[j] * L;
+        const size_t plen = (size_t)sh[c->biggest] << 8 | sh[c->biggest + 1];
+        memcpy(out + total, sh, plen);
+        total += plen;
+    }
+    printf("ok\nbytes ");
+    print_hex(out, total);
+    printf("\n");
+    free(out);
+    free(buf);
+    return 0;
+}
+
+/* ---------------------------------------------------------------- xor_hip.go */
+
+static void xor_frame(uint8_t *dst, const Sym *s, int biggest) {
+    memcpy(dst, s->p, s->len);
+    dst[biggest] ^= (uint8_t)(s->len >> 8);
+    dst[biggest + 1] ^= (uint8_t)(s->len & 0xFF);
+}
+
+static int xor_repair_direct(fec_ctx *ctx, Case *c) {
+    if (!is_complete(c)) return fail("block does not have enough source symbols to generate repair symbols");
+    if (c->tot_rep != 1) return fail("xor only supports 1 repair symbol. Expected 1, received %d", c->tot_rep);
+    if (c->biggest > MAX_FEC_PAYLOAD)
+        return fail("source symbol payload len is greater is too big for FEC headers. Max %d and got %d",
+                    MAX_FEC_PAYLOAD, c->biggest);
+    const size_t L = META + (size_t)c->biggest;
+    const int k = c->nsrc;
+    uint8_t *buf = calloc((size_t)(k + 1), L);
+    for (int i = 0; i < k; ++i) xor_frame(buf + (size_t)i * L, &c->src[i], c->biggest);
+    int rc = fec_xor_encode_batch(ctx, k, L, 1, buf, (size_t)(k + 1) * L, buf + (size_t)k * L, (size_t)(k + 1) * L, L,
+                                  FEC_HOST);
+    if (rc) {
+        free(buf);
+        return hip_err(rc);
+    }
+    printf("ok\nframe 0 ");
+    print_hex(buf + (size_t)k * L, L);
+    printf("\n");
+    free(buf);
+    return 0;
+}
+
+static int xor_recover_direct(fec_ctx *ctx, Case *c) {
+    if (!is_recoverable(c)) return fail("not enough present symbols to repair the missing ones");
+    if (is_complete(c)) {
+        printf("ok\nbytes -\n");
+        return 0;
+    }
+    const size_t L = MAX_PACKET;
+    const int k = c->nrep + c->nsrc;
+    uint8_t *buf = calloc((size_t)(k + 1), L);
+    int i = 0;
+    for (int r = 0; r < c->nrep; ++r, ++i) memcpy(buf + (size_t)i * L, c->rep[r].p, c->rep[r].len < L ? c->rep[r].len : L);
+    for (int s = 0; s < c->nsrc; ++s, ++i) xor_frame(buf + (size_t)i * L, &c->src[s], c->biggest);
+    int rc = fec_xor_encode_batch(ctx, k, L, 1, buf, (size_t)(k + 1) * L, buf + (size_t)k * L, (size_t)(k + 1) * L, L,
+                                  FEC_HOST);
+    if (rc) {
+        free(buf);
+        return hip_err(rc);
+    }
+    const uint8_t *rec = buf + (size_t)k * L;
+    const size_t plen = (size_t)rec[c->biggest] << 8 | rec[c->biggest + 1];
+    /* the block then holds the payload at every missing SSID of [smallest, largest]; complete? */
+    int filled = c->nsrc;
+    for (uint64_t ssid = c->smallest; ssid <= c->largest; ++ssid)
+        if (!source(c, ssid)) ++filled;
+    if (filled != c->tot_src) {
+        free(buf);
+        return fail("block is not complete after recovery");
+    }
+    printf("ok\nbytes ");
+    print_hex(rec, plen);
+    printf("\n");
+    free(buf);
+    return 0;
+}
+
+/* ---------------------------------------------------------------- batch_hip.go */
+
+static int batch_repair(Case *c, int scheme) {
+    int rc = 0;
+    /* NewBatchSender(id, k, m): XOR senders are (k, 1), manager.go:54-56 */
+    fec_go_encoder *e = fec_go_encoder_new(scheme, c->k, scheme == FEC_SCHEME_XOR ? 1 : c->m, 64, 0, &rc);
+    if (!e) return go_err(rc);
+    const int mm = scheme == FEC_SCHEME_XOR ? 1 : c->m;
+    /* BatchSender.Submit: repairSymbols' block-level checks on the Go block, in its order
+     * (reed_solomon.go:27-33, xor.go:15-25); then XOR takes the map in any order, RS the SSID
+     * window (reed_solomon.go:36-42) */
+    const uint8_t *ptrs[MAX_SYM];
+    size_t lens[MAX_SYM];
+    int n = 0;
+    const char *bad = NULL;
+    char msg[256];
+    if (!is_complete(c)) {
+        bad = "block does not have enough source symbols to generate repair symbols";
+    } else if (scheme == FEC_SCHEME_XOR && c->tot_rep != 1) {
+        snprintf(msg, sizeof msg, "xor only supports 1 repair symbol. Expected 1, received %d", c->tot_rep);
+        bad = msg;
+    } else if (c->biggest > MAX_FEC_PAYLOAD) {
+        snprintf(msg, sizeof msg, "source symbol payload len is greater is too big for FEC headers. Max %d and got %d",
+                 MAX_FEC_PAYLOAD, c->biggest);
+        bad = msg;
+    }
+    if (!bad && scheme == FEC_SCHEME_XOR) {
+        for (int i = 0; i < c->nsrc && n < c->k; ++i, ++n) {
+            ptrs[n] = c->src[i].p;
+            lens[n] = c->src[i].len;
+        }
+    } else if (!bad) {
+        for (int i = 0; i < c->tot_src && n < c->k; ++i, ++n) {
+            Sym *s = source(c, c->smallest + (uint64_t)i);
+            if (!s) {
+                snprintf(msg, sizeof msg, "block [%llu, %llu] is complete but SID %llu does not exist",
+                         (unsigned long long)c->smallest, (unsigned long long)c->largest,
+                         (unsigned long long)(c->smallest + (uint64_t)i));
+                bad = msg;
+                break;
+            }
+            ptrs[n] = s->p;
+            lens[n] = s->len;
+        }
+    }
+    if (bad) {
+        fec_go_encoder_free(e);
+        return fail("%s", bad);
+    }
+    if ((rc = fec_go_encoder_submit(e, c->id, ptrs, lens, n))) {
+        fec_go_encoder_free(e);
+        return go_err(rc);
+    }
+    uint64_t ids[4];
+    uint32_t rlen[4];
+    uint8_t *repairs = malloc((size_t)4 * mm * FEC_GO_SLOT);
+    size_t nb = 0;
+    rc = fec_go_encoder_poll(e, 1, ids, rlen, repairs, 4, &nb);
+    if (rc || nb != 1 || ids[0] != c->id) {
+        free(repairs);
+        fec_go_encoder_free(e);
+        return rc ? go_err(rc) : fail("poll returned %zu blocks", nb);
+    }
+    printf("ok\n");
+    for (int i = 0; i < mm; ++i) {
+        printf("frame %d ", i);
+        print_hex(repairs + (size_t)i * FEC_GO_SLOT, rlen[0]);
+        printf("\n");
+    }
+    free(repairs);
+    fec_go_encoder_free(e);
+    return 0;
+}
+
+static int batch_recover(Case *c, int scheme) {
+    /* BatchReceiver.Submit: the block-level checks first, on the Go block (recoverSymbolPayloads'
+     * order), then the pointers by SSID window */
+    if (!is_recoverable(c)) return fail("not enough present symbols to repair the missing ones");
+    if (is_complete(c)) {
+        printf("ok\nbytes -\n");
+        return 0;
+    }
+    int rc = 0;
+    fec_go_decoder *d = fec_go_decoder_new(scheme, c->k, c->m, 64, 0, &rc);
+    if (!d) return go_err(rc);
+    const int mm = scheme == FEC_SCHEME_XOR ? 1 : c->m;
+    /* BatchReceiver.Submit: k source pointers by SSID window, m repair pointers by ParityID */
+    const uint8_t *ptrs[2 * MAX_SYM];
+    size_t lens[2 * MAX_SYM];
+    static const uint8_t empty[1];
+    for (int i = 0; i < c->k; ++i) {
+        Sym *s = source(c, c->smallest + (uint64_t)i);
+        ptrs[i] = s ? (s->len ? s->p : empty) : NULL;
+        lens[i] = s ? s->len : 0;
+    }
+    for (int p = 0; p < mm; ++p) {
+        Sym *r = repair(c, (uint64_t)p);
+        ptrs[c->k + p] = r ? (r->len ? r->p : empty) : NULL;
+        lens[c->k + p] = r ? r->len : 0;
+    }
+    int staged = 0;
+    rc = fec_go_decoder_submit(d, c->id, c->smallest, c->largest, c->biggest, ptrs, lens, ptrs + c->k, lens + c->k,
+                               &staged);
+    if (rc) {
+        fec_go_decoder_free(d);
+        return go_err(rc);
+    }
+    if (!staged) {
+        fec_go_decoder_free(d);
+        printf("ok\nbytes -\n");
+        return 0;
+    }
+    uint64_t ids[4], offs[4];
+    uint32_t plen[4];
+    const size_t cap = (size_t)4 * c->k * MAX_PACKET;
+    uint8_t *out = malloc(cap);
+    size_t nb = 0;
+    rc = fec_go_decoder_poll(d, 1, ids, plen, offs, out, cap, 4, &nb);
+    if (rc || nb != 1 || ids[0] != c->id) {
+        free(out);
+        fec_go_decoder_free(d);
+        return rc ? go_err(rc) : fail("poll returned %zu blocks", nb);
+    }
+    printf("ok\nbytes ");
+    print_hex(out + offs[0], plen[0]);
+    printf("\n");
+    free(out);
+    fec_go_decoder_free(d);
+    return 0;
+}
+
+/* ---------------------------------------------------------------- driver */
+
+static uint8_t *unhex(const char *h, size_t cap, size_t *len) {
+    const size_t n = strcmp(h, "-") ? strlen(h) / 2 : 0;
+    uint8_t *p = calloc(cap > n ? cap : n ? n : 1, 1);   /* Go capacity beyond len: zeros */
+    for (size_t i = 0; i < n; ++i) {
+        unsigned v;
+        sscanf(h + 2 * i, "%2x", &v);
+        p[i] = (uint8_t)v;
+    }
+    *len = n;
+    return p;
+}
+
+static int run_case(Case *c, int batch) {
+    const int rs = !strncmp(c->kind, "rs_", 3), rep = strstr(c->kind, "repair") != NULL;
+    if (batch) {
+        const int scheme = rs ? FEC_SCHEME_REED_SOLOMON : FEC_SCHEME_XOR;
+        return rep ? batch_repair(c, scheme) : batch_recover(c, scheme);
+    }
+    /* newHipReedSolomonScheme / newHipXorScheme, then the one call */
+    fec_ctx *ctx = NULL;
+    int rc = fec_ctx_create(0, &ctx);
+    if (rc) return hip_err(rc);
+    if (rs && (rc = fec_rs_prepare(ctx, c->k, c->m))) {
+        fec_ctx_destroy(ctx);
+        return hip_err(rc);
+    }
+    if (rs) rc = rep ? rs_repair_direct(ctx, c) : rs_recover_direct(ctx, c);
+    else rc = rep ? xor_repair_direct(ctx, c) : xor_recover_direct(ctx, c);
+    fec_ctx_destroy(ctx);
+    return rc;
+}
+
+int main(int argc, char **argv) {
+    if (argc != 3) {
+        fprintf(stderr, "usage: %s <fixture> direct|batch\n", argv[0]);
+        return 2;
+    }
+    const int batch = !strcmp(argv[2], "batch");
+    FILE *f = fopen(argv[1], "r");
+    if (!f) {
+        perror(argv[1]);
+        return 2;
+    }
+    static char line[1 << 16];
+    static Case c;
+    int ncase = 0;
+    while (fgets(line, sizeof line, f)) {
+        char tag[16];
+        if (sscanf(line, "%15s", tag) != 1) continue;
+        if (!strcmp(tag, "case")) {
+            memset(&c, 0, sizeof c);
+            unsigned long long id, sm, lg;
+            sscanf(line, "case %31s %d %d %llu %llu %llu %d %d %d", c.kind, &c.k, &c.m, &id, &sm, &lg, &c.biggest,
+                   &c.tot_src, &c.tot_rep);
+            c.id = id;
+            c.smallest = sm;
+            c.largest = lg;
+        } else if (!strcmp(tag, "src") || !strcmp(tag, "rep")) {
+            unsigned long long id;
+            size_t cap;
+            static char hex[1 << 16];
+            sscanf(line, "%*s %llu %zu %65535s", &id, &cap, hex);
+            Sym *s = !strcmp(tag, "src") ? &c.src[c.nsrc++] : &c.rep[c.nrep++];
+            s->present = 1;
+            s->id = id;
+            s->cap = cap;
+            s->p = unhex(hex, cap, &s->len);
+        } else if (!strcmp(tag, "end")) {
+            printf("result %d ", ncase++);
+            g_err[0] = 0;
+            if (run_case(&c, batch)) printf("err %s\n", g_err);
+            for (int i = 0; i < c.nsrc; ++i) free(c.src[i].p);
+            for (int i = 0; i < c.nrep; ++i) free(c.rep[i].p);
+            fflush(stdout);
+        }
+    }
+    fclose(f);
+    return 0;
+}
