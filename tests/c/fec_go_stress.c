@@ -1,0 +1,224 @@
+/*
+ * fec_go_stress.c — many-block round trips through the batched Go ABI (include/fec_go.h), in
+ * the order a connection issues them: BatchSender submits complete blocks (payload pointers,
+ * ragged lengths 0..1434) and polls frames as they finish; BatchReceiver submits the blocks a
+ * lossy path delivers (lost sources, some repairs dropped, some blocks complete, some beyond
+ * repair) and polls payloads into a deliberately small buffer, so held-back results, batch
+ * rollover, both staging sets and backpressure are all exercised. Every recovered payload is
+ * compared with what was sent (recoverSymbolPayloads' result: the lost payloads in SSID order).
+ * Built normally and with host ASan/UBSan (tests/c/build.py); run by tests/test_sanitizers.py.
+ *
+ *   usage: fec_go_stress rs|xor <k> <m> <blocks> <max_blocks> <seed>
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "fec_go.h"
+
+static uint64_t g_rng;
+static uint64_t rnd(void) {   /* splitmix64 */
+    uint64_t z = (g_rng += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+#define CHECK(c, ...)                                             \
+    do {                                                          \
+        if (!(c)) {                                               \
+            fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__);  \
+            fprintf(stderr, __VA_ARGS__);                         \
+            fprintf(stderr, " [%s]\n", fec_last_error());         \
+            exit(1);                                              \
+        }                                                         \
+    } while (0)
+
+typedef struct {
+    uint8_t **pay;          /* k payloads */
+    size_t *len;
+    uint8_t *rep;           /* m repairs, FEC_GO_SLOT each */
+    uint32_t rlen;
+    int got_repairs;
+    int expect;             /* receiver: 0 nothing (complete), 1 payload, -1 error */
+    uint8_t *want;
+    size_t want_len;
+    int got;
+} Blk;
+
+int main(int argc, char **argv) {
+    if (argc != 7) {
+        fprintf(stderr, "usage: %s rs|xor k m blocks max_blocks seed\n", argv[0]);
+        return 2;
+    }
+    const int xor_ = !strcmp(argv[1], "xor");
+    const int scheme = xor_ ? FEC_SCHEME_XOR : FEC_SCHEME_REED_SOLOMON;
+    const int k = atoi(argv[2]), m = xor_ ? 1 : atoi(argv[3]);
+    const int nb = atoi(argv[4]);
+    const size_t maxb = (size_t)atoi(argv[5]);
+    g_rng = strtoull(argv[6], NULL, 0);
+    Blk *B = calloc((size_t)nb, sizeof *B);
+    int rc = 0;
+
+    /* ---- sender */
+    fec_go_encoder *e = fec_go_encoder_new(scheme, k, m, maxb, 0, &rc);
+    CHECK(e, "encoder_new rc=%d", rc);
+    uint64_t *ids = malloc(maxb * 8);
+    uint32_t *rl = malloc(maxb * 4);
+    uint8_t *rp = malloc(maxb * (size_t)m * FEC_GO_SLOT);
+    int polled = 0;
+    const uint8_t **ptrs = malloc((size_t)k * sizeof *ptrs);
+    for (int b = 0; b < nb; ++b) {
+        B[b].pay = malloc((size_t)k * sizeof(uint8_t *));
+        B[b].len = malloc((size_t)k * sizeof(size_t));
+        const int shape = (int)(rnd() % 4);   /* all full / ragged / tiny / one empty */
+        for (int i = 0; i < k; ++i) {
+            size_t L = shape == 0 ? 1434 : shape == 2 ? rnd() % 40 : rnd() % 1435;
+            if (shape == 3 && i == 0) L = 0;
+            B[b].len[i] = L;
+            B[b].pay[i] = malloc(L ? L : 1);
+            for (size_t j = 0; j < L; ++j) B[b].pay[i][j] = (uint8_t)rnd();
+            ptrs[i] = B[b].pay[i];
+        }
+        B[b].rep = malloc((size_t)m * FEC_GO_SLOT);
+        CHECK(fec_go_encoder_submit(e, (uint64_t)b, ptrs, B[b].len, k) == 0, "submit %d", b);
+        if (rnd() % 8 == 0) {   /* the run loop polls now and then */
+            size_t got = 0;
+            CHECK(fec_go_encoder_poll(e, 0, ids, rl, rp, maxb, &got) == 0, "poll");
+            for (size_t d = 0; d < got; ++d, ++polled) {
+                CHECK(ids[d] == (uint64_t)polled, "order %llu != %d", (unsigned long long)ids[d], polled);
+                B[polled].rlen = rl[d];
+                memcpy(B[polled].rep, rp + d * (size_t)m * FEC_GO_SLOT, (size_t)m * FEC_GO_SLOT);
+                B[polled].got_repairs = 1;
+            }
+        }
+    }
+    while (polled < nb) {
+        size_t got = 0;
+        CHECK(fec_go_encoder_poll(e, 1, ids, rl, rp, maxb, &got) == 0, "poll wait");
+        CHECK(got > 0, "no progress at %d", polled);
+        for (size_t d = 0; d < got; ++d, ++polled) {
+            CHECK(ids[d] == (uint64_t)polled, "order");
+            B[polled].rlen = rl[d];
+            memcpy(B[polled].rep, rp + d * (size_t)m * FEC_GO_SLOT, (size_t)m * FEC_GO_SLOT);
+            B[polled].got_repairs = 1;
+        }
+    }
+    fec_go_encoder_free(e);
+    for (int b = 0; b < nb; ++b) {
+        size_t big = 0;
+        for (int i = 0; i < k; ++i) big = B[b].len[i] > big ? B[b].len[i] : big;
+        CHECK(B[b].got_repairs && B[b].rlen == big + 2, "repair length block %d", b);
+    }
+
+    /* ---- receiver */
+    fec_go_decoder *d = fec_go_decoder_new(scheme, k, m, maxb, 0, &rc);
+    CHECK(d, "decoder_new rc=%d", rc);
+    const uint8_t **src = malloc((size_t)k * sizeof *src), **rep = malloc((size_t)m * sizeof *rep);
+    size_t *sl = malloc((size_t)k * 8), *rpl = malloc((size_t)m * 8);
+    const size_t out_cap = (size_t)k * 1434 + 7;   /* about one block's worth: forces hold-backs */
+    uint8_t *out = malloc(out_cap);
+    uint64_t *oid = malloc(maxb * 8), *off = malloc(maxb * 8);
+    uint32_t *ol = malloc(maxb * 4);
+    int next = 0, staged_n = 0, recovered = 0, complete = 0, failed = 0;
+    int *order = malloc((size_t)nb * sizeof(int));
+    for (int b = 0; b < nb; ++b) {
+        const int kind = (int)(rnd() % 10);   /* 0: complete, 1: beyond repair, else lossy */
+        int lost[64], nl = 0;
+        if (kind == 0) {
+            nl = 0;
+        } else if (kind == 1) {
+            nl = m + 1 <= k ? m + 1 : k;
+        } else {
+            nl = 1 + (int)(rnd() % (uint64_t)m);
+            if (nl > k) nl = k;
+        }
+        int is_lost[64] = {0};
+        for (int t = 0; t < nl;) {
+            const int i = (int)(rnd() % (uint64_t)k);
+            if (!is_lost[i]) {
+                is_lost[i] = 1;
+                lost[t++] = i;
+            }
+        }
+        (void)lost;
+        int keep_rep = m;
+        if (kind >= 2 && m > nl) keep_rep = nl + (int)(rnd() % (uint64_t)(m - nl + 1));   /* drop spare repairs */
+        int big = 0;
+        for (int i = 0; i < k; ++i) {
+            src[i] = is_lost[i] ? NULL : B[b].pay[i];
+            sl[i] = B[b].len[i];
+            if (!is_lost[i] && (int)B[b].len[i] > big) big = (int)B[b].len[i];
+        }
+        int kept = 0;
+        for (int p = 0; p < m; ++p) {
+            const int keep = kind == 1 ? 1 : kept < keep_rep && (rnd() % 2 || m - p <= keep_rep - kept);
+            rep[p] = keep ? B[b].rep + (size_t)p * FEC_GO_SLOT : NULL;
+            rpl[p] = B[b].rlen;
+            kept += keep;
+            if (keep) big = (int)B[b].rlen - 2;   /* block.go:80: a repair overwrites biggest */
+        }
+        const int present = (k - nl) + kept;
+        /* BatchReceiver.Submit's block-level checks (batch_hip.go) */
+        if (present < k) {
+            B[b].expect = -1;
+            ++failed;
+            continue;
+        }
+        if (nl == 0) {
+            B[b].expect = 0;
+            ++complete;
+            continue;
+        }
+        B[b].expect = 1;
+        B[b].want = malloc((size_t)nl * 1434 + 1);
+        B[b].want_len = 0;
+        for (int i = 0; i < k; ++i)
+            if (is_lost[i]) {
+                if (B[b].len[i]) memcpy(B[b].want + B[b].want_len, B[b].pay[i], B[b].len[i]);
+                B[b].want_len += B[b].len[i];
+            }
+        int st = 0;
+        rc = fec_go_decoder_submit(d, (uint64_t)b, (uint64_t)b * (uint64_t)k, (uint64_t)b * (uint64_t)k + (uint64_t)k - 1,
+                                   big, src, sl, rep, rpl, &st);
+        CHECK(rc == 0 && st == 1, "decoder submit %d rc=%d st=%d", b, rc, st);
+        order[staged_n++] = b;
+        if (rnd() % 4 == 0) {
+            size_t got = 0;
+            CHECK(fec_go_decoder_poll(d, 0, oid, ol, off, out, out_cap, maxb, &got) == 0, "dpoll");
+            for (size_t q = 0; q < got; ++q, ++next) {
+                const int bb = order[next];
+                CHECK(oid[q] == (uint64_t)bb, "dorder %llu != %d", (unsigned long long)oid[q], bb);
+                CHECK(ol[q] == B[bb].want_len && !memcmp(out + off[q], B[bb].want, B[bb].want_len),
+                      "payload mismatch block %d (%u vs %zu)", bb, ol[q], B[bb].want_len);
+                ++recovered;
+            }
+        }
+    }
+    while (next < staged_n) {
+        size_t got = 0;
+        CHECK(fec_go_decoder_poll(d, 1, oid, ol, off, out, out_cap, maxb, &got) == 0, "dpoll wait");
+        CHECK(got > 0, "decoder made no progress at %d of %d", next, staged_n);
+        for (size_t q = 0; q < got; ++q, ++next) {
+            const int bb = order[next];
+            CHECK(oid[q] == (uint64_t)bb, "dorder");
+            CHECK(ol[q] == B[bb].want_len && !memcmp(out + off[q], B[bb].want, B[bb].want_len),
+                  "payload mismatch block %d", bb);
+            ++recovered;
+        }
+    }
+    fec_go_decoder_free(d);
+    printf("ok blocks=%d recovered=%d complete=%d beyond_repair=%d\n", nb, recovered, complete, failed);
+    for (int b = 0; b < nb; ++b) {
+        for (int i = 0; i < k; ++i) free(B[b].pay[i]);
+        free(B[b].pay);
+        free(B[b].len);
+        free(B[b].rep);
+        free(B[b].want);
+    }
+    free(B);
+    free(ids), free(rl), free(rp), free(ptrs), free(src), free(rep), free(sl), free(rpl), free(out), free(oid),
+        free(off), free(ol), free(order);
+    return 0;
+}

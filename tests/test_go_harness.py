@@ -108,19 +108,17 @@ def _synthetic_cases(oracle):
 
 
 @pytest.fixture(scope="module")
-def harness(tmp_path_factory, fec):
-    d = tmp_path_factory.mktemp("goh")
-    exe = str(d / "fec_go_harness")
-    subprocess.run(["gcc", "-std=c11", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
-                    os.path.join(ROOT, "tests", "c", "fec_go_harness.c"), "-L", LIBDIR, "-l0xfec_hip",
-                    "-Wl,-rpath," + LIBDIR, "-o", exe], check=True)
-    return exe
+def harness(fec):
+    from native import binary
+    return binary("fec_go_harness")
 
 
-def _run(harness, cases, mode, tmp_path):
+def _run(harness, cases, mode, tmp_path, env=None):
     fx = tmp_path / ("cases_%s.txt" % mode)
     fx.write_text("\n".join(_case_text(kind, blk, k, m) for kind, blk, k, m, _, _ in cases) + "\n")
-    out = subprocess.run([harness, str(fx), mode], capture_output=True, text=True, timeout=300, check=True).stdout
+    p = subprocess.run([harness, str(fx), mode], capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-4000:]
+    out = p.stdout
     results, cur = [], None
     for line in out.splitlines():
         tag, _, rest = line.partition(" ")
