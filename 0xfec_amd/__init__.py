@@ -23,6 +23,10 @@ except ImportError:
 
 from ._build import LIB as _LIB_PATH
 
+# FEC_LIB_PATH selects another build of the same library: the host-ASan/UBSan build
+# (0xfec_amd/_san/lib0xfec_hip_san.so) that tests/test_sanitizers.py runs the CPU suite against
+_LIB_PATH = os.environ.get("FEC_LIB_PATH") or _LIB_PATH
+
 if not os.path.exists(_LIB_PATH):
     raise ImportError("lib0xfec_hip.so not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
                       "(or python 0xfec_amd/_build.py)")

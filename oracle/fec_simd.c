@@ -89,7 +89,7 @@ static void coefs_init(Coefs *cf, int rows, int cols, const uint8_t *coef) {
     cf->rows = rows;
     cf->cols = cols;
     cf->coef = (uint8_t *)malloc((size_t)rows * cols);
-    cf->nib = (uint8_t *)aligned_alloc(64, (size_t)rows * cols * 32 + 64);
+    cf->nib = (uint8_t *)aligned_alloc(64, ((size_t)rows * cols * 32 + 127) & ~(size_t)63);   /* C11: size a multiple of the alignment */
     cf->aff = (uint64_t *)malloc((size_t)rows * cols * 8);
     memcpy(cf->coef, coef, (size_t)rows * cols);
     for (int i = 0; i < rows * cols; ++i) {

@@ -22,6 +22,10 @@ def binary(name):
 
 def san_env(gpu):
     env = dict(os.environ)
+    if "libclang_rt.asan" in env.get("LD_PRELOAD", ""):
+        # our own sanitized CPU-suite run (tools/cpu_tests_sanitized.sh) preloads the shared ASan
+        # runtime for python; the test programs carry the static one
+        del env["LD_PRELOAD"]
     env.update(SAN_ENV)
     if gpu:
         env["ASAN_OPTIONS"] += ":detect_leaks=0"

@@ -114,3 +114,30 @@ def test_sanitized_harness_golden(golden, oracle, mode, tmp_path):
     cases = h._with_oracle_texts(h._golden_cases(golden), oracle) + h._synthetic_cases(oracle)
     h._check(h._run(binary("fec_go_harness_san"), cases, mode, tmp_path, env=san_env(gpu=True)), cases,
              texts=(mode == "direct"))
+
+
+def test_loaded_library_is_the_requested_build(fec):
+    """Under tools/cpu_tests_sanitized.sh (FEC_LIB_PATH) the process really runs the sanitized
+    library: it is the one mapped, and the ASan runtime is live in the process."""
+    want = os.environ.get("FEC_LIB_PATH")
+    maps = open("/proc/self/maps").read()
+    if not want:
+        assert os.path.basename(fec._LIB_PATH) == "lib0xfec_hip.so" and fec._LIB_PATH in maps
+        return
+    assert fec._LIB_PATH == want and want in maps
+    import ctypes
+    assert hasattr(ctypes.CDLL(None), "__asan_init")
+
+
+def test_host_suite_under_asan_ubsan(fec):
+    """The host-logic CPU tests (C-ABI checks, scheme/batch layers, wire codecs, Go-call harness)
+    pass against the ASan+UBSan build of the library (no GPU here: every HIP call fails cleanly)."""
+    if fec.device_count() > 0 or os.environ.get("FEC_LIB_PATH"):
+        pytest.skip("CPU container only, and not from inside the sanitized run itself")
+    tests = ["test_capi_exports.py", "test_batch_host.py", "test_scheme_host.py", "test_wire.py",
+             "test_go_harness.py", "test_sanitizers.py::test_loaded_library_is_the_requested_build"]
+    p = subprocess.run([os.path.join(ROOT, "tools", "cpu_tests_sanitized.sh"), "-x"] +
+                       [os.path.join(ROOT, "tests", t) for t in tests],
+                       capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
+    assert " passed" in p.stdout and "failed" not in p.stdout
