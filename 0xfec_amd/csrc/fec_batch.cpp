@@ -421,18 +421,17 @@ Error BatchDecoder::stage(Block& b, uint8_t* dst, size_t slot, Pending* p, bool*
     return Error::nil();
 }
 
-Error BatchDecoder::Submit(Block& b, RecoveredQueue* q, bool* staged) {
+template <class StageFn>
+Error BatchDecoder::submitWith(size_t want, RecoveredQueue* q, bool* staged, StageFn&& stage_fn) {
     if (staged) *staged = false;
     if (!q) return Error::text("nil recovered queue");
-    size_t want = kRepairPayloadMetadataLen + (size_t)std::max(0, b.biggestSourceSymbolLenSoFar);
-    for (auto& kv : b.pidToRepairPayload) want = std::max(want, kv.second.len);
     want = std::min(kDecSlotMax, std::max<size_t>(16, round16(want)));
     const size_t n = (size_t)k_ + m_;
     bool nothing = false;
     Pending p;
     if (!ready_) {   // validate before any device work
         std::vector<uint8_t> scratch(n * kDecSlotMax);
-        Error e = stage(b, scratch.data(), kDecSlotMax, &p, &nothing);
+        Error e = stage_fn(scratch.data(), kDecSlotMax, &p, &nothing);
         if (!e.ok() || nothing) return e;
         if (!(e = init()).ok()) return e;
     }
@@ -449,7 +448,7 @@ Error BatchDecoder::Submit(Block& b, RecoveredQueue* q, bool* staged) {
     }
     if (s->blocks.empty()) s->slot = want;
     const size_t idx = s->blocks.size();
-    Error e = stage(b, s->h_in + idx * n * s->slot, s->slot, &p, &nothing);
+    Error e = stage_fn(s->h_in + idx * n * s->slot, s->slot, &p, &nothing);
     if (!e.ok() || nothing) return e;
     s->h_masks[idx] = p.plan.mask;
     s->maxLen = std::max(s->maxLen, rs_ ? p.plan.len : s->slot);
@@ -458,6 +457,46 @@ Error BatchDecoder::Submit(Block& b, RecoveredQueue* q, bool* staged) {
     s->blocks.push_back(std::move(p));
     if (staged) *staged = true;
     return Error::nil();
+}
+
+Error BatchDecoder::Submit(Block& b, RecoveredQueue* q, bool* staged) {
+    size_t want = kRepairPayloadMetadataLen + (size_t)std::max(0, b.biggestSourceSymbolLenSoFar);
+    for (auto& kv : b.pidToRepairPayload) want = std::max(want, kv.second.len);
+    return submitWith(want, q, staged, [&](uint8_t* dst, size_t slot, Pending* p, bool* nothing) {
+        return stage(b, dst, slot, p, nothing);
+    });
+}
+
+Error BatchDecoder::SubmitPayloads(BlockID id, SourceSymbolID smallest, SourceSymbolID largest, int biggest,
+                                   const uint8_t* const* src, const size_t* slen, const uint8_t* const* rep,
+                                   const size_t* rlen, RecoveredQueue* q, bool* staged) {
+    if (staged) *staged = false;
+    if (!src || !slen || !rep || !rlen) return Error::text("invalid payload list");
+    size_t want = kRepairPayloadMetadataLen + (size_t)std::max(0, biggest);
+    for (int p = 0; p < m_; ++p)
+        if (rep[p]) want = std::max(want, rlen[p]);
+    return submitWith(want, q, staged, [&](uint8_t* dst, size_t slot, Pending* p, bool* nothing) {
+        *nothing = false;
+        p->id = id;
+        p->meta = Block{};
+        p->meta.id = id;
+        p->meta.totNumSourceSymbols = k_;
+        p->meta.totNumRepairSymbols = m_;
+        p->meta.smallestSSID = smallest;
+        p->meta.largestSSID = largest;
+        p->meta.biggestSourceSymbolLenSoFar = biggest;
+        if (rs_) {
+            Error e = rs_->stageRecoverPayloads(biggest, src, slen, rep, rlen, dst, slot, &p->plan);
+            if (e.ok()) *nothing = p->plan.nothing;
+            return e;
+        }
+        int count = 0;
+        Error e = xor_->stageRecoverPayloads(k_, m_, biggest, src, slen, rep, rlen, dst, slot, (size_t)k_, nothing,
+                                             &count);
+        p->plan = ReedSolomonScheme::RecoverPlan{};
+        p->plan.len = slot;
+        return e;
+    });
 }
 
 Error BatchDecoder::Flush() { return flushImpl(nullptr); }

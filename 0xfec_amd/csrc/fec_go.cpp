@@ -171,21 +171,12 @@ int fec_go_decoder_submit(fec_go_decoder* d, uint64_t block_id, uint64_t smalles
                           const uint8_t* const* repairs, const size_t* repair_lens, int* staged) {
     if (staged) *staged = 0;
     if (!d || !sources || !source_lens || !repairs || !repair_lens) return FEC_ERR_INVALID_ARG;
-    fec::Block b = fec::Block::New(block_id, d->k, d->m);
-    b.smallestSSID = smallest_ssid;
-    b.largestSSID = largest_ssid;
-    b.biggestSourceSymbolLenSoFar = biggest;
-    for (int i = 0; i < d->k; ++i) {
-        if (!sources[i]) continue;
-        if (source_lens[i] > fec::kMaxPacketBufferSize)
+    for (int i = 0; i < d->k; ++i)
+        if (sources[i] && source_lens[i] > fec::kMaxPacketBufferSize)
             return report(fec::Error::text("source payload longer than a packet buffer"));
-        b.ssidToSourcePayload[smallest_ssid + (uint64_t)i] =
-            fec::Slice::from(sources[i], source_lens[i], fec::kMaxPacketBufferSize);
-    }
-    for (int p = 0; p < d->m; ++p)
-        if (repairs[p]) b.pidToRepairPayload[(uint64_t)p] = fec::Slice::from(repairs[p], repair_lens[p], repair_lens[p]);
     bool st = false;
-    const int rc = report(d->dec->Submit(b, &d->q, &st));
+    const int rc = report(d->dec->SubmitPayloads(block_id, smallest_ssid, largest_ssid, biggest, sources, source_lens,
+                                                  repairs, repair_lens, &d->q, &st));
     if (staged) *staged = st ? 1 : 0;
     return rc;
 }

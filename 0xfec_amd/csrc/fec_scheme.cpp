@@ -276,6 +276,74 @@ Error ReedSolomonScheme::stageRecoverInput(Block& b, uint8_t* dst, size_t stride
     return Error::nil();
 }
 
+Error ReedSolomonScheme::stageRecoverPayloads(int biggest, const uint8_t* const* src, const size_t* slen,
+                                              const uint8_t* const* rep, const size_t* rlen, uint8_t* dst,
+                                              size_t stride, RecoverPlan* plan) {
+    // stageRecoverInput over the payloads themselves: the block is k sources (SSID order) and m
+    // repairs (ParityID order); every check of reed_solomon.go:92-124 and ReconstructData, in order
+    plan->nothing = false;
+    plan->missing.clear();
+    int nsrc = 0, nrep = 0;
+    for (int i = 0; i < k_; ++i) nsrc += src[i] != nullptr;
+    for (int p = 0; p < m_; ++p) nrep += rep[p] != nullptr;
+    if (nsrc + nrep < k_) return Error::text(kNotRecoverable);   // isRecoverable (block.go:88)
+    if (nsrc == k_) {
+        plan->nothing = true;   // isComplete: nil, nil
+        return Error::nil();
+    }
+    // addLengthToSourceSymbolPayload per present source (reed_solomon.go:70-89): a received
+    // source payload has the capacity of a packet buffer
+    const int shardLen = (int)kRepairPayloadMetadataLen + biggest;
+    for (int i = 0; i < k_; ++i) {
+        if (!src[i]) {
+            plan->missing.push_back(i);
+            continue;
+        }
+        if (shardLen > (int)kMaxPacketBufferSize)
+            return Error::text(fmt("shard len (%d) is greater than capacity of payload (%d)", shardLen,
+                                   (int)kMaxPacketBufferSize));
+        if (shardLen < (int)kRepairPayloadMetadataLen) return Error::text(fmt("shard len (%d) is negative", biggest));
+    }
+    // enc.ReconstructData: shard length = the first non-empty shard's; all non-empty ones equal
+    const int nsh = k_ + m_;
+    auto len_of = [&](int i) -> size_t {
+        return i < k_ ? (src[i] ? (size_t)shardLen : 0) : (rep[i - k_] ? rlen[i - k_] : 0);
+    };
+    size_t L = 0;
+    for (int i = 0; i < nsh && !L; ++i) L = len_of(i);
+    if (L == 0) return codec_error(FEC_ERR_SHARD_NO_DATA);
+    int present = 0;
+    uint32_t mask = 0;
+    for (int i = 0; i < nsh; ++i) {
+        const size_t li = len_of(i);
+        if (li == 0) continue;
+        if (li != L) return codec_error(FEC_ERR_SHARD_SIZE);
+        ++present;
+    }
+    if (present < k_) return codec_error(FEC_ERR_TOO_FEW_SHARDS);
+    if (nsh > FEC_MAX_DECODE_SHARDS) return codec_error(FEC_ERR_MAX_SHARD_NUM);
+    if (L > stride) return Error::text(fmt("shard len (%zu) exceeds the staging slot (%zu)", L, stride));
+    const size_t pad = std::min(stride, (L + 15) & ~(size_t)15) - L;
+    for (int i = 0; i < nsh; ++i) {
+        if (len_of(i) == 0) continue;
+        mask |= 1u << i;
+        uint8_t* d = dst + (size_t)i * stride;
+        if (i < k_) {   // payload[:shardLen] of a zeroed packet buffer, BE16 length at [biggest]
+            const size_t c = std::min(slen[i], L);
+            if (c) memcpy(d, src[i], c);
+            memset(d + c, 0, L - c);
+            d[biggest] = (uint8_t)((uint16_t)slen[i] >> 8);
+            d[biggest + 1] = (uint8_t)(slen[i] & 0xFF);
+        } else {
+            memcpy(d, rep[i - k_], L);
+        }
+        memset(d + L, 0, pad);
+    }
+    plan->len = L;
+    plan->mask = mask;
+    return Error::nil();
+}
+
 Error ReedSolomonScheme::finishRecover(const Block& b, const RecoverPlan& plan, const uint8_t* const* rebuilt,
                                        Slice* out) {
     // reed_solomon.go:126-135: concatenation of the rebuilt payloads, each cut to its trailer
@@ -326,14 +394,17 @@ Error ReedSolomonScheme::recoverSymbolPayloads(Block& b, Slice* out) {   // reed
 
 // One source payload as the XOR scheme folds it in (xor.go:44-56): payload bytes at
 // [0, len), big-endian uint16(len) XORed at [biggest, biggest+2), in an L-byte shard.
-static bool xor_frame(const Slice& p, int biggest, size_t L, uint8_t* dst) {
-    if (biggest < 0 || (size_t)biggest + 2 > L || p.len > L) return false;
+static bool xor_frame(const uint8_t* p, size_t len, int biggest, size_t L, uint8_t* dst) {
+    if (biggest < 0 || (size_t)biggest + 2 > L || len > L) return false;
     memset(dst, 0, L);
-    if (p.len) memcpy(dst, p.data(), p.len);
-    const uint16_t ln = (uint16_t)p.len;
+    if (len) memcpy(dst, p, len);
+    const uint16_t ln = (uint16_t)len;
     dst[biggest] ^= (uint8_t)(ln >> 8);
     dst[biggest + 1] ^= (uint8_t)(ln & 0xFF);
     return true;
+}
+static bool xor_frame(const Slice& p, int biggest, size_t L, uint8_t* dst) {
+    return xor_frame(p.data(), p.len, biggest, L, dst);
 }
 
 static Error xor_reduce(std::shared_ptr<Engine>& engine, std::vector<uint8_t>& shards, int count, size_t L,
@@ -415,6 +486,42 @@ Error XorScheme::stageRecoverInput(Block& b, uint8_t* dst, size_t stride, size_t
         memset(slot, 0, stride);
         if (!xor_frame(kv.second, b.biggestSourceSymbolLenSoFar, L, slot))
             return Error::text("source payload overruns the packet buffer");
+    }
+    for (size_t z = (size_t)i; z < slots; ++z) memset(dst + z * stride, 0, stride);
+    *count = i;
+    return Error::nil();
+}
+
+Error XorScheme::stageRecoverPayloads(int k, int m, int biggest, const uint8_t* const* src, const size_t* slen,
+                                     const uint8_t* const* rep, const size_t* rlen, uint8_t* dst, size_t stride,
+                                     size_t slots, bool* nothing, int* count) {
+    // stageRecoverInput over the payloads: repairs (ParityID order) whole, then the present
+    // sources (SSID order) framed, as xor.go:78-84 walks the block's maps
+    *nothing = false;
+    int nsrc = 0, nrep = 0;
+    for (int i = 0; i < k; ++i) nsrc += src[i] != nullptr;
+    for (int p = 0; p < m; ++p) nrep += rep[p] != nullptr;
+    if (nsrc + nrep < k) return Error::text(kNotRecoverable);
+    if (nsrc == k) {
+        *nothing = true;
+        return Error::nil();
+    }
+    const size_t L = std::min(stride, kMaxPacketBufferSize);
+    const size_t n = (size_t)(nrep + nsrc);
+    if (n > slots) return Error::text(fmt("%zu XOR inputs exceed the %zu staging slots", n, slots));
+    int i = 0;
+    for (int p = 0; p < m; ++p) {
+        if (!rep[p]) continue;
+        if (rlen[p] > L) return Error::text("repair payload longer than the packet buffer");
+        uint8_t* slot = dst + (size_t)(i++) * stride;
+        memset(slot, 0, stride);
+        if (rlen[p]) memcpy(slot, rep[p], rlen[p]);
+    }
+    for (int j = 0; j < k; ++j) {
+        if (!src[j]) continue;
+        uint8_t* slot = dst + (size_t)(i++) * stride;
+        memset(slot, 0, stride);
+        if (!xor_frame(src[j], slen[j], biggest, L, slot)) return Error::text("source payload overruns the packet buffer");
     }
     for (size_t z = (size_t)i; z < slots; ++z) memset(dst + z * stride, 0, stride);
     *count = i;

@@ -174,6 +174,14 @@ public:
     // recoverable block. A block that is already complete is the reference's nil, nil: nothing
     // is staged or delivered (*staged = false).
     Error Submit(Block& b, RecoveredQueue* q, bool* staged = nullptr);
+    // Zero-copy form for integrations that keep their own block bookkeeping (the Go binding,
+    // include/fec_go.h): the block's SSID range, biggest and payload pointers (src: k entries,
+    // SSID smallest + i; rep: m entries, ParityID p; nullptr = absent), validated and framed
+    // straight into pinned staging with the same checks, errors and order as Submit. Nothing is
+    // retained after the call.
+    Error SubmitPayloads(BlockID id, SourceSymbolID smallest, SourceSymbolID largest, int biggest,
+                         const uint8_t* const* src, const size_t* slen, const uint8_t* const* rep, const size_t* rlen,
+                         RecoveredQueue* q, bool* staged = nullptr);
     Error Flush();
     Error Poll(size_t* blocks = nullptr);
     Error Drain(size_t* blocks = nullptr);
@@ -206,6 +214,9 @@ private:
         : scheme_(scheme), k_(k), m_(m), maxBlocks_(maxBlocks), engine_(std::move(e)) {}
     Error init();
     Error stage(Block& b, uint8_t* dst, size_t slot, Pending* p, bool* nothing);
+    // Submit's body: `stage_fn(dst, slot, &pending, &nothing)` validates and stages one block
+    template <class StageFn>
+    Error submitWith(size_t want, RecoveredQueue* q, bool* staged, StageFn&& stage_fn);
     Error flushImpl(size_t* delivered);
     Error waitSet(Set& s);
     Error deliver(Set& s, size_t* blocks);

@@ -141,6 +141,11 @@ public:
         std::vector<int> missing;   // ascending missing data shard indices
     };
     Error stageRecoverInput(Block& b, uint8_t* dst, size_t stride, RecoverPlan* plan);
+    // The same for a block given as its payloads (fec_go_decoder_submit: no Block built):
+    // src[i] = the payload of SSID smallestSSID + i or nullptr, read with the capacity of a
+    // packet buffer (kMaxPacketBufferSize); rep[p] = the payload of ParityID p or nullptr.
+    Error stageRecoverPayloads(int biggest, const uint8_t* const* src, const size_t* slen, const uint8_t* const* rep,
+                               const size_t* rlen, uint8_t* dst, size_t stride, RecoverPlan* plan);
     // The rest of recoverSymbolPayloads: rebuilt[r] = the rebuilt shard of plan.missing[r].
     Error finishRecover(const Block& b, const RecoverPlan& plan, const uint8_t* const* rebuilt, Slice* out);
 
@@ -163,6 +168,10 @@ public:
     // recoverSymbolPayloads up to the XOR loop (same checks): repairs and framed sources into
     // `slots` slots of `stride` bytes (unused slots zeroed); *nothing when already complete.
     Error stageRecoverInput(Block& b, uint8_t* dst, size_t stride, size_t slots, bool* nothing, int* count);
+    // The same for a block given as its k source / m repair payload pointers (nullptr absent).
+    Error stageRecoverPayloads(int k, int m, int biggest, const uint8_t* const* src, const size_t* slen,
+                               const uint8_t* const* rep, const size_t* rlen, uint8_t* dst, size_t stride,
+                               size_t slots, bool* nothing, int* count);
     // The rest of recoverSymbolPayloads from the XOR of the inputs (len bytes of it).
     Error finishRecover(Block& b, const uint8_t* rec, size_t len, Slice* out);
 

@@ -6,6 +6,7 @@
                         C++ (C-ABI, scheme/batch layers, wire codecs, Go ABI) compiled with
                         AddressSanitizer + UBSan on the host side only (-Xarch_host), kernels
                         unchanged (device code is never instrumented)
+  go_batch_bench        host-resident throughput of the batched Go ABI (tools/go_batch_bench.c)
   fuzz_wire             libFuzzer target for the frame parsers (tests/fuzz/fuzz_wire.cpp)
 
 Called by __graft_entry__.build(); rebuilds only what is stale."""
@@ -87,6 +88,11 @@ def build():
         if _stale(exe, [src, san_lib] + hdrs):
             jobs.append([CLANG, "-std=c11", "-O1", "-Wall", "-Werror"] + SAN_C +
                         ["-I", INCLUDE, src, "-L", SAN, "-l0xfec_hip_san", "-Wl,-rpath," + SAN, "-o", exe])
+    gb_src = os.path.join(ROOT, "tools", "go_batch_bench.c")
+    gb = os.path.join(BIN, "go_batch_bench")
+    if _stale(gb, [gb_src, lib] + hdrs):
+        jobs.append(["gcc", "-std=c11", "-O2", "-Wall", "-Werror", "-I", INCLUDE, gb_src, "-L", PKG, "-l0xfec_hip",
+                     "-Wl,-rpath," + PKG, "-o", gb])
     fz_src = [os.path.join(ROOT, "tests", "fuzz", "fuzz_wire.cpp"), os.path.join(PKG, "csrc", "fec_wire.cpp")]
     fz = os.path.join(BIN, "fuzz_wire")
     if _stale(fz, fz_src + hdrs):
