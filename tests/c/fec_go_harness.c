@@ -17,10 +17,12 @@
  * kind: rs_repair rs_recover xor_repair xor_recover. Output per case:
  *   result <n> err <text> | result <n> ok, then "frame <pid> <hex>" lines or "bytes <hex|->"
  */
+#define _DEFAULT_SOURCE
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "fec_go.h"
 #include "fec_hip.h"
@@ -461,5 +463,10 @@ int main(int argc, char **argv) {
         }
     }
     fclose(f);
-    return 0;
+    /* leave without running the HIP runtime's shared-library finalizers: under the host-ASan
+     * build, ASan's interception of the HSA allocator trips a check in the runtime's teardown
+     * (libamdhip64 __cxa_finalize), after all work is done and checked */
+    fflush(stdout);
+    fflush(stderr);
+    _exit(0);
 }

@@ -10,10 +10,12 @@
  *
  *   usage: fec_go_stress rs|xor <k> <m> <blocks> <max_blocks> <seed>
  */
+#define _DEFAULT_SOURCE
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "fec_go.h"
 
@@ -220,5 +222,10 @@ int main(int argc, char **argv) {
     free(B);
     free(ids), free(rl), free(rp), free(ptrs), free(src), free(rep), free(sl), free(rpl), free(out), free(oid),
         free(off), free(ol), free(order);
-    return 0;
+    /* leave without running the HIP runtime's shared-library finalizers: under the host-ASan
+     * build, ASan's interception of the HSA allocator trips a check in the runtime's teardown
+     * (libamdhip64 __cxa_finalize), after all work is done and checked */
+    fflush(stdout);
+    fflush(stderr);
+    _exit(0);
 }

@@ -22,3 +22,10 @@ cd "$R"
 python tools/pmc_traffic.py "$O/pmc_fetch" "$O/pmc_write" "$O/pmc_traffic.json"
 timeout -k 10 300 python -u tools/config_bench.py > "$O/config_bench.log" 2>&1
 grep -v amdgpu.ids "$O/config_bench.log"
+# host-resident Go-ABI throughput (one host thread, submit + poll), then counters for the
+# configs furthest from the roofline
+for c in "rs 8 4 32768 4096" "rs 20 10 16384 2048" "rs 2 1 65536 8192" "xor 2 1 65536 8192"; do
+    timeout -k 10 90 "$R/0xfec_amd/_bin/go_batch_bench" $c
+done > "$O/go_batch_bench.log" 2>&1
+cat "$O/go_batch_bench.log"
+tools/pmc_configs.sh "$TAG/counters" "rs1624,rs23"
