@@ -163,7 +163,6 @@ Error BatchEncoder::slotFor(size_t want, Set** out) {
 
 Error BatchEncoder::SubmitPayloads(BlockID id, const uint8_t* const* payloads, const size_t* lens, int count,
                                    RepairQueue* q) {
-    if (!q) return Error::text("nil repair queue");
     if (count < 0 || (count && (!payloads || !lens))) return Error::text("invalid payload list");
     // repairSymbols' checks for a block holding exactly these payloads: complete (reed_solomon.go:27,
     // xor.go:15) -> (XOR: one repair symbol) -> size (reed_solomon.go:31, xor.go:23)
@@ -191,6 +190,13 @@ Error BatchEncoder::SubmitPayloads(BlockID id, const uint8_t* const* payloads, c
 }
 
 Error BatchEncoder::Flush() { return flushImpl(nullptr); }
+
+bool BatchEncoder::PopRaw(RawBlock* out) {
+    if (raw_.empty()) return false;
+    *out = std::move(raw_.front());
+    raw_.pop_front();
+    return true;
+}
 
 Error BatchEncoder::flushImpl(size_t* delivered) {
     Set& s = sets_[cur_];
@@ -238,6 +244,16 @@ Error BatchEncoder::retire(Set& s) {
     if (!e.ok()) return e;
     for (size_t i = 0; i < s.blocks.size(); ++i) {
         const Pending& p = s.blocks[i];
+        if (!p.q) {   // no queue: keep the payloads, back to back, for PopRaw
+            RawBlock rb;
+            rb.id = p.id;
+            rb.len = p.len;
+            rb.bytes.resize((size_t)m_ * p.len);
+            for (int j = 0; j < m_; ++j)
+                memcpy(rb.bytes.data() + (size_t)j * p.len, s.h_out + (i * (size_t)m_ + j) * s.slot, p.len);
+            raw_.push_back(std::move(rb));
+            continue;
+        }
         Ready r{p.q, p.id, {}};
         r.payloads.reserve((size_t)m_);
         for (int j = 0; j < m_; ++j) {

@@ -25,9 +25,7 @@ using fec::cabi::report;
 
 struct fec_go_encoder {
     int k = 0, m = 0;
-    std::unique_ptr<fec::BatchEncoder> enc;
-    // the encoder's frames land here (no connection queue: the Go side keeps its own)
-    fec::RepairQueue q{nullptr, std::numeric_limits<size_t>::max()};
+    std::unique_ptr<fec::BatchEncoder> enc;   // blocks go in without a queue (PopRaw)
     struct Building {
         std::vector<std::vector<uint8_t>> payload;
         std::vector<bool> have;
@@ -87,7 +85,7 @@ int fec_go_encoder_commit(fec_go_encoder* e, uint64_t block_id) {
                 ptrs.push_back(it->second.payload[i].data());
                 lens.push_back(it->second.payload[i].size());
             }
-    const int rc = report(e->enc->SubmitPayloads(block_id, ptrs.data(), lens.data(), (int)ptrs.size(), &e->q));
+    const int rc = report(e->enc->SubmitPayloads(block_id, ptrs.data(), lens.data(), (int)ptrs.size(), nullptr));
     if (it != e->building.end()) e->building.erase(it);
     return rc;
 }
@@ -95,7 +93,7 @@ int fec_go_encoder_commit(fec_go_encoder* e, uint64_t block_id) {
 int fec_go_encoder_submit(fec_go_encoder* e, uint64_t block_id, const uint8_t* const* payloads, const size_t* lens,
                           int count) {
     if (!e) return FEC_ERR_INVALID_ARG;
-    return report(e->enc->SubmitPayloads(block_id, payloads, lens, count, &e->q));
+    return report(e->enc->SubmitPayloads(block_id, payloads, lens, count, nullptr));
 }
 
 int fec_go_encoder_flush(fec_go_encoder* e) { return e ? report(e->enc->Flush()) : FEC_ERR_INVALID_ARG; }
@@ -107,15 +105,14 @@ int fec_go_encoder_poll(fec_go_encoder* e, int wait, uint64_t* block_ids, uint32
     const fec::Error err = wait ? e->enc->Drain() : e->enc->Poll();
     if (!err.ok()) return report(err);
     size_t d = 0;
-    for (; d < max_blocks && e->q.Len() >= (size_t)e->m; ++d)
-        for (int i = 0; i < e->m; ++i) {
-            const fec::RepairFrame* f = e->q.Peek();
-            block_ids[d] = f->block_id;
-            repair_len[d] = (uint32_t)f->payload.len;
-            memcpy(repairs + (d * (size_t)e->m + (size_t)i) * FEC_GO_SLOT, f->payload.data(),
-                   std::min(f->payload.len, (size_t)FEC_GO_SLOT));
-            e->q.Pop();
-        }
+    fec::BatchEncoder::RawBlock rb;
+    for (; d < max_blocks && e->enc->PopRaw(&rb); ++d) {
+        block_ids[d] = rb.id;
+        repair_len[d] = (uint32_t)rb.len;
+        const size_t c = std::min(rb.len, (size_t)FEC_GO_SLOT);
+        for (int i = 0; i < e->m; ++i)
+            memcpy(repairs + (d * (size_t)e->m + (size_t)i) * FEC_GO_SLOT, rb.bytes.data() + (size_t)i * rb.len, c);
+    }
     if (nblocks) *nblocks = d;
     return report(fec::Error::nil());
 }

@@ -79,7 +79,17 @@ public:
     // packet buffers into pinned staging (one copy; nothing retained after the call, so cgo
     // may pass Go slices). Same checks and errors as repairSymbols for a block holding exactly
     // these payloads.
+    // q == nullptr: the block's payloads are kept for PopRaw instead of going to a queue.
     Error SubmitPayloads(BlockID id, const uint8_t* const* payloads, const size_t* lens, int count, RepairQueue* q);
+    // Encoded blocks submitted without a queue (the Go ABI, include/fec_go.h, whose caller keeps
+    // its own queue), in submission order: the m repair payloads back to back, len bytes each.
+    struct RawBlock {
+        BlockID id = 0;
+        size_t len = 0;
+        std::vector<uint8_t> bytes;
+    };
+    bool PopRaw(RawBlock* out);
+    size_t RawLen() const { return raw_.size(); }
     // Start encoding the staged blocks (asynchronous). No-op when nothing is staged.
     Error Flush();
     // Deliver the frames of every completed batch (non-blocking); *blocks = blocks delivered.
@@ -114,6 +124,7 @@ private:
         size_t maxLen = 0;          // largest L of this batch
         bool inFlight = false;
     };
+    std::deque<RawBlock> raw_;
     struct Ready {                  // an encoded block whose frames wait for queue room
         RepairQueue* q;
         BlockID id;

@@ -129,9 +129,9 @@ int main(int argc, char **argv) {
         best_d = td < best_d ? td : best_d;
     }
     const double bytes = (double)nb * k * len;
-    printf("{\"scheme\": \"%s(%d,%d)\", \"blocks\": %d, \"max_blocks\": %zu, \"payload_len\": %zu, "
+    printf("{\"scheme\": \"%s(%d,%d)\", \"host_threads\": 1, \"blocks\": %d, \"max_blocks\": %zu, \"payload_len\": %zu, "
            "\"encode_GBps\": %.3f, \"encode_blocks_per_s\": %.0f, \"decode_GBps\": %.3f, \"decode_blocks_per_s\": %.0f}\n",
-           xr ? "XOR" : "RS", k, k + m, nb, maxb, len, bytes / best_e / 1e9, nb / best_e, bytes / best_d / 1e9,
+           xr ? "XOR" : "RS", k, xr ? 1 : k + m, nb, maxb, len, bytes / best_e / 1e9, nb / best_e, bytes / best_d / 1e9,
            nb / best_d);
     return 0;
 }
