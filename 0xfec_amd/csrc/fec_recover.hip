@@ -62,15 +62,42 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint8_t* slice = smem + (size_t)wave * direct_wave_bytes(k);
     const uint32_t total = a.nblocks * a.cps;
+    const uint32_t all = low_mask(k + m), kmask = low_mask(k);
+    // Statuses (recover: e rebuilt; in place: 0; failures as rs_plan_kernel reports them) and
+    // failure flags of blocks [64 w, 64 w + 64), w = this wave's launch index: one coalesced mask
+    // load and one coalesced status store per 64 blocks. (Stored by the waves of each block, the
+    // 4-byte statuses of neighbouring blocks were scattered partial-line stores from different
+    // waves: RS(2,3) 45 -> 57 us with a status array.)
+    {
+        const uint32_t w = blockIdx.x * (kThreads / 64) + wave;
+        if (w * 64u < a.nblocks) {   // wave-uniform
+            const uint32_t b = w * 64u + lane;
+            uint32_t bad = 0;
+            if (b < a.nblocks) {
+                const uint32_t mask = a.masks[b] & all;
+                const uint32_t e = k - __popc(mask & kmask);
+                int32_t st = a.max_out ? (int32_t)e : 0;
+                if (e != 0 && (uint32_t)__popc(mask) < k) {
+                    st = -4;   // FEC_ERR_TOO_FEW_SHARDS
+                    bad = 1;
+                } else if (a.max_out && e > a.max_out) {
+                    st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
+                    bad = 2;
+                }
+                if (a.status) a.status[b] = st;
+            }
+            const bool f1 = __ballot(bad == 1) != 0, f2 = __ballot(bad == 2) != 0;
+            if (lane == 0 && (f1 || f2)) atomicOr(a.err, (f1 ? 1 : 0) | (f2 ? 2 : 0));
+        }
+    }
     const uint32_t i0 = xcd_order(a.swz) * kThreads + (wave << 6);
     if (i0 >= total) return;
     const uint32_t bfirst = fdiv(i0, a.div_cps);
     const uint32_t nb = fdiv(min(i0 + 63u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
-    const uint32_t all = low_mask(k + m), kmask = low_mask(k);
     const uint32_t mine = lane < nb ? a.masks[bfirst + lane] : 0u;   // the wave's masks in one load
 
     // A block with two or more erasures (and enough shards) sends the whole wave to the
-    // worklist of rs_recover_hard_kernel; it writes that wave's statuses.
+    // worklist of rs_recover_hard_kernel.
     bool hard = false;
     for (uint32_t g = 0; g < nb; ++g) {
         const uint32_t mask = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)g) & all;
@@ -81,32 +108,16 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
         if (lane == 0) a.hard[kHardList + atomicAdd(a.hard, 1u)] = i0;
         return;
     }
-    // Per block (uniform): status (recover: e rebuilt; in place: 0) and failures, as
-    // rs_plan_kernel reports them, and the table row (E0 * m + R0) of a single-erasure block.
+    // Per block (uniform): the table row (E0 * m + R0) of a single-erasure block.
     uint32_t row[kWaveBlocks] = {0, 0, 0};
-    int32_t stg[kWaveBlocks] = {0, 0, 0};
 #pragma unroll
     for (uint32_t g = 0; g < kWaveBlocks; ++g) {
         if (g >= nb) break;
         const uint32_t mask = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)g) & all;
         const uint32_t e = k - __popc(mask & kmask);
-        int32_t st = a.max_out ? (int32_t)e : 0;
-        if (e != 0 && (uint32_t)__popc(mask) < k) {
-            st = -4;   // FEC_ERR_TOO_FEW_SHARDS
-            if (lane == 0) atomicOr(a.err, 1);
-        } else if (a.max_out && e > a.max_out) {
-            st = -1;   // FEC_ERR_INVALID_ARG
-            if (lane == 0) atomicOr(a.err, 2);
-        } else if (e == 1) {
+        if (e == 1 && (uint32_t)__popc(mask) >= k && !(a.max_out && e > a.max_out))
             row[g] = (__ffs(~mask & kmask) - 1) * m + (__ffs(mask >> k) - 1);   // m >= 1 here: k < 32
-        }
-        stg[g] = st;
     }
-    // statuses: lane g < nb writes block g's, one store, issued after the data loads (a store
-    // before them would make the loads wait for its completion)
-    auto store_status = [&]() {
-        if (a.status && lane < nb) a.status[bfirst + lane] = lane == 0 ? stg[0] : lane == 1 ? stg[1] : stg[2];
-    };
     // The PermTab rows of the wave's blocks into its LDS slice, prepared while the data loads are
     // in flight (vector loads return in order: LDS writes that wait for a row load wait for that
     // load only, and scalar loads are counted apart).
@@ -184,7 +195,6 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
 #pragma unroll
         for (int j = 0; j < K - 1; ++j) x[j] = ld16<NTL>(d0 + (uint64_t)(j + (j >= (int)E0)) * ss);
         x[K - 1] = ld16<NTL>(p0);
-        store_status();
         if constexpr (TAB == 0) rows_to_lds(wt, tv, lane, nb * 2 * k);
         else expand_rows();
         if (!work) return;
@@ -200,7 +210,6 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
             }
         }
     } else {
-        store_status();
         if constexpr (TAB == 0) rows_to_lds(wt, tv, lane, nb * 2 * k);
         else expand_rows();
         if (!work) return;
@@ -334,7 +343,9 @@ static hipError_t direct_dispatch(const ReconArgs& a, int ncu, hipStream_t s) {
     else
         e = a.k == 2 ? direct_launch<2, POL, 1>(a, cw, s) : a.k == 8 ? direct_launch<8, POL, 1>(a, cw, s)
                                                                      : direct_launch<0, POL, 1>(a, cw, s);
-    if (e != hipSuccess || a.m < 2) return e;   // m = 1: two erasures always leave too few shards
+    // m = 1: two erasures always leave too few shards; one output slot: a block with two or more
+    // erasures is an error the direct kernel reports itself (nothing goes to the worklist)
+    if (e != hipSuccess || a.m < 2 || a.max_out == 1) return e;
     if (a.maxe <= 2) return hard_launch<2, POL>(a, ncu, s);
     if (a.maxe <= 4) return hard_launch<4, POL>(a, ncu, s);
     if (a.maxe <= 8) return hard_launch<8, POL>(a, ncu, s);

@@ -22,14 +22,20 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 PAYLOAD, L, S = 1200, 1202, 1216
 
 
-def timed(torch, fn, iters):
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        fn()
-    e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / iters
+def timed(torch, fn, iters, bursts=5):
+    """ms per launch: the median of `bursts` back-to-back bursts of `iters` launches (the first
+    burst after a change of kernel runs up to 25 % slow for the 40-us RS(2,3) launches,
+    tools/cb_probe.py)."""
+    r = []
+    for _ in range(bursts):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        r.append(s.elapsed_time(e) / iters)
+    return sorted(r)[len(r) // 2]
 
 
 def make_data(torch, B, k, g):

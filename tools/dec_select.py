@@ -30,6 +30,7 @@ def main():
     out = torch.zeros((B, 1, S), dtype=torch.uint8, device="cuda")
     erased = torch.randint(0, k, (B,), device="cuda")
     masks = ((1 << (k + m)) - 1 - (1 << erased)).to(torch.int32)
+    status = torch.zeros((B,), dtype=torch.int32, device="cuda")
     dp, pp, op = data.data_ptr(), par.data_ptr(), out.data_ptr()
     D = dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=1, dec_ipl=0, dec_direct=1)
     variants = {"direct (default)": D,
@@ -39,10 +40,13 @@ def main():
                 "plan + wave ipl2": dict(D, dec_direct=0, dec_ipl=2)}
     for w in (4, 6):
         variants["direct wpc%d" % w] = dict(D, dec_wpc=w)
+    variants["direct + status array"] = dict(D, _status=1)
     base = codec.set_tuning(**D)
+    use_status = [False]
 
     def run():
-        codec.rs_recover_raw(k, m, L, B, dp, k * S, pp, m * S, S, masks.data_ptr(), op, S, 1, None)
+        codec.rs_recover_raw(k, m, L, B, dp, k * S, pp, m * S, S, masks.data_ptr(), op, S, 1,
+                             status.data_ptr() if use_status[0] else None)
 
     def t(iters):
         run()
@@ -58,19 +62,23 @@ def main():
     run()
     torch.cuda.synchronize()
     ref = out.clone()
+    def tune(kv):
+        use_status[0] = bool(kv.get("_status"))
+        codec.set_tuning(**{x: y for x, y in kv.items() if not x.startswith("_")})
+
     for n, kv in variants.items():
-        codec.set_tuning(**kv)
+        tune(kv)
         out.zero_()
         run()
         torch.cuda.synchronize()
         assert torch.equal(out, ref), n
-        codec.set_tuning(**base)
+        tune(D)
     res = {n: [] for n in variants}
     for _ in range(args.rounds):
         for n, kv in variants.items():
-            codec.set_tuning(**kv)
+            tune(kv)
             res[n].append(t(args.iters))
-            codec.set_tuning(**base)
+            tune(D)
     byts = B * (k + 1) * L
     print(json.dumps({"shape": "RS(%d,%d) x %d" % (k, k + m, B),
                       "median_us_TBps_best": {n: [round(sorted(v)[len(v) // 2] * 1e6, 1),
