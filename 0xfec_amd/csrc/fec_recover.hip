@@ -353,7 +353,10 @@ static hipError_t direct_dispatch(const ReconArgs& a, int ncu, hipStream_t s) {
 }
 
 hipError_t launch_rs_recover_direct(const ReconArgs& a, int ncu, hipStream_t s) {
-    return (g_tune.dec_nt & 3) ? direct_dispatch<3>(a, ncu, s) : direct_dispatch<0>(a, ncu, s);
+    // cache policy: 3 non-temporal loads and stores (default), 2 plain loads + non-temporal
+    // stores, else plain
+    const int nt = g_tune.dec_nt & 3;
+    return nt == 3 ? direct_dispatch<3>(a, ncu, s) : nt == 2 ? direct_dispatch<2>(a, ncu, s) : direct_dispatch<0>(a, ncu, s);
 }
 
 }  // namespace fk

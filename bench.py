@@ -35,7 +35,7 @@ SHARD_STRIDE = 1216              # 16-byte aligned device slot per shard
 HBM_PEAK = 8.0e12                # MI355X HBM3E spec, bytes/s (MI355X_MICROARCH.md)
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of this bench (separate passes, tools/pmc_traffic.py,
 # gfx950 FETCH_SIZE x2 correction): HBM bytes per launch of each codec kernel
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "pmc_traffic_v10.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02", "pmc_traffic_r02b.json")
 
 
 def encode_kernel_name(k, m):
@@ -361,8 +361,8 @@ def main():
         dominant, dom_bw, dom_bytes = enc_kernel + ">", enc_bw, enc_bytes
         traffic, traffic_src = committed_traffic(enc_kernel)
     else:
-        dominant, dom_bw, dom_bytes = "rs_plan_kernel+rs_reconstruct_kernel (recover)", dec_bw, dec_bytes
-        traffic, traffic_src = committed_traffic("rs_reconstruct_kernel")
+        dominant, dom_bw, dom_bytes = "rs_recover_direct_kernel<%d" % k, dec_bw, dec_bytes
+        traffic, traffic_src = committed_traffic("rs_recover_direct_kernel")
 
     if rank == 0:
         out = {
@@ -392,10 +392,10 @@ def main():
                 "encode": {"ms": round(enc_ms, 4), "GB/s": round(enc_bw / 1e9, 1), "bytes": enc_bytes,
                            "frac": round(enc_bw / HBM_PEAK, 4)},
                 "decode": {"ms": round(dec_ms, 4), "GB/s": round(dec_bw / 1e9, 1), "bytes": dec_bytes,
-                           "frac": round(dec_bw / HBM_PEAK, 4), "api": "fec_rs_recover_batch (plan + kernel)"},
+                           "frac": round(dec_bw / HBM_PEAK, 4), "api": "fec_rs_recover_batch (direct single-erasure kernel, no plan launch)"},
                 "decode_inplace": {"ms": round(inplace_ms, 4),
                                    "GB/s": round(dec_bytes / (inplace_ms / 1e3) / 1e9, 1),
-                                   "api": "fec_rs_reconstruct_batch (plan + kernel), not in the step"},
+                                   "api": "fec_rs_reconstruct_batch (direct kernel, in place), not in the step"},
                 "step_frac": round((enc_bytes + dec_bytes) / ((enc_ms + dec_ms) / 1000.0) / HBM_PEAK, 4),
             },
             "check": {"roundtrip_full_batch": ok_roundtrip, "encode_vs_oracle_64_blocks": ok_parity},

@@ -16,25 +16,35 @@ from collections import defaultdict
 
 
 def per_kernel(d, counter):
+    """Mean counter value per dispatch of each kernel's largest launch size (Grid_Size): bench.py
+    also launches its kernels on small batches (checks, host-resident leg), which must not be
+    averaged into the full-size launches the roofline is quoted on."""
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     vals = defaultdict(list)
+    grids = {}
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if row.get("Counter_Name") != counter:
                     continue
                 name = row.get("Kernel_Name", "?")
-                vals[(name, row.get("Dispatch_Id"))].append(float(row["Counter_Value"]))
+                key = (name, row.get("Dispatch_Id"))
+                vals[key].append(float(row["Counter_Value"]))
+                grids[key] = int(float(row.get("Grid_Size") or 0))
+    biggest = defaultdict(int)
+    for (name, did), g in grids.items():
+        biggest[name] = max(biggest[name], g)
     out = defaultdict(list)
-    for (name, _), v in vals.items():
-        out[name].append(sum(v))            # sum over XCD / instance rows of one dispatch
-    return {k: sum(v) / len(v) for k, v in out.items()}, {k: len(v) for k, v in out.items()}
+    for (name, did), v in vals.items():
+        if grids[(name, did)] == biggest[name]:
+            out[name].append(sum(v))            # sum over XCD / instance rows of one dispatch
+    return {k: sum(v) / len(v) for k, v in out.items()}, {k: len(v) for k, v in out.items()}, dict(biggest)
 
 
 def main():
     fdir, wdir, dst = sys.argv[1:4]
-    fetch, nf = per_kernel(fdir, "FETCH_SIZE")
-    write, nw = per_kernel(wdir, "WRITE_SIZE")
+    fetch, nf, grid = per_kernel(fdir, "FETCH_SIZE")
+    write, nw, _ = per_kernel(wdir, "WRITE_SIZE")
     res = {}
     for k in sorted(set(fetch) | set(write)):
         if not k.startswith("void fk::"):
@@ -42,6 +52,7 @@ def main():
         f_kb, w_kb = fetch.get(k), write.get(k)
         res[k] = {
             "dispatches": [nf.get(k, 0), nw.get(k, 0)],
+            "grid_size": grid.get(k),
             "FETCH_SIZE_KiB": f_kb, "WRITE_SIZE_KiB": w_kb,
             "read_bytes_corrected": None if f_kb is None else 2 * f_kb * 1024,
             "write_bytes": None if w_kb is None else w_kb * 1024,
