@@ -977,7 +977,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 20 ? &fk::g_tune.dec_ipl : key == 21 ? &fk::g_tune.dec_diag
               : key == 22 ? &fk::g_tune.enc_dyadic : key == 23 ? &fk::g_tune.dec_direct
               : key == 24 ? &fk::g_tune.dec_sorted : key == 25 ? &fk::g_tune.dec_fixk
-              : key == 26 ? &fk::g_tune.host_chunk : nullptr;
+              : key == 26 ? &fk::g_tune.host_chunk : key == 27 ? &fk::g_tune.dir_wpc
+              : key == 28 ? &fk::g_tune.dir_nt : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

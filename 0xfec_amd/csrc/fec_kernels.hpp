@@ -161,6 +161,10 @@ struct Tuning {
     int dec_sorted = 1;       // multi-erasure codes (plan path, shards of 32+ chunks): sorted parallel plans
     int dec_ipl = 0;          // wave-form reconstruct items per lane: 1; 2 loaded together; 3: 2 one
                               // after the other (one plan stage); 0: 2 for k <= 4, else 1
+    int dir_wpc = -1;         // direct decode residency (workgroups per CU, 0 uncapped); -1: by shape,
+                              // 4 for k >= 8 (RS(8,12) +3.6 %), uncapped below (RS(2,3): caps cost 10-60 %)
+    int dir_nt = -1;          // direct decode cache policy (3 nt loads + stores, 2 plain loads + nt
+                              // stores, 0 plain); -1: by shape, 2 for k <= 4 (RS(2,3) +8 %), else 3
 };
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):

@@ -317,7 +317,8 @@ static hipError_t direct_launch(const ReconArgs& a, const CoefWords& cw, hipStre
     const uint64_t total = (uint64_t)a.nblocks * a.cps;
     const int grid = (int)((total + kThreads - 1) / kThreads);
     if (grid == 0) return hipSuccess;
-    const size_t lds = occupancy_lds(g_tune.dec_wpc, 4 * direct_wave_bytes(a.k));
+    const int wpc = g_tune.dir_wpc >= 0 ? g_tune.dir_wpc : (a.k >= 8 ? 4 : 0);
+    const size_t lds = occupancy_lds(wpc, 4 * direct_wave_bytes(a.k));
     hipLaunchKernelGGL((rs_recover_direct_kernel<K, POL, TAB>), dim3(grid), dim3(kThreads), lds, s, a, cw);
     return hipGetLastError();
 }
@@ -355,7 +356,7 @@ static hipError_t direct_dispatch(const ReconArgs& a, int ncu, hipStream_t s) {
 hipError_t launch_rs_recover_direct(const ReconArgs& a, int ncu, hipStream_t s) {
     // cache policy: 3 non-temporal loads and stores (default), 2 plain loads + non-temporal
     // stores, else plain
-    const int nt = g_tune.dec_nt & 3;
+    const int nt = g_tune.dir_nt >= 0 ? (g_tune.dir_nt & 3) : (a.k <= 4 ? 2 : 3);
     return nt == 3 ? direct_dispatch<3>(a, ncu, s) : nt == 2 ? direct_dispatch<2>(a, ncu, s) : direct_dispatch<0>(a, ncu, s);
 }
 

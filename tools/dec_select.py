@@ -32,17 +32,16 @@ def main():
     masks = ((1 << (k + m)) - 1 - (1 << erased)).to(torch.int32)
     status = torch.zeros((B,), dtype=torch.int32, device="cuda")
     dp, pp, op = data.data_ptr(), par.data_ptr(), out.data_ptr()
-    D = dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=1, dec_ipl=0, dec_direct=1, dec_nt=3)
+    D = dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=1, dec_ipl=0, dec_direct=1, dec_nt=3, dir_wpc=-1, dir_nt=-1)
     variants = {"direct (default)": D,
                 "direct, PermTab rows by vector load": dict(D, dec_direct=2),
                 "direct noswz": dict(D, dec_swz=0),
-                "plan + wave": dict(D, dec_direct=0),
-                "plan + wave ipl2": dict(D, dec_direct=0, dec_ipl=2)}
-    for w in (4, 6):
-        variants["direct wpc%d" % w] = dict(D, dec_wpc=w)
+                "plan + wave": dict(D, dec_direct=0)}
+    for w in (0, 3, 4, 6):
+        for nt, nm in ((3, "nt"), (2, "plain loads")):
+            variants["direct wpc%d, %s" % (w, nm)] = dict(D, dir_wpc=w, dir_nt=nt)
     variants["direct + status array"] = dict(D, _status=1)
-    variants["direct, plain loads, nt stores"] = dict(D, dec_nt=2)
-    variants["direct, plain loads and stores"] = dict(D, dec_nt=0)
+    variants["direct, plain loads and stores"] = dict(D, dir_nt=0)
     base = codec.set_tuning(**D)
     use_status = [False]
 
