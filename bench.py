@@ -389,10 +389,14 @@ def main():
                          "traffic_unit": "GB per launch", "traffic_source": traffic_src,
                          "kernel": dominant, "algorithmic_bytes_per_launch": dom_bytes},
             "kernels": {
+                # read_frac: the HBM-read roofline of SURVEY.md 8(d) (reads alone: k shards per block)
                 "encode": {"ms": round(enc_ms, 4), "GB/s": round(enc_bw / 1e9, 1), "bytes": enc_bytes,
-                           "frac": round(enc_bw / HBM_PEAK, 4)},
+                           "frac": round(enc_bw / HBM_PEAK, 4),
+                           "read_frac": round(B * k * L / (enc_ms / 1000.0) / HBM_PEAK, 4)},
                 "decode": {"ms": round(dec_ms, 4), "GB/s": round(dec_bw / 1e9, 1), "bytes": dec_bytes,
-                           "frac": round(dec_bw / HBM_PEAK, 4), "api": "fec_rs_recover_batch (direct single-erasure kernel, no plan launch)"},
+                           "frac": round(dec_bw / HBM_PEAK, 4),
+                           "read_frac": round(B * k * L / (dec_ms / 1000.0) / HBM_PEAK, 4),
+                           "api": "fec_rs_recover_batch (direct single-erasure kernel, no plan launch)"},
                 "decode_inplace": {"ms": round(inplace_ms, 4),
                                    "GB/s": round(dec_bytes / (inplace_ms / 1e3) / 1e9, 1),
                                    "api": "fec_rs_reconstruct_batch (direct kernel, in place), not in the step"},

@@ -5,7 +5,7 @@ toolchain in the image), so tests/c/fec_go_harness.c restates each Go function's
 line (same checks, buffer layout, strides, present masks and FEC_HOST flags) and is run over
 
   * every case of reed_solomon_test.go / xor_test.go (tests/golden/reference_cases.json), and
-  * seeded synthetic blocks (RS(20,10) / RS(8,4) / RS(6,2) / XOR(k,1), ragged payload lengths,
+  * seeded synthetic blocks (RS(20,10) / RS(8,4) / RS(6,2) / RS(2,1) (config #1's code) / XOR(k,1), ragged payload lengths,
     random losses) whose expected frames / payloads / errors come from the oracle's scheme
     layer (oracle/oracle.py, restating reed_solomon.go / xor.go).
 
@@ -65,7 +65,7 @@ def _synthetic_cases(oracle):
     """Seeded blocks as a connection builds them (manager.go:123-227), expected from the oracle."""
     rng = np.random.default_rng(0x60FEC)
     cases = []
-    for kind_base, k, m in (("rs", 20, 10), ("rs", 8, 4), ("rs", 6, 2), ("xor", 2, 1), ("xor", 5, 1)):
+    for kind_base, k, m in (("rs", 20, 10), ("rs", 8, 4), ("rs", 6, 2), ("rs", 2, 1), ("xor", 2, 1), ("xor", 5, 1)):
         for t in range(4):
             bid = int(rng.integers(0, 1 << 20))
             lens = rng.integers(0, 1435, k)
@@ -205,7 +205,7 @@ def test_go_call_sequence_synthetic(harness, oracle, mode, tmp_path):
 def test_synthetic_cases_are_well_formed(oracle):
     """The seeded blocks cover repairs, every loss count up to m, and the too-many-losses error."""
     cases = _synthetic_cases(oracle)
-    assert len(cases) == 40
+    assert len(cases) == 48
     errs = [c for c in cases if c[4][0] == "err"]
-    assert len(errs) == 3 and all(e[4][1] == "not enough present symbols to repair the missing ones" for e in errs)
-    assert sum(1 for c in cases if c[4][0] == "bytes" and c[4][1]) == 17
+    assert len(errs) == 4 and all(e[4][1] == "not enough present symbols to repair the missing ones" for e in errs)
+    assert sum(1 for c in cases if c[4][0] == "bytes" and c[4][1]) == 20

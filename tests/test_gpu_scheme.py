@@ -133,3 +133,25 @@ def test_manager_reed_solomon_20_10(S, oracle):
             out, err = rcv.handle_repair_frame(bid, pid, rp)
             assert err is None
         assert out == b"".join(payloads[i] for i in lost)
+
+
+def test_config1_plumbing_rs23_one_block(S, oracle):
+    """BASELINE.json config #1: RS rate-2/3 (k=2, n=3), one block of two 1200-B symbols. The
+    repair is row `03 02` of the default matrix applied to the framed shards (SURVEY.md 8a);
+    losing shard 0 and recovering it returns the 1200-B payload (reed_solomon.go:128-133)."""
+    rng = np.random.default_rng(0x0FEC)
+    p = [bytes(rng.integers(0, 256, 1200, dtype=np.uint8)) for _ in range(2)]
+    s, err = S.new_reed_solomon_scheme(2, 1)
+    assert err is None
+    b = S.Block.literal(id=0, tot_src=2, tot_rep=1, biggest=1200, smallest=0, largest=1,
+                        sources={0: (p[0], 1452), 1: (p[1], 1452)})
+    frames, err = s.repair_symbols(b)
+    assert err is None and len(frames) == 1 and frames[0][:2] == (0, 0)
+    shards = [np.frombuffer(x + bytes([0x04, 0xB0]), dtype=np.uint8) for x in p]   # trailer 1200 = 0x04B0
+    t3, t2 = (np.array([oracle.gf_mul(c, x) for x in range(256)], dtype=np.uint8) for c in (3, 2))
+    want = bytes(t3[shards[0]] ^ t2[shards[1]])
+    assert frames[0][2] == want and len(want) == 1202
+    rb = S.Block.literal(id=0, tot_src=2, tot_rep=1, biggest=1200, smallest=0, largest=1,
+                         sources={1: (p[1], 1452)}, repairs={0: frames[0][2]})
+    got, err = s.recover_symbol_payloads(rb)
+    assert err is None and got == p[0]
