@@ -91,8 +91,8 @@ def build():
     gb_src = os.path.join(ROOT, "tools", "go_batch_bench.c")
     gb = os.path.join(BIN, "go_batch_bench")
     if _stale(gb, [gb_src, lib] + hdrs):
-        jobs.append(["gcc", "-std=c11", "-O2", "-Wall", "-Werror", "-I", INCLUDE, gb_src, "-L", PKG, "-l0xfec_hip",
-                     "-Wl,-rpath," + PKG, "-o", gb])
+        jobs.append(["gcc", "-std=c11", "-O2", "-Wall", "-Werror", "-pthread", "-I", INCLUDE, gb_src, "-L", PKG,
+                     "-l0xfec_hip", "-Wl,-rpath," + PKG, "-o", gb])
     fz_src = [os.path.join(ROOT, "tests", "fuzz", "fuzz_wire.cpp"), os.path.join(PKG, "csrc", "fec_wire.cpp")]
     fz = os.path.join(BIN, "fuzz_wire")
     if _stale(fz, fz_src + hdrs):
