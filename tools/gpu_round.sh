@@ -12,6 +12,8 @@ O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$O/pytest_gpu.log" 2>&1
 tail -2 "$O/pytest_gpu.log"
+timeout -k 10 120 python -u -c 'import __graft_entry__ as g; g.smoke(); print("smoke ok")' > "$O/smoke.log" 2>&1
+tail -1 "$O/smoke.log"
 timeout -k 10 300 python -u bench.py > "$O/bench.log" 2>&1
 tail -1 "$O/bench.log"
 cd /tmp && export TMPDIR=/tmp
@@ -19,12 +21,13 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/pr
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$O/pmc_fetch.log" 2>&1
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$O/pmc_write.log" 2>&1
 cd "$R"
-python tools/pmc_traffic.py "$O/pmc_fetch" "$O/pmc_write" "$O/pmc_traffic.json"
+python tools/pmc_traffic.py "$O/pmc_fetch" "$O/pmc_write" "$O/pmc_traffic.json" > /dev/null
+python tools/trace_summary.py "$O/prof" "$O/kernel_trace_summary.json" > /dev/null
 timeout -k 10 300 python -u tools/config_bench.py > "$O/config_bench.log" 2>&1
 grep -v amdgpu.ids "$O/config_bench.log"
 # host-resident Go-ABI throughput (one host thread, submit + poll), then counters for the
 # configs furthest from the roofline
-for c in "rs 8 4 32768 4096" "rs 20 10 16384 2048" "rs 2 1 65536 8192" "xor 2 1 65536 8192"; do
+for c in "rs 8 4 65536 2048 1200 1" "rs 8 4 65536 2048 1200 8" "rs 20 10 32768 1024 1200 1" "rs 20 10 32768 1024 1200 8" "rs 2 1 131072 4096 1200 8" "xor 2 1 131072 4096 1200 8"; do
     timeout -k 10 90 "$R/0xfec_amd/_bin/go_batch_bench" $c
 done > "$O/go_batch_bench.log" 2>&1
 cat "$O/go_batch_bench.log"
