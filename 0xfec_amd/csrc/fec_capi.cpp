@@ -73,9 +73,27 @@ constexpr uint64_t kMaxItems = uint64_t(1) << 31;
 
 }  // namespace
 
+// Device scratch of the kernels enqueued on one stream: decode plan records, the direct decode's
+// multi-erasure worklist and the queue kernels' ticket counters. Each stream the ctx launches on
+// (its own / the caller's, and one per host-path staging set) has its own, so launches that
+// overlap on different streams never share one (nor free one the other stream still reads).
+struct Work {
+    uint8_t* d_plans = nullptr;
+    size_t plans_cap = 0;
+    uint32_t* d_hard = nullptr;   // fk::kHardList + waves words; count and done rewound by the kernel
+    size_t hard_cap = 0;
+    uint32_t* d_ctr = nullptr;    // fk::kCtrWords ticket counters, self-rewinding
+    void release() {
+        for (void* q : {(void*)d_plans, (void*)d_hard, (void*)d_ctr})
+            if (q) (void)hipFree(q);
+        *this = Work{};
+    }
+};
+
 // One staging set of the host-resident path (pinned host + device buffers, a stream, an event):
 // with two, chunk c+1 is staged and copied up while chunk c is coded and copied down.
 struct HostSet {
+    Work w;                      // scratch of the kernels on this set's stream
     uint8_t* h_in = nullptr;
     uint8_t* h_out = nullptr;
     uint8_t* d_in = nullptr;
@@ -95,12 +113,9 @@ struct fec_ctx {
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
     std::map<std::pair<int, int>, Code> codes;
-    uint8_t* d_plans = nullptr;
-    size_t plans_cap = 0;
-    uint32_t* d_hard = nullptr;   // direct decode's multi-erasure worklist (fk::kHardList + waves words)
-    size_t hard_cap = 0;
+    Work main;               // scratch of the kernels on `own` / the caller's stream
+    Work* work = &main;      // scratch of the kernels on `stream` (on_stream switches both)
     int* d_err = nullptr;    // [0] sticky device-path error, [1] host-path error
-    uint32_t* d_ctr = nullptr;   // ticket counters of the queue kernels (fk::kCtrWords words)
     uint8_t* h_stage = nullptr;
     uint8_t* d_stage = nullptr;
     size_t stage_cap = 0;
@@ -210,30 +225,48 @@ static int get_code(fec_ctx* ctx, int k, int m, Code** out) {
     }
     auto res = ctx->codes.emplace(key, std::move(c));
     *out = &res.first->second;
+    // the uploads above are plain hipMemcpy (null stream, and from pageable memory they may return
+    // before the DMA lands): finish them before a kernel on a non-blocking ctx stream reads a table
+    HIP_TRY(hipDeviceSynchronize());
     return FEC_OK;
 }
 
 static int grow_plans(fec_ctx* ctx, size_t bytes) {
-    if (bytes <= ctx->plans_cap) return FEC_OK;
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    if (ctx->d_plans) HIP_TRY(hipFree(ctx->d_plans));
-    ctx->d_plans = nullptr;
-    ctx->plans_cap = 0;
-    HIP_TRY(hipMalloc(&ctx->d_plans, bytes));
-    ctx->plans_cap = bytes;
+    Work& w = *ctx->work;
+    if (bytes <= w.plans_cap) return FEC_OK;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));   // the only stream that reads this workspace
+    if (w.d_plans) HIP_TRY(hipFree(w.d_plans));
+    w.d_plans = nullptr;
+    w.plans_cap = 0;
+    HIP_TRY(hipMalloc(&w.d_plans, bytes));
+    w.plans_cap = bytes;
     return FEC_OK;
 }
 
 static int grow_hard(fec_ctx* ctx, size_t waves) {
+    Work& w = *ctx->work;
     const size_t words = fk::kHardList + waves;
-    if (words <= ctx->hard_cap) return FEC_OK;
+    if (words <= w.hard_cap) return FEC_OK;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    if (ctx->d_hard) HIP_TRY(hipFree(ctx->d_hard));
-    ctx->d_hard = nullptr;
-    ctx->hard_cap = 0;
-    HIP_TRY(hipMalloc(&ctx->d_hard, words * 4));
-    HIP_TRY(hipMemset(ctx->d_hard, 0, fk::kHardList * 4));   // count and done: rewound by the kernel after
-    ctx->hard_cap = words;
+    if (w.d_hard) HIP_TRY(hipFree(w.d_hard));
+    w.d_hard = nullptr;
+    w.hard_cap = 0;
+    HIP_TRY(hipMalloc(&w.d_hard, words * 4));
+    // count and done (the kernel rewinds them after each use). Ordered on the stream: a plain
+    // hipMemset runs on the null stream, which does not order against the ctx's non-blocking
+    // streams, so the next direct kernel could append to a worklist still holding garbage.
+    HIP_TRY(hipMemsetAsync(w.d_hard, 0, fk::kHardList * 4, ctx->stream));
+    w.hard_cap = words;
+    return FEC_OK;
+}
+
+// The queue kernels' ticket counters of the current stream's workspace (zeroed once; the kernels
+// rewind them).
+static int ensure_ctr(fec_ctx* ctx) {
+    Work& w = *ctx->work;
+    if (w.d_ctr) return FEC_OK;
+    HIP_TRY(hipMalloc(&w.d_ctr, fk::kCtrWords * sizeof(uint32_t)));
+    HIP_TRY(hipMemsetAsync(w.d_ctr, 0, fk::kCtrWords * sizeof(uint32_t), ctx->stream));
     return FEC_OK;
 }
 
@@ -312,7 +345,11 @@ static int rs_encode_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks
             a.rot = fk::g_tune.rotate ? fk::line_rotation(ss, cps) : 0;
             a.swz = (uint32_t)fk::g_tune.xcd_swz;
             if (fk::fixed_encode_applies((uint32_t)k, (uint32_t)mr)) {
-                a.ctr = ctx->d_ctr;
+                if (fk::g_tune.enc_queue) {
+                    const int rc = ensure_ctr(ctx);
+                    if (rc) return rc;
+                }
+                a.ctr = ctx->work->d_ctr;
                 a.dytabs = (r0 == 0 && mr == code->m) ? code->d_dytabs : nullptr;
                 HIP_TRY(fk::launch_rs_encode_fixed(a, ctx->ncu, ctx->stream));
                 continue;
@@ -357,7 +394,7 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         const size_t nb = std::min(per_launch, nblocks - b0);
         fk::PlanArgs p{};
         p.masks = masks + b0;
-        p.plans = ctx->d_plans;
+        p.plans = ctx->work->d_plans;
         p.status = status ? status + b0 : nullptr;
         p.err = err;
         p.prows = code->d_prows;
@@ -377,7 +414,7 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         a.pbs = pbs;
         a.ss = ss;
         a.pss = pss;
-        a.plans = ctx->d_plans;
+        a.plans = ctx->work->d_plans;
         a.k = k;
         a.len = (uint32_t)len;
         a.cps = cps;
@@ -404,7 +441,8 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
             a.single = code->d_single;
             a.single_coef = code->d_single_coef;
             a.single_coef_host = code->single_coef.data();
-            a.hard = ctx->d_hard;
+            a.hard = ctx->work->d_hard;
+            a.hard_cap = (uint32_t)(ctx->work->hard_cap - fk::kHardList);
             HIP_TRY(fk::launch_rs_recover_direct(a, ctx->ncu, ctx->stream));
             continue;
         }
@@ -628,13 +666,16 @@ static int host_set_grow(fec_ctx* ctx, HostSet& s, size_t in_bytes, size_t out_b
     return FEC_OK;
 }
 
-// Run `fn` with the ctx's kernels enqueued on `s` (the host path's set stream).
+// Run `fn` with the ctx's kernels enqueued on the host-path set's stream, with that set's scratch.
 template <class F>
-static int on_stream(fec_ctx* ctx, hipStream_t s, F fn) {
+static int on_stream(fec_ctx* ctx, HostSet& hs, F fn) {
     hipStream_t keep = ctx->stream;
-    ctx->stream = s;
+    Work* keep_w = ctx->work;
+    ctx->stream = hs.s;
+    ctx->work = &hs.w;
     const int rc = fn();
     ctx->stream = keep;
+    ctx->work = keep_w;
     return rc;
 }
 
@@ -679,7 +720,7 @@ static int host_encode(fec_ctx* ctx, Code* code, int k, int m, size_t len, size_
             });
             HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, nb * k * ssd, hipMemcpyHostToDevice, s.s));
         }
-        rc = on_stream(ctx, s.s, [&] {
+        rc = on_stream(ctx, s, [&] {
             return code ? rs_encode_device(ctx, code, len, nb, s.d_in, (size_t)k * ssd, s.d_out, (size_t)m * ssd, ssd)
                         : xor_encode_device(ctx, k, len, nb, s.d_in, (size_t)k * ssd, s.d_out, ssd, ssd);
         });
@@ -786,7 +827,7 @@ static int host_reconstruct_rs(fec_ctx* ctx, Code* code, int k, int m, size_t le
             HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, (nb * k + P * nb) * ssd, hipMemcpyHostToDevice, s.s));
         }
         HIP_TRY(hipMemcpyAsync(s.d_masks, s.h_masks, nb * 4, hipMemcpyHostToDevice, s.s));
-        rc = on_stream(ctx, s.s, [&] {
+        rc = on_stream(ctx, s, [&] {
             return rs_reconstruct_device(ctx, code, len, nb, s.d_in, (size_t)k * ssd, d_par, ssd, ssd, s.d_masks,
                                          s.d_status, ctx->d_err + 1, s.d_out, slots * ssd, (uint32_t)slots, nb * ssd);
         });
@@ -900,9 +941,10 @@ int fec_ctx_create(int device, fec_ctx** out) {
     ctx->device = device;
     if (hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&ctx->d_err, 2 * sizeof(int)) != hipSuccess ||
-        hipMalloc(&ctx->d_ctr, fk::kCtrWords * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(ctx->d_ctr, 0, fk::kCtrWords * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(ctx->d_err, 0, 2 * sizeof(int)) != hipSuccess) {
+        hipMalloc(&ctx->main.d_ctr, fk::kCtrWords * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(ctx->main.d_ctr, 0, fk::kCtrWords * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(ctx->d_err, 0, 2 * sizeof(int)) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {   // null-stream memsets done before any ctx stream runs
         (void)hipGetLastError();
         fec_ctx_destroy(ctx);
         return FEC_ERR_HIP;
@@ -929,10 +971,10 @@ void fec_ctx_destroy(fec_ctx* ctx) {
         if (kv.second.d_single_coef) (void)hipFree(kv.second.d_single_coef);
         if (kv.second.d_dall) (void)hipFree(kv.second.d_dall);
     }
-    if (ctx->d_plans) (void)hipFree(ctx->d_plans);
-    if (ctx->d_hard) (void)hipFree(ctx->d_hard);
+    if (ctx->own) (void)hipStreamSynchronize(ctx->own);
+    if (ctx->stream && ctx->stream != ctx->own) (void)hipStreamSynchronize(ctx->stream);
+    ctx->main.release();
     if (ctx->d_err) (void)hipFree(ctx->d_err);
-    if (ctx->d_ctr) (void)hipFree(ctx->d_ctr);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
     if (ctx->d_masks) (void)hipFree(ctx->d_masks);
@@ -943,6 +985,7 @@ void fec_ctx_destroy(fec_ctx* ctx) {
             if (q) (void)hipHostFree(q);
         for (void* q : {(void*)s.d_in, (void*)s.d_out, (void*)s.d_masks, (void*)s.d_status, (void*)s.d_raw})
             if (q) (void)hipFree(q);
+        s.w.release();
         if (s.done) (void)hipEventDestroy(s.done);
         if (s.s) (void)hipStreamDestroy(s.s);
     }
@@ -978,12 +1021,24 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 22 ? &fk::g_tune.enc_dyadic : key == 23 ? &fk::g_tune.dec_direct
               : key == 24 ? &fk::g_tune.dec_sorted : key == 25 ? &fk::g_tune.dec_fixk
               : key == 26 ? &fk::g_tune.host_chunk : key == 27 ? &fk::g_tune.dir_wpc
-              : key == 28 ? &fk::g_tune.dir_nt : nullptr;
+              : key == 28 ? &fk::g_tune.dir_nt : key == 29 ? &fk::g_tune.dec_pseg : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;
     memset(ctx->grid_cache, 0, sizeof(ctx->grid_cache));
     return old;
+}
+
+// Internal diagnostics (not part of the public ABI): the multi-erasure worklist's count and
+// done words of the ctx's own workspace, after waiting for its stream. Both are 0 between calls.
+int fec__worklist_state(fec_ctx* ctx, uint32_t* out2) {
+    if (!ctx || !out2) return FEC_ERR_INVALID_ARG;
+    out2[0] = out2[1] = 0;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (!ctx->main.d_hard) return FEC_OK;
+    HIP_TRY(hipMemcpy(&out2[0], ctx->main.d_hard, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&out2[1], ctx->main.d_hard + fk::kHardDone, 4, hipMemcpyDeviceToHost));
+    return FEC_OK;
 }
 
 int fec_ctx_reset_stream(fec_ctx* ctx) {
@@ -1001,8 +1056,10 @@ int fec_sync(fec_ctx* ctx) {
     int err = 0;
     HIP_TRY(hipMemcpy(&err, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (err) {
-        HIP_TRY(hipMemset(ctx->d_err, 0, sizeof(int)));
-        return (err & 1) ? FEC_ERR_TOO_FEW_SHARDS : FEC_ERR_INVALID_ARG;
+        HIP_TRY(hipMemsetAsync(ctx->d_err, 0, sizeof(int), ctx->stream));
+        // 1: a block with too few shards; 2: more erasures than output slots; 4: internal
+        // (a worklist past its capacity)
+        return (err & 1) ? FEC_ERR_TOO_FEW_SHARDS : (err & 4) ? FEC_ERR_HIP : FEC_ERR_INVALID_ARG;
     }
     return FEC_OK;
 }

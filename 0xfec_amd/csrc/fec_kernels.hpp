@@ -107,6 +107,7 @@ struct ReconArgs {
     const uint32_t* single_coef;   // the same plans' coefficient bytes: (k*m) rows of ceil(k/4) dwords
     const uint32_t* single_coef_host;   // host copy of single_coef (passed as a kernel argument when small)
     uint32_t* hard;            // multi-erasure worklist: [0] count, [kHardDone] done, [kHardList..] wave items
+    uint32_t hard_cap;         // entries the worklist holds (a count past it is reported, never written)
 };
 
 constexpr uint32_t kHardDone = 32, kHardList = 64;   // worklist words (own 128-byte lines)
@@ -163,6 +164,7 @@ struct Tuning {
                               // after the other (one plan stage); 0: 2 for k <= 4, else 1
     int dir_wpc = -1;         // direct decode residency (workgroups per CU, 0 uncapped); -1: by shape,
                               // 4 for k >= 8 (RS(8,12) +3.6 %), uncapped below (RS(2,3): caps cost 10-60 %)
+    int dec_pseg = 0;         // sorted plan kernel: segments of blocks per workgroup (0: by batch size)
     int dir_nt = -1;          // direct decode cache policy (3 nt loads + stores, 2 plain loads + nt
                               // stores, 0 plain); -1: by shape, 2 for k <= 4 (RS(2,3) +8 %), else 3
 };

@@ -12,6 +12,8 @@
 // rebuild kernel walks records in storage order, so the <= 3 blocks a rebuild wave touches have
 // (nearly always) the same erasure count: its wave-uniform row count is the blocks' own, not the
 // maximum of unrelated neighbours (RS(16,24) with 1-8 losses: 3.8 -> 3.1 rows per wave).
+#include <algorithm>
+
 #include "fec_recon.hpp"
 
 namespace fk {
@@ -36,7 +38,7 @@ __host__ __device__ inline SortLds sort_lds(uint32_t m, uint32_t k, uint32_t gro
 }
 
 template <uint32_t LPB>
-__global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanArgs a) {
+__global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanArgs a, uint32_t segs) {
     constexpr uint32_t G = kPlanSortThreads / LPB;   // blocks per workgroup segment
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const PlanLayout lay = a.lay;
@@ -47,11 +49,8 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
     uint32_t* s_pos = reinterpret_cast<uint32_t*>(smem + L.pos);
     const uint32_t k = a.k, m = a.m, n = k + m;
     const uint32_t gb = threadIdx.x / LPB, gl = threadIdx.x % LPB;   // block group, lane in group
-    const uint32_t b = blockIdx.x * G + gb;
-    const bool valid = b < a.nblocks;
-    // the block's present mask first: its HBM round trip overlaps the table staging below
-    const uint32_t mask_in = valid ? a.masks[b] : 0u;
-    // exp | log (768 bytes, contiguous in gf::kTables) as dwords, then the parity rows and dall
+    // exp | log (768 bytes, contiguous in gf::kTables) as dwords, then the parity rows and dall:
+    // staged once per workgroup, which then plans `segs` consecutive segments of G blocks
     {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(&gf::kTables);
         if (threadIdx.x < 192) reinterpret_cast<uint32_t*>(smem)[threadIdx.x] = src[threadIdx.x];
@@ -59,8 +58,6 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
     for (uint32_t i = threadIdx.x; i < m * k; i += kPlanSortThreads) s_prows[i] = a.prows[i];
     uint8_t* s_dall = smem + L.dall;
     if (threadIdx.x < n) s_dall[threadIdx.x] = a.dall[threadIdx.x];
-    __syncthreads();
-
     uint8_t* S = smem + L.scratch + gb * kGroupScratch;   // first k present shards
     uint8_t* O = S + 32;                                  // erased data shards, ascending
     uint8_t* X = S + 64;                                  // the other n - k shard indices
@@ -68,124 +65,143 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
     uint8_t* Nt = Dt + k;
     uint8_t* P = smem + L.recs + (size_t)gb * lay.stride;
     const uint32_t all = low_mask(n), kmask = low_mask(k);
-    const uint32_t mask = valid ? mask_in & all : all;   // past the batch: nothing to rebuild
-    const uint32_t e = k - __popc(mask & kmask);
-    int32_t st = a.max_out ? (int32_t)e : 0;
-    uint32_t nout = 0;
-    if (e != 0) {
-        if ((uint32_t)__popc(mask) < k) {
-            st = -4;   // FEC_ERR_TOO_FEW_SHARDS
-            if (gl == 0) atomicOr(a.err, 1);
-        } else if (a.max_out && e > a.max_out) {
-            st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
-            if (gl == 0) atomicOr(a.err, 2);
-        } else {
-            nout = e;
-        }
-    }
-    if (gl == 0) {
-        P[lay.nout_off] = (uint8_t)nout;
-        *reinterpret_cast<uint32_t*>(P + lay.blk_off) = b;
-        if (valid && a.status) a.status[b] = st;
-    }
-    if (nout) {
-        for (uint32_t t = gl; t < n; t += LPB) {
-            const uint32_t pos = __popc(mask & low_mask(t));
-            if (((mask >> t) & 1u) && pos < k) {
-                S[pos] = (uint8_t)t;
+    const uint32_t seg0 = blockIdx.x * segs;
+    // the first segment's masks in flight while the tables stage
+    uint32_t mask_next = seg0 * G + gb < a.nblocks ? a.masks[seg0 * G + gb] : 0u;
+    for (uint32_t sg = 0; sg < segs; ++sg) {
+        const uint32_t base = (seg0 + sg) * G;
+        if (base >= a.nblocks) break;   // workgroup-uniform
+        const uint32_t b = base + gb;
+        const bool valid = b < a.nblocks;
+        const uint32_t mask_in = mask_next;
+        // the next segment's mask loads before this segment's work
+        const uint32_t bn = b + G;
+        mask_next = (sg + 1 < segs && bn < a.nblocks) ? a.masks[bn] : 0u;
+        __syncthreads();   // tables staged (first pass); the previous segment's records copied out
+        const uint32_t mask = valid ? mask_in & all : all;   // past the batch: nothing to rebuild
+        const uint32_t e = k - __popc(mask & kmask);
+        int32_t st = a.max_out ? (int32_t)e : 0;
+        uint32_t nout = 0;
+        if (e != 0) {
+            if ((uint32_t)__popc(mask) < k) {
+                st = -4;   // FEC_ERR_TOO_FEW_SHARDS
+                if (gl == 0) atomicOr(a.err, 1);
+            } else if (a.max_out && e > a.max_out) {
+                st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
+                if (gl == 0) atomicOr(a.err, 2);
             } else {
-                X[t - min(pos, k)] = (uint8_t)t;   // not an input: erased, or present past the first k
-                if (t < k && !((mask >> t) & 1u)) O[__popc(~mask & kmask & low_mask(t))] = (uint8_t)t;
+                nout = e;
             }
         }
-    }
-    wave_sync();
-    uint8_t* C = P + lay.coef_off;
-    if (nout) {
-        if (gl < k) P[lay.in_off + gl] = S[gl];
-        if (gl < nout) P[lay.out_off + gl] = O[gl];
-        if (e == 1) {
-            // one erasure: x_E = inv(A[R0][E]) * (p_R0 ^ sum_j A[R0][j] x_j)
-            const uint32_t E0 = O[0];
-            const uint32_t R0 = __ffs(mask >> k) - 1;   // e = 1 with k present shards: a parity, k < 32
-            const uint8_t* row = s_prows + R0 * k;
-            const uint32_t inv = s_exp[255 - s_log[row[E0]]];
-            if (gl < k) {
-                const uint32_t sj = S[gl];
-                C[gl] = (uint8_t)(sj < k ? (row[sj] ? s_exp[s_log[inv] + s_log[row[sj]]] : 0u) : inv);
-            }
-        } else {
-            // Lagrange over the shard indices (rs_plan_kernel): D_p = sum_{q != p} log(s_p ^ s_q),
-            // N_r = sum_q log(i_r ^ s_q), coef[r][p] = exp(N_r - log(i_r ^ s_p) - D_p). With
-            // fewer other shards than inputs (n - k < k), both sums run over the complement:
-            // sum over all n indices (dall, per code) minus the n - k others X.
-            const bool comp = n - k < k;
-            if (gl < k) {
-                const uint32_t sp = S[gl];
-                uint32_t d = 0;
-                if (comp) {
-                    for (uint32_t u = 0; u < n - k; ++u) d += s_log[sp ^ X[u]];
-                    d = s_dall[sp] + 255u * 32u - d;
+        if (gl == 0) {
+            P[lay.nout_off] = (uint8_t)nout;
+            *reinterpret_cast<uint32_t*>(P + lay.blk_off) = b;
+            if (valid && a.status) a.status[b] = st;
+        }
+        if (nout) {
+            for (uint32_t t = gl; t < n; t += LPB) {
+                const uint32_t pos = __popc(mask & low_mask(t));
+                if (((mask >> t) & 1u) && pos < k) {
+                    S[pos] = (uint8_t)t;
                 } else {
-                    for (uint32_t q = 0; q < k; ++q)
-                        if (q != gl) d += s_log[sp ^ S[q]];
+                    X[t - min(pos, k)] = (uint8_t)t;   // not an input: erased, or present past the first k
+                    if (t < k && !((mask >> t) & 1u)) O[__popc(~mask & kmask & low_mask(t))] = (uint8_t)t;
                 }
-                Dt[gl] = (uint8_t)(d % 255u);
             }
-            if (gl < e) {
-                const uint32_t i = O[gl];
-                uint32_t ns = 0;
-                if (comp) {
-                    for (uint32_t u = 0; u < n - k; ++u) {
-                        const uint32_t x = X[u];
-                        if (x != i) ns += s_log[i ^ x];
+        }
+        wave_sync();
+        uint8_t* C = P + lay.coef_off;
+        if (nout) {
+            if (gl < k) P[lay.in_off + gl] = S[gl];
+            if (gl < nout) P[lay.out_off + gl] = O[gl];
+            if (e == 1) {
+                // one erasure: x_E = inv(A[R0][E]) * (p_R0 ^ sum_j A[R0][j] x_j)
+                const uint32_t E0 = O[0];
+                const uint32_t R0 = __ffs(mask >> k) - 1;   // e = 1 with k present shards: a parity, k < 32
+                const uint8_t* row = s_prows + R0 * k;
+                const uint32_t inv = s_exp[255 - s_log[row[E0]]];
+                if (gl < k) {
+                    const uint32_t sj = S[gl];
+                    C[gl] = (uint8_t)(sj < k ? (row[sj] ? s_exp[s_log[inv] + s_log[row[sj]]] : 0u) : inv);
+                }
+            } else {
+                // Lagrange over the shard indices (rs_plan_kernel): D_p = sum_{q != p} log(s_p ^ s_q),
+                // N_r = sum_q log(i_r ^ s_q), coef[r][p] = exp(N_r - log(i_r ^ s_p) - D_p). With
+                // fewer other shards than inputs (n - k < k), both sums run over the complement:
+                // sum over all n indices (dall, per code) minus the n - k others X.
+                const bool comp = n - k < k;
+                if (gl < k) {
+                    const uint32_t sp = S[gl];
+                    uint32_t d = 0;
+                    if (comp) {
+                        for (uint32_t u = 0; u < n - k; ++u) d += s_log[sp ^ X[u]];
+                        d = s_dall[sp] + 255u * 32u - d;
+                    } else {
+                        for (uint32_t q = 0; q < k; ++q)
+                            if (q != gl) d += s_log[sp ^ S[q]];
                     }
-                    ns = s_dall[i] + 255u * 32u - ns;
-                } else {
-                    for (uint32_t q = 0; q < k; ++q) ns += s_log[i ^ S[q]];
+                    Dt[gl] = (uint8_t)(d % 255u);
                 }
-                Nt[gl] = (uint8_t)(ns % 255u);
+                if (gl < e) {
+                    const uint32_t i = O[gl];
+                    uint32_t ns = 0;
+                    if (comp) {
+                        for (uint32_t u = 0; u < n - k; ++u) {
+                            const uint32_t x = X[u];
+                            if (x != i) ns += s_log[i ^ x];
+                        }
+                        ns = s_dall[i] + 255u * 32u - ns;
+                    } else {
+                        for (uint32_t q = 0; q < k; ++q) ns += s_log[i ^ S[q]];
+                    }
+                    Nt[gl] = (uint8_t)(ns % 255u);
+                }
             }
         }
-    }
-    wave_sync();
-    if (nout >= 2 && gl < k) {
-        const uint32_t sp = S[gl], dp = Dt[gl];
-        for (uint32_t r = 0; r < nout; ++r) {
-            const uint32_t v = Nt[r] + 2u * 255u - s_log[O[r] ^ sp] - dp;
-            C[r * k + gl] = s_exp[v % 255u];
+        wave_sync();
+        if (nout >= 2 && gl < k) {
+            const uint32_t sp = S[gl], dp = Dt[gl];
+            for (uint32_t r = 0; r < nout; ++r) {
+                const uint32_t v = Nt[r] + 2u * 255u - s_log[O[r] ^ sp] - dp;
+                C[r * k + gl] = s_exp[v % 255u];
+            }
         }
-    }
-    __syncthreads();
-    // storage order of the segment: erasure count descending, then block order (stable)
-    const uint32_t nseg = min(G, a.nblocks - blockIdx.x * G);
-    if (threadIdx.x < G) {
-        const uint32_t t = threadIdx.x;
-        const uint32_t kt = smem[L.recs + (size_t)t * lay.stride + lay.nout_off];
-        uint32_t pos = 0;
-        for (uint32_t j = 0; j < G; ++j) {
-            const uint32_t kj = smem[L.recs + (size_t)j * lay.stride + lay.nout_off];
-            pos += (kj > kt) || (kj == kt && j < t);
+        __syncthreads();
+        // storage order of the segment: erasure count descending, then block order (stable)
+        const uint32_t nseg = min(G, a.nblocks - base);
+        if (threadIdx.x < G) {
+            const uint32_t t = threadIdx.x;
+            const uint32_t kt = smem[L.recs + (size_t)t * lay.stride + lay.nout_off];
+            uint32_t pos = 0;
+            for (uint32_t j = 0; j < G; ++j) {
+                const uint32_t kj = smem[L.recs + (size_t)j * lay.stride + lay.nout_off];
+                pos += (kj > kt) || (kj == kt && j < t);
+            }
+            s_pos[t] = pos;   // past-the-batch groups (nothing to rebuild, last indices) rank last
         }
-        s_pos[t] = pos;   // past-the-batch groups (nothing to rebuild, last indices) rank last
-    }
-    __syncthreads();
-    const uint32_t per = lay.stride / 16;
-    const uint4* src = reinterpret_cast<const uint4*>(smem + L.recs);
-    uint4* dst = reinterpret_cast<uint4*>(a.plans + (uint64_t)blockIdx.x * G * lay.stride);
-    for (uint32_t i = threadIdx.x; i < nseg * per; i += kPlanSortThreads) {
-        const uint32_t r = i / per, q = i - r * per;
-        dst[(size_t)s_pos[r] * per + q] = src[i];
+        __syncthreads();
+        const uint32_t per = lay.stride / 16;
+        const uint4* src = reinterpret_cast<const uint4*>(smem + L.recs);
+        uint4* dst = reinterpret_cast<uint4*>(a.plans + (uint64_t)base * lay.stride);
+        for (uint32_t i = threadIdx.x; i < nseg * per; i += kPlanSortThreads) {
+            const uint32_t r = i / per, q = i - r * per;
+            dst[(size_t)s_pos[r] * per + q] = src[i];
+        }
     }
 }
 
 template <uint32_t LPB>
 hipError_t sorted_launch(const PlanArgs& a, hipStream_t s) {
     constexpr uint32_t G = kPlanSortThreads / LPB;
-    const uint32_t grid = (a.nblocks + G - 1) / G;
-    if (grid == 0) return hipSuccess;
+    const uint32_t nseg = (a.nblocks + G - 1) / G;
+    if (nseg == 0) return hipSuccess;
+    // segments per workgroup (knob dec_pseg, 0: by batch size): enough workgroups to fill the
+    // chip several times over, each staging the tables once for all its segments
+    uint32_t segs = g_tune.dec_pseg > 0 ? (uint32_t)g_tune.dec_pseg : std::max<uint32_t>(1, nseg / 4096);
+    segs = std::min<uint32_t>(segs, 64);
+    const uint32_t grid = (nseg + segs - 1) / segs;
     const size_t lds = sort_lds(a.m, a.k, G, a.lay.stride).total;
-    hipLaunchKernelGGL((rs_plan_sorted_kernel<LPB>), dim3(grid), dim3(kPlanSortThreads), lds, s, a);
+    hipLaunchKernelGGL((rs_plan_sorted_kernel<LPB>), dim3(grid), dim3(kPlanSortThreads), lds, s, a, segs);
     return hipGetLastError();
 }
 

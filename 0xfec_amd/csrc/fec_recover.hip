@@ -105,7 +105,11 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
         if (e >= 2 && (uint32_t)__popc(mask) >= k && !(a.max_out && e > a.max_out)) hard = true;
     }
     if (hard) {
-        if (lane == 0) a.hard[kHardList + atomicAdd(a.hard, 1u)] = i0;
+        if (lane == 0) {
+            const uint32_t slot = atomicAdd(a.hard, 1u);
+            if (slot < a.hard_cap) a.hard[kHardList + slot] = i0;
+            else atomicOr(a.err, 4);   // never expected: the worklist holds one entry per wave
+        }
         return;
     }
     // Per block (uniform): the table row (E0 * m + R0) of a single-erasure block.
@@ -253,7 +257,7 @@ __global__ __launch_bounds__(kThreads) void rs_recover_hard_kernel(ReconArgs a) 
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t k = a.k, m = a.m, maxe = a.maxe;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t count = __hip_atomic_load(a.hard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t count = min(__hip_atomic_load(a.hard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.hard_cap);
     const uint32_t W = gridDim.x * (kThreads / 64);
     uint32_t t = blockIdx.x * (kThreads / 64) + wave;
     if (t < count) {

@@ -461,3 +461,31 @@ def test_xor_host_pipeline_matches_oracle(codec, oracle, torch, fec, pinned):
         codec.set_tuning(**old)
     got = buf.numpy() if pinned else buf
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("k,m,chunk", [(8, 4, 61), (16, 8, 37), (20, 10, 64)])
+def test_rs_host_pipeline_many_chunks_multi_erasure(codec, oracle, fec, k, m, chunk):
+    """Host-path reconstruct over many small chunks (consecutive chunks run on the two staging
+    sets' streams at once) with up to m erasures per block: the multi-erasure worklist (RS(8,12))
+    and the plan records (RS(16,24), RS(20,30)) are per stream, so overlapping chunks never share
+    one. Checked against the oracle block by block."""
+    rng = np.random.default_rng(7000 + k + chunk)
+    n, B, L = k + m, 1500, 600
+    full = np.zeros((B, n, L), dtype=np.uint8)
+    full[:, :k] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    oracle.rs_encode(k, m, full)
+    masks = _random_masks(rng, B, k, m, max_loss=m)
+    dmg = full[:, :k].copy()
+    for b in range(B):
+        for i in range(k):
+            if not (masks[b] >> i) & 1:
+                dmg[b, i] = 0xA1
+    par = full[:, k:].copy()
+    old = codec.set_tuning(host_chunk=chunk)
+    try:
+        st = np.full(B, 7, dtype=np.int32)
+        rc = codec.rs_reconstruct_split(k, m, dmg, par, masks, status=st, shard_len=L)
+        assert rc == fec.FEC_OK and (st == 0).all()
+        assert np.array_equal(dmg, full[:, :k])
+    finally:
+        codec.set_tuning(**old)

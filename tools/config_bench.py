@@ -6,6 +6,8 @@
   RS(8,12)   2^20 blocks, one random erased data shard per block (bench.py's workload)
   RS(16,24)  2^19 blocks, e ~ U{1..8} erasures per block, uniform over all 24 shards
   XOR(2,1)   2^20 blocks (the reference's XOR factory code), one erased data shard
+  RS(20,30)  2^19 blocks (the reference's RS factory code, manager.go:58-60): one erased data
+             shard, and e ~ U{1..10} erasures uniform over all 30 shards
 
 Algorithmic bytes (L = 1202): encode k*L read + m*L written per block; decode (recover into an
 output buffer) (k + e_d)*L per block with e_d >= 1 erased data shards, nothing for blocks whose
@@ -172,7 +174,10 @@ def main():
     cases = [("rs23", lambda: run_rs(torch, fec, codec, 2, 1, 65536, 0, max(args.iters, 100), 0x0FEC)),
              ("rs812", lambda: run_rs(torch, fec, codec, 8, 4, 1 << 20, 0, args.iters, 0x0FEC)),
              ("rs1624", lambda: run_rs(torch, fec, codec, 16, 8, 1 << 19, 8, args.iters, 0x0FEC)),
-             ("xor21", lambda: run_xor(torch, fec, codec, 2, 1 << 20, args.iters, 0x0FEC))]
+             ("xor21", lambda: run_xor(torch, fec, codec, 2, 1 << 20, args.iters, 0x0FEC)),
+             # the reference's own factory code (manager.go:58-60), not a BASELINE config
+             ("rs2030", lambda: run_rs(torch, fec, codec, 20, 10, 1 << 19, 0, args.iters, 0x0FEC)),
+             ("rs2030m", lambda: run_rs(torch, fec, codec, 20, 10, 1 << 19, 10, args.iters, 0x0FEC))]
     for name, fn in cases:
         if args.only and name not in args.only.split(","):
             continue

@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--blocks", type=int, default=1 << 20)
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--multi", type=int, default=0,
+                    help="e ~ U{1..multi} erasures uniform over all n shards (config_bench's RS(16,24) mix)")
     args = ap.parse_args()
     import torch
     fec = importlib.import_module("0xfec_amd")
@@ -27,12 +29,28 @@ def main():
     codec = fec.Codec(0).use_torch_stream()
     data = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device="cuda")
     par = torch.randint(0, 256, (B, m, S), dtype=torch.uint8, device="cuda")
-    out = torch.zeros((B, 1, S), dtype=torch.uint8, device="cuda")
-    erased = torch.randint(0, k, (B,), device="cuda")
-    masks = ((1 << (k + m)) - 1 - (1 << erased)).to(torch.int32)
+    n = k + m
+    if args.multi:
+        e = torch.randint(1, args.multi + 1, (B,), device="cuda")
+        rank = torch.rand((B, n), device="cuda").argsort(dim=1).argsort(dim=1)
+        lost = rank < e[:, None]
+        weights = torch.bitwise_left_shift(torch.ones(n, dtype=torch.int64, device="cuda"),
+                                           torch.arange(n, device="cuda"))
+        masks = (((~lost).to(torch.int64) * weights).sum(dim=1)).to(torch.int32)
+        slots = max(1, int(lost[:, :k].sum(dim=1).max().item()))
+        e_d = lost[:, :k].sum(dim=1)
+        byts_total = int(((k + e_d) * (e_d > 0)).sum().item()) * L
+    else:
+        erased = torch.randint(0, k, (B,), device="cuda")
+        masks = ((1 << n) - 1 - (1 << erased)).to(torch.int32)
+        slots = 1
+        byts_total = B * (k + 1) * L
+    out = torch.zeros((B, slots, S), dtype=torch.uint8, device="cuda")
     status = torch.zeros((B,), dtype=torch.int32, device="cuda")
     dp, pp, op = data.data_ptr(), par.data_ptr(), out.data_ptr()
-    D = dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=1, dec_ipl=0, dec_direct=1, dec_nt=3, dir_wpc=-1, dir_nt=-1)
+    # every knob any variant sets, at its default: tune(D) must undo each variant completely
+    D = dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=1, dec_ipl=0, dec_direct=1, dec_nt=3, dir_wpc=-1, dir_nt=-1,
+             dec_fixk=1, dec_sorted=1, dec_pseg=0)
     variants = {"direct (default)": D,
                 "direct, PermTab rows by vector load": dict(D, dec_direct=2),
                 "direct noswz": dict(D, dec_swz=0),
@@ -42,11 +60,18 @@ def main():
             variants["direct wpc%d, %s" % (w, nm)] = dict(D, dir_wpc=w, dir_nt=nt)
     variants["direct + status array"] = dict(D, _status=1)
     variants["direct, plain loads and stores"] = dict(D, dir_nt=0)
+    if args.multi:   # the plan + wave path: residency, cache policy, compile-time k, plan form
+        variants = {"default": D}
+        variants["wave runtime k"] = dict(D, dec_fixk=0)
+        variants["unsorted plans"] = dict(D, dec_sorted=0)
+        for ps in (1, 2, 4, 8, 16):
+            variants["plan segs %d" % ps] = dict(D, dec_pseg=ps)
+        variants["default + status array"] = dict(D, _status=1)
     base = codec.set_tuning(**D)
     use_status = [False]
 
     def run():
-        codec.rs_recover_raw(k, m, L, B, dp, k * S, pp, m * S, S, masks.data_ptr(), op, S, 1,
+        codec.rs_recover_raw(k, m, L, B, dp, k * S, pp, m * S, S, masks.data_ptr(), op, slots * S, slots,
                              status.data_ptr() if use_status[0] else None)
 
     def t(iters):
@@ -80,8 +105,8 @@ def main():
             tune(kv)
             res[n].append(t(args.iters))
             tune(D)
-    byts = B * (k + 1) * L
-    print(json.dumps({"shape": "RS(%d,%d) x %d" % (k, k + m, B),
+    byts = byts_total
+    print(json.dumps({"shape": "RS(%d,%d) x %d%s" % (k, k + m, B, " e~U{1..%d}" % args.multi if args.multi else ""),
                       "median_us_TBps_best": {n: [round(sorted(v)[len(v) // 2] * 1e6, 1),
                                                   round(byts / sorted(v)[len(v) // 2] / 1e12, 3),
                                                   round(byts / min(v) / 1e12, 3)] for n, v in res.items()}}))

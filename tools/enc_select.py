@@ -24,9 +24,12 @@ def main():
         variants["matrix flat wpc%d" % w] = dict(enc_queue=0, enc_wpc=w, enc_dyadic=0)
     for w in (0, 3, 4, 5):
         variants["dyadic flat wpc%d" % w] = dict(enc_queue=0, enc_wpc=w, enc_dyadic=1)
+    for w in (3, 4):
+        variants["dyadic flat wpc%d, plain loads" % w] = dict(enc_queue=0, enc_wpc=w, enc_dyadic=1, enc_nt=2)
+    variants["matrix flat wpc3, plain loads"] = dict(enc_queue=0, enc_wpc=3, enc_dyadic=0, enc_nt=2)
     if k == 8:
         variants["matrix queue d0 wpc2"] = dict(enc_queue=1, enc_qwpc=2, enc_qdepth=0, enc_dyadic=0)
-    base = codec.set_tuning(enc_queue=0, enc_wpc=4, enc_qwpc=2, enc_qdepth=0, enc_dyadic=1)
+    base = codec.set_tuning(enc_queue=0, enc_wpc=3, enc_qwpc=2, enc_qdepth=0, enc_dyadic=1, enc_nt=3)
     ref = None
     for n, kv in variants.items():   # every form writes the same parity bytes
         codec.set_tuning(**kv)
