@@ -1021,7 +1021,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 22 ? &fk::g_tune.enc_dyadic : key == 23 ? &fk::g_tune.dec_direct
               : key == 24 ? &fk::g_tune.dec_sorted : key == 25 ? &fk::g_tune.dec_fixk
               : key == 26 ? &fk::g_tune.host_chunk : key == 27 ? &fk::g_tune.dir_wpc
-              : key == 28 ? &fk::g_tune.dir_nt : key == 29 ? &fk::g_tune.dec_pseg : nullptr;
+              : key == 28 ? &fk::g_tune.dir_nt : key == 29 ? &fk::g_tune.dec_pseg
+              : key == 30 ? &fk::g_tune.enc_bits : key == 31 ? &fk::g_tune.enc_bwpc : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

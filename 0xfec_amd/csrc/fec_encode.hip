@@ -342,6 +342,135 @@ __global__ __launch_bounds__(kThreads) void rs_encode_queue0_kernel(EncodeArgs a
     }
 }
 
+// ------------------------------------------------------------------ RS encode, bit-sliced
+// The fixed shapes as one XOR network over bit planes (gen_bitslice.py): a lane takes two
+// 16-byte chunks of every data shard, turns each shard's 8 dwords into 8 bit planes (plane b holds bit b of the 32 bytes), runs the compile-time network
+// (shared sub-sums, three-input XORs, no tables), and turns the parity planes back into bytes.
+// RS(16,24): 2 x 48 ops of transposes per shard plus 1202 network ops per 32 bytes, against 54
+// v_perm products of the dyadic body per 16 bytes.
+template <int K, int M>
+struct BsShape;   // G: shards per network group
+template <int K, int M, int GI>
+__device__ __forceinline__ void bs_grp(const uint32_t (&x)[BsShape<K, M>::G][8], uint32_t (&y)[M][8]);
+#include "fec_bitslice.inc"
+
+// In every byte column q of the 8 dwords, transpose the 8x8 bit block (row = dword i, column =
+// bit b): afterwards bit 8q + i of w[b] is what was bit 8q + b of w[i]. Three delta swaps (block
+// sizes 4, 2, 1), two ops per register per stage. A transpose is its own inverse.
+// (a & m) | (b & ~m) as one v_bfi_b32 (left to the compiler, the masks are merged into the
+// neighbouring XORs as AND + three-input ops: more instructions)
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+    uint32_t d;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(d) : "s"(m), "v"(a), "v"(b));
+    return d;
+}
+template <int S>
+__device__ __forceinline__ void delta_swap8(uint32_t (&w)[8]) {
+    constexpr uint32_t lo = S == 4 ? 0x0F0F0F0Fu : S == 2 ? 0x33333333u : 0x55555555u;   // bits with (b & S) == 0
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        if (i & S) continue;
+        const uint32_t a = w[i], c = w[i + S];
+        w[i] = bfi(lo, a, c << S);
+        w[i + S] = bfi(lo, a >> S, c);
+    }
+}
+__device__ __forceinline__ void bit_transpose8(uint32_t (&w)[8]) {
+    delta_swap8<4>(w);
+    delta_swap8<2>(w);
+    delta_swap8<1>(w);
+}
+
+// Group GI of the network: transpose the group's raw chunks into planes, fold them into y.
+// STREAM: the next group's loads are issued first, behind an opaque dependence on the previous
+// group's last output, so only two groups of inputs are ever held (fewer VGPRs, more waves) and
+// every wave keeps loads in flight while it computes.
+template <int K, int M, int POL, bool STREAM, int GI>
+__device__ __forceinline__ void bs_stream(const uint8_t* s0, const uint8_t* s1, uint64_t ss,
+                                          uint4 (&cur)[BsShape<K, M>::G][2], uint32_t (&y)[M][8]) {
+    constexpr int G = BsShape<K, M>::G, NG = K / G;
+    constexpr bool NTL = POL & 1;
+    uint4 nxt[G][2];
+    if constexpr (STREAM && GI + 1 < NG) {
+        uint64_t off = (uint64_t)(GI + 1) * G * ss;
+        if constexpr (GI > 0) asm volatile("" : "+v"(off) : "v"(y[M - 1][7]));
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            nxt[j][0] = ld16<NTL>(s0 + off + (uint64_t)j * ss);
+            nxt[j][1] = ld16<NTL>(s1 + off + (uint64_t)j * ss);
+        }
+    }
+    uint32_t x[G][8];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        x[j][0] = cur[j][0].x, x[j][1] = cur[j][0].y, x[j][2] = cur[j][0].z, x[j][3] = cur[j][0].w;
+        x[j][4] = cur[j][1].x, x[j][5] = cur[j][1].y, x[j][6] = cur[j][1].z, x[j][7] = cur[j][1].w;
+        bit_transpose8(x[j]);
+    }
+    bs_grp<K, M, GI>(x, y);
+    if constexpr (GI + 1 < NG) {
+        if constexpr (!STREAM) {
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                nxt[j][0] = ld16<NTL>(s0 + (uint64_t)((GI + 1) * G + j) * ss);
+                nxt[j][1] = ld16<NTL>(s1 + (uint64_t)((GI + 1) * G + j) * ss);
+            }
+        }
+        bs_stream<K, M, POL, STREAM, GI + 1>(s0, s1, ss, nxt, y);
+    }
+}
+
+template <int K, int M, int POL>
+__global__ __launch_bounds__(kThreads) void rs_encode_bits_kernel(EncodeArgs a) {
+    constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
+    // A wave takes 128 consecutive (block, chunk) items: lane l items w*128 + l and w*128 + 64 + l,
+    // so each load and store instruction covers 64 consecutive chunks, as in the one-chunk
+    // kernels. The two chunks of a lane may belong to different blocks: the network treats every
+    // byte column alike.
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t f0 = (xcd_order(a.swz) * kThreads + (threadIdx.x & ~63u)) * 2u + lane;
+    if (f0 >= a.total) return;
+    const uint32_t f1 = f0 + 64u;
+    const bool two = f1 < a.total;
+    const uint32_t b0 = fdiv(f0, a.div_cps), c0 = f0 - b0 * a.cps;
+    const uint32_t fb = two ? f1 : f0;   // without a second item the first is loaded again (no
+    const uint32_t b1 = fdiv(fb, a.div_cps), c1 = fb - b1 * a.cps;   // branch); its outputs are not stored
+    const uint8_t* s0 = a.in + (uint64_t)b0 * a.in_bs + (uint64_t)c0 * kChunk;
+    const uint8_t* s1 = a.in + (uint64_t)b1 * a.in_bs + (uint64_t)c1 * kChunk;
+    constexpr int G = BsShape<K, M>::G;
+    uint4 g0[G][2];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        g0[j][0] = ld16<NTL>(s0 + (uint64_t)j * a.ss);
+        g0[j][1] = ld16<NTL>(s1 + (uint64_t)j * a.ss);
+    }
+    uint32_t y[M][8];
+    bs_stream<K, M, POL, (POL & 16) != 0, 0>(s0, s1, a.ss, g0, y);
+    uint8_t* d0 = a.out + (uint64_t)b0 * a.out_bs + (uint64_t)c0 * kChunk;
+    uint8_t* d1 = a.out + (uint64_t)b1 * a.out_bs + (uint64_t)c1 * kChunk;
+    const uint32_t nb0 = min(a.len - c0 * kChunk, (uint32_t)kChunk);
+    const uint32_t nb1 = min(a.len - c1 * kChunk, (uint32_t)kChunk);
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        bit_transpose8(y[r]);
+        st16<NTS>(d0 + (uint64_t)r * a.ss, keep_bytes(make_uint4(y[r][0], y[r][1], y[r][2], y[r][3]), nb0));
+        if (two) st16<NTS>(d1 + (uint64_t)r * a.ss, keep_bytes(make_uint4(y[r][4], y[r][5], y[r][6], y[r][7]), nb1));
+    }
+}
+
+template <int K, int M>
+static hipError_t enc_bits_dispatch(const EncodeArgs& a, hipStream_t s) {
+    const int grid = (int)((a.total + 2 * kThreads - 1) / (2 * kThreads));
+    if (grid == 0) return hipSuccess;
+    const size_t lds = occupancy_lds(g_tune.enc_bwpc, 0);
+    const bool nt = g_tune.enc_nt & 1, stream = g_tune.enc_bits & 4;
+    if (stream && nt) hipLaunchKernelGGL((rs_encode_bits_kernel<K, M, 19>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (stream) hipLaunchKernelGGL((rs_encode_bits_kernel<K, M, 18>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (nt) hipLaunchKernelGGL((rs_encode_bits_kernel<K, M, 3>), dim3(grid), dim3(kThreads), lds, s, a);
+    else hipLaunchKernelGGL((rs_encode_bits_kernel<K, M, 2>), dim3(grid), dim3(kThreads), lds, s, a);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ launchers
 template <int MAXM, int POL>
 static hipError_t enc_dispatch2(const EncodeArgs& a, int grid, hipStream_t s) {
@@ -411,6 +540,9 @@ static hipError_t enc_fixed_dispatch(const EncodeArgs& a, int grid, size_t lds, 
 hipError_t launch_rs_encode_fixed(EncodeArgs a, int ncu, hipStream_t s) {
     const uint32_t chunks = (a.total + kThreads - 1) / kThreads;
     if (chunks == 0) return hipSuccess;
+    // bit-sliced network (knob enc_bits: bit 0 RS(16,24), bit 1 RS(8,12), bit 2 streamed loads)
+    if (a.k == 16 && a.m == 8 && (g_tune.enc_bits & 1)) return enc_bits_dispatch<16, 8>(a, s);
+    if (a.k == 8 && a.m == 4 && (g_tune.enc_bits & 2)) return enc_bits_dispatch<8, 4>(a, s);
     // Per shape (measured): RS(8,12) and RS(16,24) run the flat grid at
     // g_tune.enc_wpc (3) workgroups per CU; RS(2,3) (2 loads per lane: little in flight per
     // wave) at full residency. The ticket-queue form stays selectable (enc_queue).

@@ -167,6 +167,11 @@ struct Tuning {
     int dec_pseg = 0;         // sorted plan kernel: segments of blocks per workgroup (0: by batch size)
     int dir_nt = -1;          // direct decode cache policy (3 nt loads + stores, 2 plain loads + nt
                               // stores, 0 plain); -1: by shape, 2 for k <= 4 (RS(2,3) +8 %), else 3
+    int enc_bits = 1;         // bit-sliced XOR-network encode (gen_bitslice.py): bit 0 RS(16,24), bit 1
+                              // RS(8,12), bit 2 loads streamed one network group ahead. Measured
+                              // (enc_select.py, one box): RS(16,24) 5.35 -> 6.36 TB/s; RS(8,12)
+                              // 6.42 vs 6.51 for the dyadic perm body (off); streamed -0.2 % (off)
+    int enc_bwpc = 0;         // its residency (workgroups per CU, 0 uncapped)
 };
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):

@@ -298,6 +298,12 @@ ENC_VARIANTS = {
     "queue_d1": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=1),
     "queue_d2": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=2),
     "queue_d1_1wg": dict(enc_fixed=1, enc_queue=1, enc_qwpc=1, enc_qdepth=1),
+    # bit-sliced XOR network (RS(8,12) and RS(16,24); RS(2,3) keeps the fixed kernel)
+    "bits": dict(enc_fixed=1, enc_queue=0, enc_bits=3, enc_bwpc=0),
+    "bits_wpc2": dict(enc_fixed=1, enc_queue=0, enc_bits=3, enc_bwpc=2),
+    "bits_plain": dict(enc_fixed=1, enc_queue=0, enc_bits=3, enc_nt=0),
+    "bits_stream": dict(enc_fixed=1, enc_queue=0, enc_bits=7, enc_bwpc=0),
+    "bits_off": dict(enc_fixed=1, enc_queue=0, enc_bits=0),
 }
 
 
