@@ -369,6 +369,7 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
                                  int32_t* status, int* err, uint8_t* out = nullptr, size_t out_bs = 0,
                                  uint32_t out_slots = 0, size_t pss = 0) {
     if (pss == 0) pss = ss;
+    if ((ss | pss) >> 32) return FEC_ERR_INVALID_ARG;   // the rebuild kernels take 32-bit shard strides
     const uint32_t k = (uint32_t)code->k, m = (uint32_t)code->m;
     const uint32_t maxe = std::max<uint32_t>(1, std::min(k, m));
     const uint32_t cps = (uint32_t)((len + fk::kChunk - 1) / fk::kChunk);

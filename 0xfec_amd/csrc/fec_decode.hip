@@ -152,10 +152,10 @@ __device__ __forceinline__ void recon_pair(const ReconArgs& a, const uint8_t* PA
             const uint32_t sa = ((jj < 4 ? slA.x : slA.y) >> (8 * (jj & 3))) & 0xFFu;
             const uint32_t sb = ((jj < 4 ? slB.x : slB.y) >> (8 * (jj & 3))) & 0xFFu;
             xa[jj] = j0 + jj < k && noutA
-                         ? ld16<NTL>(sa < k ? dA + (uint64_t)sa * a.ss : pA + (uint64_t)(sa - k) * a.pss)
+                         ? ld16<NTL>(slot_addr(dA, parity_base(pA, k, a.pss), sa, k, (uint32_t)a.ss, (uint32_t)a.pss))
                          : make_uint4(0, 0, 0, 0);
             xb[jj] = j0 + jj < k && noutB
-                         ? ld16<NTL>(sb < k ? dB + (uint64_t)sb * a.ss : pB + (uint64_t)(sb - k) * a.pss)
+                         ? ld16<NTL>(slot_addr(dB, parity_base(pB, k, a.pss), sb, k, (uint32_t)a.ss, (uint32_t)a.pss))
                          : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll

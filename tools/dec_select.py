@@ -63,6 +63,8 @@ def main():
     if args.multi:   # the plan + wave path: residency, cache policy, compile-time k, plan form
         variants = {"default": D}
         variants["wave runtime k"] = dict(D, dec_fixk=0)
+        for w in (2, 3):
+            variants["K=16 wpc%d" % w] = dict(D, dec_wpc=w)
         variants["unsorted plans"] = dict(D, dec_sorted=0)
         for ps in (1, 2, 4, 8, 16):
             variants["plan segs %d" % ps] = dict(D, dec_pseg=ps)
