@@ -951,6 +951,11 @@ int fec_ctx_create(int device, fec_ctx** out) {
         return FEC_ERR_HIP;
     }
     ctx->stream = ctx->own;
+    {   // LDS a workgroup may use (160 KiB on gfx950): bounds the wave-form rebuild's slices
+        int lds = 0;
+        if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess && lds > 0)
+            fk::g_max_lds = (size_t)lds;
+    }
     if (hipDeviceGetAttribute(&ctx->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
         ctx->ncu <= 0) {
         (void)hipGetLastError();

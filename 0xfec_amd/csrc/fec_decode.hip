@@ -380,9 +380,9 @@ static hipError_t recon_dispatch(const ReconArgs& a, int grid, hipStream_t s) {
 }
 
 // The wave form applies to shards of 32+ chunks (at most 3 blocks per wave) while its LDS
-// (4 wave slices per workgroup) stays within 64 KiB.
+// (4 wave slices per workgroup) fits a workgroup (gfx950: 160 KiB; RS(20,30) needs 80 KiB).
 bool wave_recon_applies(uint32_t cps, uint32_t k, uint32_t maxe, uint32_t stride) {
-    return g_tune.dec_wave && cps >= 32 && 4 * fused_slice_bytes(k, maxe, stride) + 2048 <= 65536;
+    return g_tune.dec_wave && cps >= 32 && 4 * fused_slice_bytes(k, maxe, stride) + 2048 <= g_max_lds;
 }
 
 template <int POL, bool FUSED, int IPL>
@@ -402,6 +402,12 @@ static hipError_t recon_wave_dispatch(const ReconArgs& a, hipStream_t s) {
     if constexpr (IPL == 1 && !FUSED) {
         if (a.k == 16 && a.maxe == 8 && g_tune.dec_fixk) {
             hipLaunchKernelGGL((rs_reconstruct_wave_kernel<8, POL, false, 1, 16>), dim3(grid), dim3(kThreads), lds,
+                               s, a);
+            return hipGetLastError();
+        }
+        // the reference's own receiver code RS(20,30) (manager.go:80-90)
+        if (a.k == 20 && a.maxe == 10 && g_tune.dec_fixk) {
+            hipLaunchKernelGGL((rs_reconstruct_wave_kernel<16, POL, false, 1, 20>), dim3(grid), dim3(kThreads), lds,
                                s, a);
             return hipGetLastError();
         }

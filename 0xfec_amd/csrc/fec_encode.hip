@@ -500,10 +500,12 @@ hipError_t launch_rs_encode(const EncodeArgs& a, int grid, hipStream_t s) {
 }
 
 // (k, m) shapes with a fixed-shape encode instance: the reference's benchmark codes RS(2,3),
-// RS(8,12), RS(16,24). Any other shape runs the generic kernel.
+// RS(8,12), RS(16,24), and (bit-sliced) its sender's RS(20,30). Any other shape runs the
+// generic kernel.
 bool fixed_encode_applies(uint32_t k, uint32_t m) {
     if (!g_tune.enc_fixed) return false;
-    return (k == 2 && m == 1) || (k == 8 && m == 4) || (k == 16 && m == 8);
+    return (k == 2 && m == 1) || (k == 8 && m == 4) || (k == 16 && m == 8) ||
+           (k == 20 && m == 10 && (g_tune.enc_bits & 8));   // bit-sliced only
 }
 
 template <int K, int M>
@@ -540,9 +542,11 @@ static hipError_t enc_fixed_dispatch(const EncodeArgs& a, int grid, size_t lds, 
 hipError_t launch_rs_encode_fixed(EncodeArgs a, int ncu, hipStream_t s) {
     const uint32_t chunks = (a.total + kThreads - 1) / kThreads;
     if (chunks == 0) return hipSuccess;
-    // bit-sliced network (knob enc_bits: bit 0 RS(16,24), bit 1 RS(8,12), bit 2 streamed loads)
+    // bit-sliced network (knob enc_bits: bit 0 RS(16,24), bit 1 RS(8,12), bit 2 streamed loads,
+    // bit 3 RS(20,30), the reference's own sender code, manager.go:80)
     if (a.k == 16 && a.m == 8 && (g_tune.enc_bits & 1)) return enc_bits_dispatch<16, 8>(a, s);
     if (a.k == 8 && a.m == 4 && (g_tune.enc_bits & 2)) return enc_bits_dispatch<8, 4>(a, s);
+    if (a.k == 20 && a.m == 10 && (g_tune.enc_bits & 8)) return enc_bits_dispatch<20, 10>(a, s);
     // Per shape (measured): RS(8,12) and RS(16,24) run the flat grid at
     // g_tune.enc_wpc (3) workgroups per CU; RS(2,3) (2 loads per lane: little in flight per
     // wave) at full residency. The ticket-queue form stays selectable (enc_queue).

@@ -24,6 +24,7 @@
 namespace fk {
 
 Tuning g_tune;
+size_t g_max_lds = 65536;
 
 FastDiv make_fastdiv(uint32_t d) {
     FastDiv f{d, 0, 0};

@@ -158,7 +158,7 @@ struct Tuning {
                               // lookup (1: rows expanded from scalar-loaded coefficients, 2: PermTab rows
                               // copied by a vector load); multi-erasure waves go to a worklist kernel
     int host_chunk = 0;       // host-resident path: blocks per staging chunk (0: 128 MiB worth)
-    int dec_fixk = 1;         // RS(16,24) rebuild with k = 16 at compile time (all 16 loads in flight)
+    int dec_fixk = 1;         // RS(16,24) / RS(20,30) rebuild with k at compile time (all k loads in flight)
     int dec_sorted = 1;       // multi-erasure codes (plan path, shards of 32+ chunks): sorted parallel plans
     int dec_ipl = 0;          // wave-form reconstruct items per lane: 1; 2 loaded together; 3: 2 one
                               // after the other (one plan stage); 0: 2 for k <= 4, else 1
@@ -167,7 +167,7 @@ struct Tuning {
     int dec_pseg = 0;         // sorted plan kernel: segments of blocks per workgroup (0: by batch size)
     int dir_nt = -1;          // direct decode cache policy (3 nt loads + stores, 2 plain loads + nt
                               // stores, 0 plain); -1: by shape, 2 for k <= 4 (RS(2,3) +8 %), else 3
-    int enc_bits = 1;         // bit-sliced XOR-network encode (gen_bitslice.py): bit 0 RS(16,24), bit 1
+    int enc_bits = 9;         // bit-sliced XOR-network encode (gen_bitslice.py): bit 0 RS(16,24), bit 1
                               // RS(8,12), bit 2 loads streamed one network group ahead. Measured
                               // (enc_select.py, one box): RS(16,24) 5.35 -> 6.36 TB/s; RS(8,12)
                               // 6.42 vs 6.51 for the dyadic perm body (off); streamed -0.2 % (off)
@@ -191,6 +191,7 @@ inline uint32_t line_rotation(uint64_t ss, uint32_t cps) {
     return r < cps ? r : 0;
 }
 extern Tuning g_tune;
+extern size_t g_max_lds;   // LDS per workgroup the device allows (set at ctx creation)
 
 hipError_t launch_rs_encode(const EncodeArgs& a, int grid, hipStream_t s);
 // Fixed-shape encode (flat grid, one item per lane) for the shapes it is instantiated for.

@@ -117,7 +117,7 @@ __device__ __forceinline__ void recon_rows_k(const ReconArgs& a, const uint8_t* 
 template <int K, int MAXE, bool NTL, bool NTS>
 __device__ __forceinline__ void recon_item_k(const ReconArgs& a, const uint8_t* P, const gf::PermTab* T,
                                              uint32_t blk, uint32_t c, uint32_t rows, uint32_t nout) {
-    static_assert(K % 8 == 0, "slot words are read 8 at a time");
+    static_assert(K % 2 == 0, "inputs are folded in pairs");
     const PlanLayout& lay = a.lay;
     uint8_t* dblk = a.data + (uint64_t)blk * a.dbs + (uint64_t)c * kChunk;
     const uint8_t* pblk = a.parity + (uint64_t)blk * a.pbs + (uint64_t)c * kChunk;
@@ -128,21 +128,26 @@ __device__ __forceinline__ void recon_item_k(const ReconArgs& a, const uint8_t* 
         const uint2 sl = *reinterpret_cast<const uint2*>(P + lay.in_off + j0);
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
+            if (j0 + jj >= K) break;   // compile-time: the slot area is rounded up to 8 bytes
             const uint32_t slot = ((jj < 4 ? sl.x : sl.y) >> (8 * (jj & 3))) & 0xFFu;
             x[j0 + jj] = ld16<NTL>(slot_addr(dblk, pbase, slot, K, (uint32_t)a.ss, (uint32_t)a.pss));
         }
     }
     uint8_t* oblk = a.out ? a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk : nullptr;
-    static_assert(MAXE <= 8, "row bodies 1..8");
+    // row bodies 1..R (R: the code's largest erasure count, min(k, m): RS(16,24) 8, RS(20,30) 10)
+    constexpr int R = MAXE < K ? (MAXE <= 8 ? MAXE : 10) : K;
+    static_assert(R <= 10, "row bodies 1..10");
     switch (rows) {   // wave-uniform
         case 1: recon_rows_k<K, 1, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
         case 2: recon_rows_k<K, 2, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
         case 3: recon_rows_k<K, 3, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
         case 4: recon_rows_k<K, 4, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
-        case 5: if constexpr (MAXE >= 5) recon_rows_k<K, 5, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
-        case 6: if constexpr (MAXE >= 6) recon_rows_k<K, 6, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
-        case 7: if constexpr (MAXE >= 7) recon_rows_k<K, 7, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
-        default: if constexpr (MAXE >= 8) recon_rows_k<K, 8, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 5: if constexpr (R >= 5) recon_rows_k<K, 5, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 6: if constexpr (R >= 6) recon_rows_k<K, 6, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 7: if constexpr (R >= 7) recon_rows_k<K, 7, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 8: if constexpr (R >= 8) recon_rows_k<K, 8, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 9: if constexpr (R >= 9) recon_rows_k<K, 9, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+        default: if constexpr (R >= 10) recon_rows_k<K, 10, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
     }
 }
 

@@ -23,7 +23,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "csrc", "fec_bitslice.inc")
-SHAPES = ((8, 4, 4), (16, 8, 4))   # (k, m, group size G)
+SHAPES = ((8, 4, 4), (16, 8, 4), (20, 10, 4))   # (k, m, group size G)
 
 # ---------------------------------------------------------------- GF(2^8), poly 0x11D, generator 2
 _EXP = [0] * 512

@@ -298,17 +298,17 @@ ENC_VARIANTS = {
     "queue_d1": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=1),
     "queue_d2": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=2),
     "queue_d1_1wg": dict(enc_fixed=1, enc_queue=1, enc_qwpc=1, enc_qdepth=1),
-    # bit-sliced XOR network (RS(8,12) and RS(16,24); RS(2,3) keeps the fixed kernel)
-    "bits": dict(enc_fixed=1, enc_queue=0, enc_bits=3, enc_bwpc=0),
-    "bits_wpc2": dict(enc_fixed=1, enc_queue=0, enc_bits=3, enc_bwpc=2),
-    "bits_plain": dict(enc_fixed=1, enc_queue=0, enc_bits=3, enc_nt=0),
-    "bits_stream": dict(enc_fixed=1, enc_queue=0, enc_bits=7, enc_bwpc=0),
+    # bit-sliced XOR network (RS(8,12), RS(16,24), RS(20,30); RS(2,3) keeps the fixed kernel)
+    "bits": dict(enc_fixed=1, enc_queue=0, enc_bits=11, enc_bwpc=0),
+    "bits_wpc2": dict(enc_fixed=1, enc_queue=0, enc_bits=11, enc_bwpc=2),
+    "bits_plain": dict(enc_fixed=1, enc_queue=0, enc_bits=11, enc_nt=0),
+    "bits_stream": dict(enc_fixed=1, enc_queue=0, enc_bits=15, enc_bwpc=0),
     "bits_off": dict(enc_fixed=1, enc_queue=0, enc_bits=0),
 }
 
 
 @pytest.mark.parametrize("variant", sorted(ENC_VARIANTS))
-@pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8)])
+@pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10)])
 @pytest.mark.parametrize("B,L", [(1, 1), (3, 17), (37, 1202), (1000, 1202), (4099, 1436), (20000, 33)])
 def test_rs_encode_kernel_variants_match_oracle(codec, oracle, torch, variant, k, m, B, L):
     rng = np.random.default_rng(B * 31 + L * 7 + k)

@@ -28,9 +28,9 @@ def main():
         variants["dyadic flat wpc%d, plain loads" % w] = dict(enc_queue=0, enc_wpc=w, enc_dyadic=1, enc_nt=2)
     variants["matrix flat wpc3, plain loads"] = dict(enc_queue=0, enc_wpc=3, enc_dyadic=0, enc_nt=2)
     for w in (0, 2, 3):
-        variants["bits wpc%d" % w] = dict(enc_queue=0, enc_bits=3, enc_bwpc=w)
-        variants["bits stream wpc%d" % w] = dict(enc_queue=0, enc_bits=7, enc_bwpc=w)
-    variants["bits wpc0, plain loads"] = dict(enc_queue=0, enc_bits=3, enc_bwpc=0, enc_nt=2)
+        variants["bits wpc%d" % w] = dict(enc_queue=0, enc_bits=11, enc_bwpc=w)
+        variants["bits stream wpc%d" % w] = dict(enc_queue=0, enc_bits=15, enc_bwpc=w)
+    variants["bits wpc0, plain loads"] = dict(enc_queue=0, enc_bits=11, enc_bwpc=0, enc_nt=2)
     if k == 8:
         variants["matrix queue d0 wpc2"] = dict(enc_queue=1, enc_qwpc=2, enc_qdepth=0, enc_dyadic=0)
     base = codec.set_tuning(enc_queue=0, enc_wpc=3, enc_qwpc=2, enc_qdepth=0, enc_dyadic=1, enc_nt=3, enc_bits=0,
