@@ -97,8 +97,8 @@ __device__ __forceinline__ void recon_rows_k(const ReconArgs& a, const uint8_t* 
         const gf::PermTab* t = T + toff;
         // the pair's inputs pass through an opaque step here, so their splits are not hoisted
         // ahead of earlier pairs (all splits at once would hold 3 words per input dword)
-        uint4 xa = x[j], xb = x[j + 1];
-        asm volatile("" : "+v"(xa.x), "+v"(xa.y), "+v"(xa.z), "+v"(xa.w), "+v"(xb.x), "+v"(xb.y), "+v"(xb.z), "+v"(xb.w));
+        const uint4 xa = x[j], xb = x[j + 1];
+        __builtin_amdgcn_sched_barrier(0);
         Idx ia[4], ib[4];
         split4(ia, xa);
         split4(ib, xb);
