@@ -1036,6 +1036,18 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
     return old;
 }
 
+// Internal self-test (not part of the public ABI, no device needed): the lane-arithmetic PermTab
+// builder the kernels use equals the byte-wise one for every coefficient. 0 on success, else
+// 1 + the first failing coefficient.
+int fec__selftest_permtab(void) {
+    for (uint32_t c = 0; c < 256; ++c) {
+        const gf::PermTab a = gf::make_permtab((uint8_t)c), b = gf::make_permtab_fast(c);
+        if (a.t0lo != b.t0lo || a.t0hi != b.t0hi || a.t1lo != b.t1lo || a.t1hi != b.t1hi || a.t2 != b.t2)
+            return 1 + (int)c;
+    }
+    return 0;
+}
+
 // Internal diagnostics (not part of the public ABI): the multi-erasure worklist's count and
 // done words of the ctx's own workspace, after waiting for its stream. Both are 0 between calls.
 int fec__worklist_state(fec_ctx* ctx, uint32_t* out2) {

@@ -234,7 +234,7 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
                 const uint32_t r = rem / k, j = rem - r * k;
                 const uint8_t* P = plans + g * lay.stride;
                 const uint8_t c = r < P[lay.nout_off] ? P[lay.coef_off + r * k + j] : 0;
-                tabs[i] = gf::make_permtab(c);
+                tabs[i] = gf::make_permtab_fast(c);
             }
         }
         __syncthreads();
@@ -302,12 +302,13 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
         const uint32_t c0 = plans[lay.nout_off] * k;
         const uint32_t c1 = nb > 1 ? plans[lay.stride + lay.nout_off] * k : 0u;
         const uint32_t c2 = nb > 2 ? plans[2 * lay.stride + lay.nout_off] * k : 0u;
+        const uint32_t kk = K > 0 ? (uint32_t)K : k;   // compile-time k: the division is a shift
         for (uint32_t i = lane; i < c0 + c1 + c2; i += 64) {
             const uint32_t g = (i >= c0) + (i >= c0 + c1);
             const uint32_t rem = i - (g == 0 ? 0u : g == 1 ? c0 : c0 + c1);
-            const uint32_t r = rem / k, j = rem - r * k;
+            const uint32_t r = rem / kk, j = rem - r * kk;
             const uint8_t* P = plans + g * lay.stride;
-            tabs[g * maxe * k + rem] = gf::make_permtab(P[lay.coef_off + r * k + j]);
+            tabs[g * maxe * k + rem] = gf::make_permtab_fast(P[lay.coef_off + r * k + j]);
         }
     }
     wave_sync();

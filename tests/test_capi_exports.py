@@ -64,3 +64,11 @@ def test_context_fails_loudly_without_gpu(fec):
     with pytest.raises(fec.FecError) as e:
         fec.Codec(0)
     assert e.value.code == fec.FEC_ERR_NO_DEVICE
+
+
+def test_lane_permtab_builder_matches_bytewise(fec):
+    # the rebuild kernels expand coefficient rows with gf::make_permtab_fast (32-bit lane
+    # arithmetic, v_perm byte moves restated on the host); it must equal the byte-wise table
+    # builder for all 256 coefficients
+    lib = ctypes.CDLL(fec._LIB_PATH)
+    assert lib.fec__selftest_permtab() == 0
