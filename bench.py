@@ -72,6 +72,10 @@ def parse():
     p.add_argument("--cpu-sample-blocks", type=int, default=1 << 15)
     p.add_argument("--host-blocks", type=int, default=1 << 17,
                    help="blocks of the host-resident (PCIe-inclusive) measurement, rank 0 at N=1; 0: skip")
+    p.add_argument("--rehearse-one-gpu", action="store_true",
+                   help="diagnostics only: every torchrun rank on cuda:0 with gloo (RCCL refuses two ranks "
+                        "on one device), to exercise the N>1 code path on a one-GPU box; its timings are "
+                        "contended and never a result")
     return p.parse_args()
 
 
@@ -271,8 +275,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rehearse_one_gpu:
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.rehearse_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     fec = importlib.import_module("0xfec_amd")
@@ -329,10 +338,11 @@ def main():
     codec.sync()
     inplace_ms = e0.elapsed_time(e1) / reps
     if world > 1:
-        t = torch.tensor([step_ms, enc_ms, dec_ms, inplace_ms], device=dev, dtype=torch.float64)
+        rdev = "cpu" if args.rehearse_one_gpu else dev   # gloo reduces host tensors
+        t = torch.tensor([step_ms, enc_ms, dec_ms, inplace_ms], device=rdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         step_ms, enc_ms, dec_ms, inplace_ms = t.tolist()
-        okt = torch.tensor([1 if ok_roundtrip else 0], device=dev)
+        okt = torch.tensor([1 if ok_roundtrip else 0], device=rdev)
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok_roundtrip = bool(okt.item())
 
