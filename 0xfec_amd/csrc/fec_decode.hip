@@ -253,10 +253,14 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
     }
 }
 
-// K: compile-time data shard count for the IPL = 1 body (0: runtime a.k).
-template <int MAXE, int POL, bool FUSED, int IPL, int K = 0>
+// K: compile-time data shard count for the IPL = 1 body (0: runtime a.k); W > 0: that body with a
+// rolling window of W loaded inputs (recon_item_roll) instead of all K up front.
+template <int MAXE, int POL, bool FUSED, int IPL, int K = 0, int W = 0>
 __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs a) {
     constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
+    // blocks per wave slice: the rolling form is launched for shards of 64+ chunks only, where
+    // 64 consecutive items span at most 2 blocks (smaller slices: more workgroups per CU)
+    constexpr uint32_t WB = W > 0 ? 2u : kWaveBlocks;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t k = a.k, maxe = a.maxe;
     const PlanLayout lay = a.lay;
@@ -277,10 +281,10 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
         s_prows = p8;
         slice = smem + L.slices + (size_t)wave * L.slice;
     } else {
-        slice = smem + (size_t)wave * wave_slice_bytes(k, maxe, lay.stride);
+        slice = smem + (size_t)wave * wave_slice_bytes(k, maxe, lay.stride, WB);
     }
-    gf::PermTab* tabs = reinterpret_cast<gf::PermTab*>(slice);                      // 3*maxe*k
-    uint8_t* plans = slice + (size_t)kWaveBlocks * maxe * k * sizeof(gf::PermTab);  // 3*stride
+    gf::PermTab* tabs = reinterpret_cast<gf::PermTab*>(slice);             // WB*maxe*k
+    uint8_t* plans = slice + (size_t)WB * maxe * k * sizeof(gf::PermTab);  // WB*stride
     const uint32_t total = a.nblocks * a.cps;
     constexpr uint32_t NI = IPL < 0 ? -IPL : IPL;   // items per lane; IPL < 0: one after the other
     const uint32_t i0 = (xcd_order(a.swz) * kThreads + (wave << 6)) * NI;
@@ -337,7 +341,8 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
         const uint32_t rows = wave_rows<MAXE>(nout);
         if (nout == 0) return;
         const uint32_t rb = a.sorted ? *reinterpret_cast<const uint32_t*>(P + lay.blk_off) : blk;
-        if constexpr (K > 0) recon_item_k<K, MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
+        if constexpr (K > 0 && W > 0) recon_item_roll<K, MAXE, W, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
+        else if constexpr (K > 0) recon_item_k<K, MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
         else recon_item<MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
     } else {
         const uint32_t itA = i0 + lane, itB = itA + 64;
@@ -401,13 +406,22 @@ static hipError_t recon_wave_dispatch(const ReconArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((rs_reconstruct_wave_kernel<E, POL, FUSED, IPL>), dim3(grid), dim3(kThreads), lds, s, a)
     // the benchmark's multi-erasure code RS(16,24) with its K known at compile time
     if constexpr (IPL == 1 && !FUSED) {
+        // rolling load window (dec_fixk 2): 120 instead of 163 VGPRs and 2-block wave slices, so
+        // 4 instead of 3 workgroups per CU; RS(16,24) +1.7 % (dec_select.py, interleaved A/B)
+        const bool roll = g_tune.dec_fixk == 2 && a.cps >= 64;
+        const size_t lds2 = occupancy_lds(g_tune.dec_wpc, 4 * wave_slice_bytes(a.k, a.maxe, a.lay.stride, 2));
         if (a.k == 16 && a.maxe == 8 && g_tune.dec_fixk) {
-            hipLaunchKernelGGL((rs_reconstruct_wave_kernel<8, POL, false, 1, 16>), dim3(grid), dim3(kThreads), lds,
-                               s, a);
+            if (roll)
+                hipLaunchKernelGGL((rs_reconstruct_wave_kernel<8, POL, false, 1, 16, 8>), dim3(grid), dim3(kThreads),
+                                   lds2, s, a);
+            else
+                hipLaunchKernelGGL((rs_reconstruct_wave_kernel<8, POL, false, 1, 16>), dim3(grid), dim3(kThreads),
+                                   lds, s, a);
             return hipGetLastError();
         }
         // the reference's own receiver code RS(20,30) (manager.go:80-90)
         if (a.k == 20 && a.maxe == 10 && g_tune.dec_fixk) {
+            // (the rolling window measured -0.8 % here: 203 VGPRs, still 2 waves/SIMD)
             hipLaunchKernelGGL((rs_reconstruct_wave_kernel<16, POL, false, 1, 20>), dim3(grid), dim3(kThreads), lds,
                                s, a);
             return hipGetLastError();

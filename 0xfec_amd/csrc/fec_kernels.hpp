@@ -158,7 +158,9 @@ struct Tuning {
                               // lookup (1: rows expanded from scalar-loaded coefficients, 2: PermTab rows
                               // copied by a vector load); multi-erasure waves go to a worklist kernel
     int host_chunk = 0;       // host-resident path: blocks per staging chunk (0: 128 MiB worth)
-    int dec_fixk = 1;         // RS(16,24) / RS(20,30) rebuild with k at compile time (all k loads in flight)
+    int dec_fixk = 2;         // RS(16,24) / RS(20,30) rebuild with k at compile time (1: all k loads in
+                              // flight; 2: RS(16,24) with a rolling window of 8 loaded inputs, shards of
+                              // 64+ chunks)
     int dec_sorted = 1;       // multi-erasure codes (plan path, shards of 32+ chunks): sorted parallel plans
     int dec_ipl = 0;          // wave-form reconstruct items per lane: 1; 2 loaded together; 3: 2 one
                               // after the other (one plan stage); 0: 2 for k <= 4, else 1

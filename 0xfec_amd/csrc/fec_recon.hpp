@@ -151,6 +151,81 @@ __device__ __forceinline__ void recon_item_k(const ReconArgs& a, const uint8_t* 
     }
 }
 
+// recon_rows_k with a rolling load window (dec_fixk = 2): W inputs are loaded up front, and each
+// folded pair's registers take the loads of the pair W inputs ahead, so at most W inputs are
+// live instead of K (K = 16: 64 -> 32 data VGPRs), for more resident waves per SIMD.
+template <int K, int ROWS, int W, bool NTL, bool NTS>
+__device__ __forceinline__ void recon_rows_roll(const ReconArgs& a, const uint8_t* P, const gf::PermTab* T,
+                                                uint8_t* dblk, const uint8_t* pbase, uint8_t* oblk, uint32_t c,
+                                                uint32_t nout) {
+    static_assert(K % 2 == 0 && W % 2 == 0 && W <= K, "inputs are folded and loaded in pairs");
+    constexpr int NS = (K + 7) / 8;   // the slot area is rounded up to 8 bytes
+    uint2 sl[NS];
+#pragma unroll
+    for (int g = 0; g < NS; ++g) sl[g] = *reinterpret_cast<const uint2*>(P + a.lay.in_off + 8 * g);
+    auto load = [&](int j) {
+        const uint32_t w = (j & 7) < 4 ? sl[j >> 3].x : sl[j >> 3].y;
+        const uint32_t slot = (w >> (8 * (j & 3))) & 0xFFu;
+        return ld16<NTL>(slot_addr(dblk, pbase, slot, K, (uint32_t)a.ss, (uint32_t)a.pss));
+    };
+    uint4 x[K];
+#pragma unroll
+    for (int j = 0; j < W; ++j) x[j] = load(j);
+    uint32_t acc[ROWS][4];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0;
+#pragma unroll
+    for (int j = 0; j < K; j += 2) {
+        uint32_t toff = 0;
+        asm volatile("" : "+s"(toff));
+        const gf::PermTab* t = T + toff;
+        const uint4 xa = x[j], xb = x[j + 1];
+        __builtin_amdgcn_sched_barrier(0);
+        Idx ia[4], ib[4];
+        split4(ia, xa);
+        split4(ib, xb);
+        // the pair W inputs ahead goes out once this pair's inputs are split
+        if (j + W < K) {
+            x[j + W] = load(j + W);
+            x[j + W + 1] = load(j + W + 1);
+        }
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) mac2(acc[r], ia, ib, t + r * K + j, t + r * K + j + 1);
+    }
+    const uint32_t nb = a.len - c * kChunk;
+    const uint8_t* out_idx = P + a.lay.out_off;
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r)
+        if (r < (int)nout)
+            store_chunk<NTS>(oblk ? oblk + (uint64_t)r * a.ss : dblk + (uint64_t)out_idx[r] * a.ss, as_uint4(acc[r]),
+                             nb, a.pad_zero);
+}
+
+template <int K, int MAXE, int W, bool NTL, bool NTS>
+__device__ __forceinline__ void recon_item_roll(const ReconArgs& a, const uint8_t* P, const gf::PermTab* T,
+                                                uint32_t blk, uint32_t c, uint32_t rows, uint32_t nout) {
+    uint8_t* dblk = a.data + (uint64_t)blk * a.dbs + (uint64_t)c * kChunk;
+    const uint8_t* pblk = a.parity + (uint64_t)blk * a.pbs + (uint64_t)c * kChunk;
+    const uint8_t* pbase = parity_base(pblk, K, a.pss);
+    uint8_t* oblk = a.out ? a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk : nullptr;
+    constexpr int R = MAXE < K ? (MAXE <= 8 ? MAXE : 10) : K;
+    static_assert(R <= 10, "row bodies 1..10");
+#define FEC_ROLL_ROWS(N) recon_rows_roll<K, N, W, NTL, NTS>(a, P, T, dblk, pbase, oblk, c, nout)
+    switch (rows) {   // wave-uniform
+        case 1: FEC_ROLL_ROWS(1); break;
+        case 2: FEC_ROLL_ROWS(2); break;
+        case 3: FEC_ROLL_ROWS(3); break;
+        case 4: FEC_ROLL_ROWS(4); break;
+        case 5: if constexpr (R >= 5) FEC_ROLL_ROWS(5); break;
+        case 6: if constexpr (R >= 6) FEC_ROLL_ROWS(6); break;
+        case 7: if constexpr (R >= 7) FEC_ROLL_ROWS(7); break;
+        case 8: if constexpr (R >= 8) FEC_ROLL_ROWS(8); break;
+        case 9: if constexpr (R >= 9) FEC_ROLL_ROWS(9); break;
+        default: if constexpr (R >= 10) FEC_ROLL_ROWS(10); break;
+    }
+#undef FEC_ROLL_ROWS
+}
+
 template <int MAXE>
 __device__ __forceinline__ uint32_t wave_rows(uint32_t nout) {
     uint32_t rows = 0;
@@ -166,8 +241,9 @@ __device__ __forceinline__ uint32_t wave_rows(uint32_t nout) {
 // between a wave's plan load and its data loads.
 constexpr uint32_t kWaveBlocks = 3;
 
-__host__ __device__ inline size_t wave_slice_bytes(uint32_t k, uint32_t maxe, uint32_t stride) {
-    return (size_t)kWaveBlocks * maxe * k * 32 + (size_t)kWaveBlocks * stride;
+__host__ __device__ inline size_t wave_slice_bytes(uint32_t k, uint32_t maxe, uint32_t stride,
+                                                   uint32_t nblk = kWaveBlocks) {
+    return (size_t)nblk * maxe * k * 32 + (size_t)nblk * stride;
 }
 
 // Fused form: the wave also builds its blocks' plan records (the work of rs_plan_kernel) from

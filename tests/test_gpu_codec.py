@@ -338,8 +338,10 @@ def test_rs_encode_kernel_variants_match_oracle(codec, oracle, torch, variant, k
 # of 64+ chunks, at most 4 erasures per block); 5, 6: as 1, 2 with two items one after the other;
 # 7: the direct form (fec_recover.hip: single-erasure tables, in-wave plans for waves holding a
 # multi-erasure block) where the code's tables fit, else as 1; 1, 3, 5 use the sorted parallel
-# plans (fec_plan.hip), 8 is 1 with the one-lane-per-block plan kernel in block order
-@pytest.mark.parametrize("wave", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+# plans (fec_plan.hip), 8 is 1 with the one-lane-per-block plan kernel in block order, 9 is 1
+# with the compile-time-k rebuild loading all k inputs up front (1 and the rest: RS(16,24) with
+# the rolling load window where shards have 64+ chunks)
+@pytest.mark.parametrize("wave", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10)])
 @pytest.mark.parametrize("L", [513, 1202, 1436])
 def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, wave, k, m, L):
@@ -358,7 +360,7 @@ def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, 
     dm = torch.from_numpy(masks.view(np.int32)).cuda()
     old = codec.set_tuning(dec_wave=1 if wave else 0, dec_fused=1 if wave in (2, 4, 6) else 0,
                            dec_ipl={3: 2, 4: 2, 5: 3, 6: 3}.get(wave, 1), dec_direct=1 if wave == 7 else 0,
-                           dec_sorted=0 if wave == 8 else 1)
+                           dec_sorted=0 if wave == 8 else 1, dec_fixk=1 if wave == 9 else 2)
     try:
         out = torch.full((B, m, S), 0xEE, dtype=torch.uint8, device="cuda")
         data = torch.from_numpy(data_np).cuda()

@@ -50,7 +50,7 @@ def main():
     dp, pp, op = data.data_ptr(), par.data_ptr(), out.data_ptr()
     # every knob any variant sets, at its default: tune(D) must undo each variant completely
     D = dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=1, dec_ipl=0, dec_direct=1, dec_nt=3, dir_wpc=-1, dir_nt=-1,
-             dec_fixk=1, dec_sorted=1, dec_pseg=0)
+             dec_fixk=2, dec_sorted=1, dec_pseg=0)
     variants = {"direct (default)": D,
                 "direct, PermTab rows by vector load": dict(D, dec_direct=2),
                 "direct noswz": dict(D, dec_swz=0),
@@ -63,6 +63,9 @@ def main():
     if args.multi:   # the plan + wave path: residency, cache policy, compile-time k, plan form
         variants = {"default": D}
         variants["wave runtime k"] = dict(D, dec_fixk=0)
+        variants["compile-time k, all k loads up front"] = dict(D, dec_fixk=1)
+        for w in (3, 4):
+            variants["rolling window wpc%d" % w] = dict(D, dec_wpc=w)
         for w in (2, 3):
             variants["K=16 wpc%d" % w] = dict(D, dec_wpc=w)
         variants["unsorted plans"] = dict(D, dec_sorted=0)
