@@ -35,7 +35,7 @@ SHARD_STRIDE = 1216              # 16-byte aligned device slot per shard
 HBM_PEAK = 8.0e12                # MI355X HBM3E spec, bytes/s (MI355X_MICROARCH.md)
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of this bench (separate passes, tools/pmc_traffic.py,
 # gfx950 FETCH_SIZE x2 correction): HBM bytes per launch of each codec kernel
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02", "pmc_traffic_r02g.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02", "pmc_traffic_r02h.json")
 
 
 def encode_kernel_name(k, m):
