@@ -343,7 +343,8 @@ def test_rs_encode_kernel_variants_match_oracle(codec, oracle, torch, variant, k
 # the rolling load window where shards have 64+ chunks)
 @pytest.mark.parametrize("wave", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10)])
-@pytest.mark.parametrize("L", [513, 1202, 1436])
+# L = 1008 / 1017: shards of 63 / 64 chunks, the edge of the two-block wave slices (rolling window)
+@pytest.mark.parametrize("L", [513, 1008, 1017, 1202, 1436])
 def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, wave, k, m, L):
     rng = np.random.default_rng(11 * k + L + wave)
     n, B = k + m, 389
