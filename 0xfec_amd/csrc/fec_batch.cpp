@@ -46,6 +46,11 @@ size_t RepairQueue::Len() {
     return q_.size();
 }
 
+bool RepairQueue::Closed() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return closed_;
+}
+
 // ------------------------------------------------------------------ BatchEncoder
 
 namespace {
@@ -134,7 +139,7 @@ Error BatchEncoder::Submit(Block& b, RepairQueue* q) {
     e = rs_ ? rs_->stageRepairInput(b, dst, s->slot, &L) : xor_->stageRepairInput(b, dst, s->slot, &L, &count);
     if (!e.ok()) return e;
     if (xor_ && count != k_) return Error::text("block does not match the encoder's source symbol count");
-    s->blocks.push_back(Pending{q, b.id, L});
+    s->blocks.push_back(Pending{q, q ? q->token() : nullptr, b.id, L});
     s->maxLen = std::max(s->maxLen, L);
     return Error::nil();
 }
@@ -184,7 +189,7 @@ Error BatchEncoder::SubmitPayloads(BlockID id, const uint8_t* const* payloads, c
         slot[biggest] = (uint8_t)(lens[i] >> 8);
         slot[biggest + 1] = (uint8_t)(lens[i] & 0xFF);
     }
-    s->blocks.push_back(Pending{q, id, L});
+    s->blocks.push_back(Pending{q, q ? q->token() : nullptr, id, L});
     s->maxLen = std::max(s->maxLen, L);
     return Error::nil();
 }
@@ -254,7 +259,7 @@ Error BatchEncoder::retire(Set& s) {
             raw_.push_back(std::move(rb));
             continue;
         }
-        Ready r{p.q, p.id, {}};
+        Ready r{p.q, p.tok, p.id, {}};
         r.payloads.reserve((size_t)m_);
         for (int j = 0; j < m_; ++j) {
             // repairSymbols makes RS payloads as make([]byte, 0, MaxPacketBufferSize)[:L']
@@ -278,16 +283,18 @@ bool BatchEncoder::pump(size_t* blocks) {
             ++it;
             continue;
         }
-        if (it->q->Len() + it->payloads.size() > it->q->MaxLen()) {
-            held.push_back(it->q);
-            ++it;
-            continue;
+        std::lock_guard<std::mutex> lk(it->tok->mu);   // the queue cannot be freed meanwhile
+        // a freed or closed queue drops its frames, as the reference's closed connection would
+        if (it->tok->alive && !it->q->Closed()) {
+            if (it->q->Len() + it->payloads.size() > it->q->MaxLen()) {
+                held.push_back(it->q);
+                ++it;
+                continue;
+            }
+            for (size_t j = 0; j < it->payloads.size(); ++j)
+                (void)it->q->Add(RepairFrame{it->id, (ParityID)j, it->payloads[j]});
+            if (blocks) ++*blocks;
         }
-        bool ok = true;
-        for (size_t j = 0; j < it->payloads.size(); ++j)
-            if (!it->q->Add(RepairFrame{it->id, (ParityID)j, it->payloads[j]}).ok()) ok = false;   // closed queue
-        (void)ok;   // a closed queue drops its frames, as the reference's connection would
-        if (blocks) ++*blocks;
         it = backlog_.erase(it);
     }
     return backlog_.empty();
@@ -470,6 +477,7 @@ Error BatchDecoder::submitWith(size_t want, RecoveredQueue* q, bool* staged, Sta
     s->maxLen = std::max(s->maxLen, rs_ ? p.plan.len : s->slot);
     s->outSlots = std::max(s->outSlots, rs_ ? p.plan.missing.size() : (size_t)1);
     p.q = q;
+    p.tok = q->token();
     s->blocks.push_back(std::move(p));
     if (staged) *staged = true;
     return Error::nil();
@@ -581,8 +589,11 @@ Error BatchDecoder::deliver(Set& s, size_t* blocks) {
             e = xor_->finishRecover(p.meta, s.h_out + s.delivered * S, S, &out);
         }
         if (!e.ok()) return e;
-        p.q->Push(RecoveredQueue::Item{p.id, out});
-        if (blocks) ++*blocks;
+        std::lock_guard<std::mutex> lk(p.tok->mu);
+        if (p.tok->alive) {   // a freed queue (its connection closed) drops the block
+            p.q->Push(RecoveredQueue::Item{p.id, out});
+            if (blocks) ++*blocks;
+        }
     }
     s.blocks.clear();
     s.maxLen = s.outSlots = s.delivered = 0;

@@ -125,6 +125,7 @@ struct fec_ctx {
     int grid_cache[3][6] = {};
     int ncu = 256;           // compute units of the device
     HostSet hs[2];           // host-resident path: two staging sets, each with its own stream
+    hipEvent_t handoff = nullptr;   // orders a newly set stream after the previous one
 };
 
 #define HIP_TRY(expr)                      \
@@ -995,15 +996,31 @@ void fec_ctx_destroy(fec_ctx* ctx) {
         if (s.done) (void)hipEventDestroy(s.done);
         if (s.s) (void)hipStreamDestroy(s.s);
     }
+    if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
     if (ctx->own) (void)hipStreamDestroy(ctx->own);
     (void)hipGetLastError();
     delete ctx;
 }
 
+// Switch the ctx to `next`. The ctx's own / caller's stream share one workspace (`main`: plan
+// records, the self-rewinding worklist, ticket counters), so work already queued on the old
+// stream must finish before anything on the new one touches it: the new stream waits on an
+// event recorded on the old one (no host wait). grow_* then sync only the current stream,
+// which by this wait covers the old one's kernels too.
+static int switch_stream(fec_ctx* ctx, hipStream_t next) {
+    if (next == ctx->stream) return FEC_OK;
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    if (!ctx->handoff) HIP_TRY(hipEventCreateWithFlags(&ctx->handoff, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(ctx->handoff, ctx->stream));
+    HIP_TRY(hipStreamWaitEvent(next, ctx->handoff, 0));
+    ctx->stream = next;
+    return FEC_OK;
+}
+
 int fec_ctx_set_stream(fec_ctx* ctx, void* hip_stream) {
     if (!ctx) return FEC_ERR_INVALID_ARG;
-    ctx->stream = (hipStream_t)hip_stream;
-    return FEC_OK;
+    return switch_stream(ctx, (hipStream_t)hip_stream);
 }
 
 // Internal tuning knob (not part of the public ABI; process-wide): kernel variants and grid
@@ -1062,8 +1079,7 @@ int fec__worklist_state(fec_ctx* ctx, uint32_t* out2) {
 
 int fec_ctx_reset_stream(fec_ctx* ctx) {
     if (!ctx) return FEC_ERR_INVALID_ARG;
-    ctx->stream = ctx->own;
-    return FEC_OK;
+    return switch_stream(ctx, ctx->own);
 }
 
 void* fec_ctx_stream(fec_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }

@@ -16,12 +16,16 @@
 namespace fec {
 namespace cabi {
 int report(const fec::Error& e);
-std::shared_ptr<fec::Engine> engine_for(int device);
 }  // namespace cabi
 }  // namespace fec
 
-using fec::cabi::engine_for;
 using fec::cabi::report;
+
+// Each encoder / decoder owns its Engine (its own fec_ctx: stream, workspace, sticky error).
+// The Go side makes one per connection and drives it from that connection's run loop
+// (connection.go:525), whose goroutine migrates between OS threads: a ctx shared per OS thread
+// (fec_scheme.cpp engine_for) would be driven by two connections at once from two threads.
+static std::shared_ptr<fec::Engine> own_engine(int device) { return std::make_shared<fec::Engine>(device); }
 
 struct fec_go_encoder {
     int k = 0, m = 0;
@@ -51,7 +55,7 @@ fec_go_encoder* fec_go_encoder_new(int scheme_id, int k, int m, size_t max_block
     std::unique_ptr<fec_go_encoder> e(new fec_go_encoder());
     e->k = k;
     e->m = scheme_id == FEC_SCHEME_XOR ? 1 : m;
-    const int rc = report(fec::BatchEncoder::New(scheme_of(scheme_id), k, m, max_blocks, engine_for(device), &e->enc));
+    const int rc = report(fec::BatchEncoder::New(scheme_of(scheme_id), k, m, max_blocks, own_engine(device), &e->enc));
     if (err) *err = rc;
     return rc ? nullptr : e.release();
 }
@@ -121,7 +125,7 @@ fec_go_decoder* fec_go_decoder_new(int scheme_id, int k, int m, size_t max_block
     std::unique_ptr<fec_go_decoder> d(new fec_go_decoder());
     d->k = k;
     d->m = scheme_id == FEC_SCHEME_XOR ? 1 : m;
-    const int rc = report(fec::BatchDecoder::New(scheme_of(scheme_id), k, m, max_blocks, engine_for(device), &d->dec));
+    const int rc = report(fec::BatchDecoder::New(scheme_of(scheme_id), k, m, max_blocks, own_engine(device), &d->dec));
     if (err) *err = rc;
     return rc ? nullptr : d.release();
 }
@@ -190,28 +194,24 @@ int fec_go_decoder_poll(fec_go_decoder* d, int wait, uint64_t* block_ids, uint32
     if (!d || (max_blocks && (!block_ids || !lens || !offsets || (out_cap && !out)))) return FEC_ERR_INVALID_ARG;
     const fec::Error err = wait ? d->dec->Drain() : d->dec->Poll();
     if (!err.ok()) return report(err);
-    size_t n = 0, used = 0;
+    // take the queue, hand out what fits from the front, put the rest back in order
+    std::vector<fec::RecoveredQueue::Item> all;
     fec::RecoveredQueue::Item it;
-    std::vector<fec::RecoveredQueue::Item> hold;
-    while (n < max_blocks && d->q.Len()) {
-        d->q.Pop(&it);
-        if (used + it.payload.len > out_cap) {   // does not fit: keep it for the next poll
-            hold.push_back(std::move(it));
-            break;
-        }
-        block_ids[n] = it.block_id;
-        lens[n] = (uint32_t)it.payload.len;
+    while (d->q.Pop(&it)) all.push_back(std::move(it));
+    size_t n = 0, used = 0;
+    for (; n < max_blocks && n < all.size() && used + all[n].payload.len <= out_cap; ++n) {
+        block_ids[n] = all[n].block_id;
+        lens[n] = (uint32_t)all[n].payload.len;
         offsets[n] = used;
-        if (it.payload.len) memcpy(out + used, it.payload.data(), it.payload.len);
-        used += it.payload.len;
-        ++n;
+        if (all[n].payload.len) memcpy(out + used, all[n].payload.data(), all[n].payload.len);
+        used += all[n].payload.len;
     }
-    if (!hold.empty()) {   // back to the front, ahead of the rest
-        std::vector<fec::RecoveredQueue::Item> rest;
-        while (d->q.Pop(&it)) rest.push_back(std::move(it));
-        for (auto& h : hold) d->q.Push(std::move(h));
-        for (auto& r : rest) d->q.Push(std::move(r));
-    }
+    const bool head_too_big = n == 0 && max_blocks && !all.empty();
+    const size_t need = head_too_big ? all[0].payload.len : 0;
+    for (size_t i = n; i < all.size(); ++i) d->q.Push(std::move(all[i]));
+    if (head_too_big)   // the next payload alone exceeds out_cap: polling again would never progress
+        return report(fec::Error{"recovered payload of " + std::to_string(need) + " bytes exceeds the poll buffer",
+                                 FEC_ERR_INVALID_ARG});
     if (nblocks) *nblocks = n;
     return report(fec::Error::nil());
 }

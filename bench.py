@@ -18,6 +18,10 @@ Inputs are resident in HBM before timing starts. value = payload GiB/s over all 
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
+`python bench.py --gpus N` with N > 1 and no torchrun environment starts torchrun itself, as a
+child process, before anything touches the GPU, and exits with its status; it refuses (exit 2)
+when fewer than N devices are visible. Under torchrun, a WORLD_SIZE different from --gpus is
+refused as well, so an N-GPU request never comes back as a 1-GPU number.
 """
 import argparse
 import importlib
@@ -267,8 +271,38 @@ def oracle_parity(k, m, data):
     return sh[:, k:]
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(args):
+    """--gpus N > 1 without a torchrun environment: run torchrun with N ranks as a child process
+    (this process has not touched the GPU: torch.cuda.device_count() does not initialise it on
+    this image) and return its exit status. Rank 0 prints the JSON line."""
+    import subprocess
+    import torch
+    have = torch.cuda.device_count()
+    if args.gpus > have and not args.rehearse_one_gpu:
+        print("bench.py: --gpus %d requested but only %d HIP device(s) are visible; refusing to report "
+              "a smaller run as an %d-GPU number" % (args.gpus, have, args.gpus), file=sys.stderr, flush=True)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    if world_env is not None and int(world_env) != args.gpus:
+        print("bench.py: WORLD_SIZE=%s but --gpus %d; refusing to mislabel the run" % (world_env, args.gpus),
+              file=sys.stderr, flush=True)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 
@@ -337,8 +371,14 @@ def main():
     e1.record(stream)
     codec.sync()
     inplace_ms = e0.elapsed_time(e1) / reps
+    rank_step_ms = [step_ms]
+    ranks_seen = 1
     if world > 1:
         rdev = "cpu" if args.rehearse_one_gpu else dev   # gloo reduces host tensors
+        ranks_seen = dist.get_world_size()
+        per = [torch.zeros(1, device=rdev, dtype=torch.float64) for _ in range(ranks_seen)]
+        dist.all_gather(per, torch.tensor([step_ms], device=rdev, dtype=torch.float64))
+        rank_step_ms = [float(x.item()) for x in per]
         t = torch.tensor([step_ms, enc_ms, dec_ms, inplace_ms], device=rdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         step_ms, enc_ms, dec_ms, inplace_ms = t.tolist()
@@ -380,6 +420,8 @@ def main():
             "value": round(value, 2),
             "unit": "GiB/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
+            "rank_ms_per_step": [round(x, 4) for x in rank_step_ms],
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(step_ms, 4),
@@ -392,7 +434,8 @@ def main():
             "config": {"workload": "RS(k=%d,n=%d) encode + random single-data-erasure decode" % (k, n),
                        "blocks_per_gpu": B, "payload_bytes": PAYLOAD, "shard_len": L,
                        "shard_stride": SHARD_STRIDE, "layout": "data [B][k][1216] + parity [B][m][1216] buffers",
-                       "parallelism": "independent block ranges per GPU"},
+                       "parallelism": "independent block ranges per GPU",
+                       "rehearsal": bool(args.rehearse_one_gpu and world > 1)},
             "roofline": {"bound": "hbm", "achieved": round(dom_bw / 1e9, 1), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(dom_bw / HBM_PEAK, 4),
                          "traffic": None if traffic is None else round(traffic / 1e9, 3),

@@ -35,6 +35,18 @@
 
 namespace fec {
 
+// Liveness of a queue that a batch coder holds by pointer until a batch completes: a queue
+// freed in the meantime (its connection closed) is marked dead under `mu`, and the coder drops
+// that queue's blocks instead of touching the freed object.
+struct QueueToken {
+    std::mutex mu;
+    bool alive = true;
+};
+inline void kill_token(const std::shared_ptr<QueueToken>& t) {
+    std::lock_guard<std::mutex> lk(t->mu);
+    t->alive = false;
+}
+
 // repair_queue.go:17-99
 class RepairQueue {
 public:
@@ -42,6 +54,11 @@ public:
 
     explicit RepairQueue(std::function<void()> hasData = nullptr, size_t maxLen = kMaxRepairSendQueueLen)
         : hasData_(std::move(hasData)), maxLen_(maxLen) {}
+    ~RepairQueue() { kill_token(token_); }
+    RepairQueue(const RepairQueue&) = delete;
+    RepairQueue& operator=(const RepairQueue&) = delete;
+    const std::shared_ptr<QueueToken>& token() const { return token_; }
+    bool Closed();
     // Add queues a new REPAIR frame for sending (repair_queue.go:40-69).
     Error Add(RepairFrame f);
     // Peek gets the next REPAIR frame for sending; nullptr when empty (repair_queue.go:73-80).
@@ -61,6 +78,7 @@ private:
     size_t maxLen_;
     bool closed_ = false;
     Error closeErr_;
+    std::shared_ptr<QueueToken> token_ = std::make_shared<QueueToken>();
 };
 
 class BatchEncoder {
@@ -94,7 +112,10 @@ public:
     Error Flush();
     // Deliver the frames of every completed batch (non-blocking); *blocks = blocks delivered.
     // Frames that do not fit their queue stay in the encoder's backlog (per queue in order)
-    // and go out on a later Poll / Drain; the call then returns "repair queue full".
+    // and go out on a later Poll / Drain; the call then returns "repair queue full" (the
+    // blocks it did deliver are counted in *blocks all the same). The backlog holds at most
+    // the blocks submitted and not yet delivered: it grows only while a queue stays full, and
+    // a queue that is closed or freed has its blocks dropped at the next Poll / Drain.
     // Backpressure never fails Submit: a staging set whose frames cannot be delivered yet
     // moves them to the backlog and is reused.
     Error Poll(size_t* blocks = nullptr);
@@ -110,6 +131,7 @@ public:
 private:
     struct Pending {
         RepairQueue* q;
+        std::shared_ptr<QueueToken> tok;   // q's liveness (null without a queue)
         BlockID id;
         size_t len;
     };
@@ -127,6 +149,7 @@ private:
     std::deque<RawBlock> raw_;
     struct Ready {                  // an encoded block whose frames wait for queue room
         RepairQueue* q;
+        std::shared_ptr<QueueToken> tok;
         BlockID id;
         std::vector<Slice> payloads;   // m repair payloads, ParityID = index
     };
@@ -163,13 +186,19 @@ public:
         BlockID block_id;
         Slice payload;   // recoverSymbolPayloads' result (the concatenation, or XOR's payload)
     };
+    RecoveredQueue() = default;
+    ~RecoveredQueue() { kill_token(token_); }
+    RecoveredQueue(const RecoveredQueue&) = delete;
+    RecoveredQueue& operator=(const RecoveredQueue&) = delete;
     void Push(Item it);
     bool Pop(Item* out);   // false when empty
     size_t Len();
+    const std::shared_ptr<QueueToken>& token() const { return token_; }
 
 private:
     std::mutex mu_;
     std::deque<Item> q_;
+    std::shared_ptr<QueueToken> token_ = std::make_shared<QueueToken>();
 };
 
 // Deferred, batched recoverSymbolPayloads: recoverable blocks of any number of connections are
@@ -203,6 +232,7 @@ public:
 private:
     struct Pending {
         RecoveredQueue* q;
+        std::shared_ptr<QueueToken> tok;   // q's liveness
         BlockID id;
         Block meta;                // id, biggest, SSID range (payload maps not kept)
         ReedSolomonScheme::RecoverPlan plan;   // RS: mask, length, missing indices

@@ -30,7 +30,10 @@
  *
  * Errors: 0, FEC_ERR_SCHEME with the reference's text in fec_last_error() (fec_scheme.h), or a
  * fec_hip.h code. An encoder / decoder is used by one goroutine at a time (the reference's
- * manager is per connection and not thread-safe, manager.go:41-48).
+ * manager is per connection and not thread-safe, manager.go:41-48); that goroutine may move
+ * between OS threads from call to call. Each encoder / decoder owns its fec_ctx (stream,
+ * workspace, sticky device error), so different ones may be driven concurrently from any
+ * threads, whichever thread created them.
  */
 #ifndef FEC_GO_H
 #define FEC_GO_H
@@ -90,7 +93,9 @@ int fec_go_decoder_submit(fec_go_decoder *d, uint64_t block_id, uint64_t smalles
 void fec_go_decoder_drop(fec_go_decoder *d, uint64_t block_id);
 int fec_go_decoder_flush(fec_go_decoder *d);
 /* Recovered blocks, in commit order: block_ids[d], its payload (recoverSymbolPayloads' result)
- * at out + offsets[d], lens[d] bytes; stops before max_blocks or when out_cap would overflow. */
+ * at out + offsets[d], lens[d] bytes; stops before max_blocks or when out_cap would overflow.
+ * When the next payload alone is larger than out_cap: FEC_ERR_INVALID_ARG with the needed size
+ * in fec_last_error(), nothing is taken (poll again with a larger buffer). */
 int fec_go_decoder_poll(fec_go_decoder *d, int wait, uint64_t *block_ids, uint32_t *lens, uint64_t *offsets,
                         uint8_t *out, size_t out_cap, size_t max_blocks, size_t *nblocks);
 

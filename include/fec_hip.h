@@ -91,7 +91,9 @@ int fec_device_count(int *count);
 /* Context: device binding, one HIP stream, cached code matrices, workspace, pinned staging. */
 int fec_ctx_create(int device, fec_ctx **out);
 void fec_ctx_destroy(fec_ctx *ctx);
-/* Run subsequent work on an external hipStream_t (NULL = the device's null stream). */
+/* Run subsequent work on an external hipStream_t (NULL = the device's null stream). Work the
+ * ctx already queued on its previous stream is ordered before the new stream's (an event wait,
+ * no host sync), since both share the ctx's workspace. */
 int fec_ctx_set_stream(fec_ctx *ctx, void *hip_stream);
 /* Go back to the ctx-owned stream. */
 int fec_ctx_reset_stream(fec_ctx *ctx);

@@ -2,6 +2,8 @@
 
   fec_go_harness        the Go binding's C call sequence (tests/test_go_harness.py)
   fec_go_stress         many-block round trips through include/fec_go.h
+  fec_go_threads        encoders / decoders created on one thread, driven concurrently from
+                        others (Go's goroutine-to-thread migration), checked against the oracle
   *_san                 the same two linked against lib0xfec_hip_san.so: the library's host
                         C++ (C-ABI, scheme/batch layers, wire codecs, Go ABI) compiled with
                         AddressSanitizer + UBSan on the host side only (-Xarch_host), kernels
@@ -78,16 +80,23 @@ def build():
     here = os.path.dirname(os.path.abspath(__file__))
     lib = os.path.join(PKG, "lib0xfec_hip.so")
     jobs = []
-    for prog in ("fec_go_harness", "fec_go_stress"):
+    # the thread test checks frames against the CPU oracle (test infrastructure, oracle/_build)
+    oracle_dir = os.path.join(ROOT, "oracle", "_build")
+    if not os.path.exists(os.path.join(oracle_dir, "liboracle.so")):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    extra = {"fec_go_threads": (["-pthread"], ["-L", oracle_dir, "-loracle", "-Wl,-rpath," + oracle_dir],
+                                [os.path.join(oracle_dir, "liboracle.so")])}
+    for prog in ("fec_go_harness", "fec_go_stress", "fec_go_threads"):
         src = os.path.join(here, prog + ".c")
+        cflags, libs, deps = extra.get(prog, ([], [], []))
         exe = os.path.join(BIN, prog)
-        if _stale(exe, [src, lib] + hdrs):
-            jobs.append(["gcc", "-std=c11", "-O1", "-Wall", "-Werror", "-I", INCLUDE, src, "-L", PKG,
-                         "-l0xfec_hip", "-Wl,-rpath," + PKG, "-o", exe])
+        if _stale(exe, [src, lib] + hdrs + deps):
+            jobs.append(["gcc", "-std=c11", "-O1", "-Wall", "-Werror"] + cflags + ["-I", INCLUDE, src, "-L", PKG,
+                         "-l0xfec_hip", "-Wl,-rpath," + PKG] + libs + ["-o", exe])
         exe = os.path.join(BIN, prog + "_san")
-        if _stale(exe, [src, san_lib] + hdrs):
-            jobs.append([CLANG, "-std=c11", "-O1", "-Wall", "-Werror"] + SAN_C +
-                        ["-I", INCLUDE, src, "-L", SAN, "-l0xfec_hip_san", "-Wl,-rpath," + SAN, "-o", exe])
+        if _stale(exe, [src, san_lib] + hdrs + deps):
+            jobs.append([CLANG, "-std=c11", "-O1", "-Wall", "-Werror"] + SAN_C + cflags +
+                        ["-I", INCLUDE, src, "-L", SAN, "-l0xfec_hip_san", "-Wl,-rpath," + SAN] + libs + ["-o", exe])
     gb_src = os.path.join(ROOT, "tools", "go_batch_bench.c")
     gb = os.path.join(BIN, "go_batch_bench")
     if _stale(gb, [gb_src, lib] + hdrs):

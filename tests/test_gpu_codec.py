@@ -498,3 +498,39 @@ def test_rs_host_pipeline_many_chunks_multi_erasure(codec, oracle, fec, k, m, ch
         assert np.array_equal(dmg, full[:, :k])
     finally:
         codec.set_tuning(**old)
+
+
+def test_stream_switch_orders_shared_workspace(fec, torch):
+    """fec_ctx_set_stream between two launches that share the ctx's workspace (the RS(16,24)
+    plan records): the second stream must not rewrite the records while the first stream's
+    rebuild still reads them. Two multi-erasure batches, one per torch stream, launched back to
+    back; both must come back equal to the original data (round trip; the kernels themselves
+    are checked against the oracle above)."""
+    k, m, L, S = 16, 8, 1202, 1216
+    n = k + m
+    c = fec.Codec(0)
+    try:
+        outs = []
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        for i, B in enumerate((1 << 16, 1 << 15)):
+            rng = np.random.default_rng(0x57 + i)
+            sh = torch.zeros((B, n, S), dtype=torch.uint8, device="cuda")
+            sh[:, :k, :L] = torch.from_numpy(rng.integers(0, 256, (B, k, L), dtype=np.uint8)).cuda()
+            c.set_stream(streams[i].cuda_stream)
+            c.rs_encode(k, m, sh, shard_len=L)
+            c.sync()
+            masks = _random_masks(rng, B, k, m, max_loss=m)
+            lost = torch.from_numpy(((masks[:, None] >> np.arange(n)) & 1) == 0).cuda()
+            outs.append((sh.clone(), sh, lost, torch.from_numpy(masks.view(np.int32)).cuda()))
+        for i, (want, sh, lost, dm) in enumerate(outs):
+            sh[lost] = 0x5A
+        torch.cuda.synchronize()
+        for i, (want, sh, lost, dm) in enumerate(outs):   # back to back, no host wait between
+            c.set_stream(streams[i].cuda_stream)
+            c.rs_reconstruct(k, m, sh, dm, shard_len=L)
+        torch.cuda.synchronize()
+        assert c.lib_sync_rc() == 0
+        for want, sh, lost, dm in outs:
+            assert torch.equal(sh[:, :k, :L], want[:, :k, :L])
+    finally:
+        c.close()

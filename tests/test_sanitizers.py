@@ -141,3 +141,25 @@ def test_host_suite_under_asan_ubsan(fec):
                        capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
     assert " passed" in p.stdout and "failed" not in p.stdout
+
+
+def test_threads_program_fails_loudly_without_device(fec):
+    if fec.device_count() > 0:
+        pytest.skip("a GPU is present")
+    p = subprocess.run([binary("fec_go_threads"), "4", "1"], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 1 and "no HIP device" in p.stderr, p.stderr[-2000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("san", [False, True], ids=["plain", "asan_ubsan"])
+def test_go_abi_concurrent_connections(san):
+    """Four encoders + four decoders (RS(8,12) twice, RS(20,30), XOR(2,1)) created on one thread
+    and driven concurrently from four others, then from swapped threads (connection.go:525 run
+    loops; goroutines migrate between OS threads). Each owns its fec_ctx, so no stream, workspace
+    or sticky error is shared; frames are checked against the oracle, payloads against the
+    originals (tests/c/fec_go_threads.c)."""
+    exe = binary("fec_go_threads_san" if san else "fec_go_threads")
+    p = subprocess.run([exe, "120", str(0xC0FFEE)], capture_output=True, text=True, timeout=110,
+                       env=san_env(gpu=True) if san else None)
+    assert p.returncode == 0, p.stderr[-4000:]
+    assert p.stdout.startswith("ok connections=4 blocks=960")
