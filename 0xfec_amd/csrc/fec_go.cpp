@@ -106,7 +106,10 @@ int fec_go_encoder_poll(fec_go_encoder* e, int wait, uint64_t* block_ids, uint32
                         size_t max_blocks, size_t* nblocks) {
     if (nblocks) *nblocks = 0;
     if (!e || (max_blocks && (!block_ids || !repair_len || !repairs))) return FEC_ERR_INVALID_ARG;
-    const fec::Error err = wait ? e->enc->Drain() : e->enc->Poll();
+    fec::Error err = wait ? e->enc->Drain() : e->enc->Poll();
+    // start coding the staged blocks when the device has no batch of this encoder in flight:
+    // a block never waits for a full batch, and batches grow while the previous one is out
+    if (err.ok() && !wait && e->enc->InFlight() == 0 && e->enc->Staged() > 0) err = e->enc->Flush();
     if (!err.ok()) return report(err);
     size_t d = 0;
     fec::BatchEncoder::RawBlock rb;
@@ -192,7 +195,8 @@ int fec_go_decoder_poll(fec_go_decoder* d, int wait, uint64_t* block_ids, uint32
                         uint8_t* out, size_t out_cap, size_t max_blocks, size_t* nblocks) {
     if (nblocks) *nblocks = 0;
     if (!d || (max_blocks && (!block_ids || !lens || !offsets || (out_cap && !out)))) return FEC_ERR_INVALID_ARG;
-    const fec::Error err = wait ? d->dec->Drain() : d->dec->Poll();
+    fec::Error err = wait ? d->dec->Drain() : d->dec->Poll();
+    if (err.ok() && !wait && d->dec->InFlight() == 0 && d->dec->Staged() > 0) err = d->dec->Flush();   // as the encoder
     if (!err.ok()) return report(err);
     // take the queue, hand out what fits from the front, put the rest back in order
     std::vector<fec::RecoveredQueue::Item> all;

@@ -118,16 +118,22 @@ func (s *BatchSender) Submit(b *block) error {
 	return goErr(C.fec_go_encoder_submit(s.e, C.uint64_t(b.id), (**C.uint8_t)(unsafe.Pointer(s.ptrs)), s.lens, C.int(n)))
 }
 
-// Poll hands back the repair frames of finished blocks, in submit order (wait: flush and wait
-// for all). Each payload is a fresh Go slice of cap MaxPacketBufferSize, as reed_solomon.go:44.
-func (s *BatchSender) Poll(wait bool) ([][]*wire.RepairFrame, error) {
+// Poll hands back the repair frames of finished blocks, in submit order, at most maxBlocks
+// blocks (< 0 or more than a batch: one batch's worth; 0: none); the rest stay in the library
+// for a later Poll. wait: flush and wait for every staged block first; otherwise the staged blocks
+// start coding when no batch is in flight. Each payload is a fresh Go slice of cap
+// MaxPacketBufferSize, as reed_solomon.go:44.
+func (s *BatchSender) Poll(wait bool, maxBlocks int) ([][]*wire.RepairFrame, error) {
 	defer lockThread()()
 	w := C.int(0)
 	if wait {
 		w = 1
 	}
+	if maxBlocks < 0 || maxBlocks > len(s.ids) {
+		maxBlocks = len(s.ids)
+	}
 	var nb C.size_t
-	rc := C.fec_go_encoder_poll(s.e, w, &s.ids[0], &s.rlen[0], (*C.uint8_t)(&s.repairs[0]), C.size_t(len(s.ids)), &nb)
+	rc := C.fec_go_encoder_poll(s.e, w, &s.ids[0], &s.rlen[0], (*C.uint8_t)(&s.repairs[0]), C.size_t(maxBlocks), &nb)
 	if err := goErr(rc); err != nil {
 		return nil, err
 	}

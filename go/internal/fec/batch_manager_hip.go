@@ -1,0 +1,223 @@
+//go:build fechip
+
+package fec
+
+import (
+	"github.com/quic-go/quic-go/internal/protocol"
+	"github.com/quic-go/quic-go/internal/wire"
+)
+
+// hipBatchBlocks is the most blocks one kernel launch codes (per staging set of the library).
+const hipBatchBlocks = 1024
+
+// hipCode: the (k, m) the reference's factories use for a scheme (manager.go:54-67, 77-90).
+func hipCode(id protocol.DecoderFECScheme) (k, m int, ok bool) {
+	switch id {
+	case protocol.XORFECScheme:
+		return 2, 1, true
+	case protocol.ReedSolomonFECScheme:
+		return 20, 10, true
+	}
+	return 0, 0, false
+}
+
+// newHIPBlockScheme: the per-block GPU schemes (FEC_HIP=block).
+func newHIPBlockScheme(id protocol.DecoderFECScheme, k, m int) (BlockFECScheme, error) {
+	if id == protocol.XORFECScheme {
+		return newHipXorScheme()
+	}
+	return newHipReedSolomonScheme(k, m)
+}
+
+// newHIPSender is the hook go/patches/manager.go.diff puts at the top of NewSender
+// (manager.go:50): (sender, true, err) when FEC_HIP selects the GPU for scheme id, else
+// (nil, false, nil) and the reference's switch runs. FECDisabled and unknown ids always fall
+// through, so their results and errors stay the reference's.
+func newHIPSender(id protocol.DecoderFECScheme) (Sender, bool, error) {
+	k, m, ok := hipCode(id)
+	if !ok || !useHIP() {
+		return nil, false, nil
+	}
+	if hipMode() == "block" {
+		s, err := newHIPBlockScheme(id, k, m)
+		if err != nil {
+			return nil, true, err
+		}
+		mgr, err := NewManager(s, k, m)
+		if err != nil {
+			return nil, true, err
+		}
+		return mgr, true, nil
+	}
+	bm, err := newBatchManager(id, k, m, true)
+	if err != nil {
+		return nil, true, err
+	}
+	return bm, true, nil
+}
+
+// newHIPReceiver is the same hook for NewReceiver (manager.go:73).
+func newHIPReceiver(id protocol.DecoderFECScheme) (Receiver, bool, error) {
+	k, m, ok := hipCode(id)
+	if !ok || !useHIP() {
+		return nil, false, nil
+	}
+	if hipMode() == "block" {
+		s, err := newHIPBlockScheme(id, k, m)
+		if err != nil {
+			return nil, true, err
+		}
+		mgr, err := NewManager(s, k, m)
+		if err != nil {
+			return nil, true, err
+		}
+		return mgr, true, nil
+	}
+	bm, err := newBatchManager(id, k, m, false)
+	if err != nil {
+		return nil, true, err
+	}
+	return bm, true, nil
+}
+
+// batchManager is manager.go's sender / receiver with its two scheme calls deferred to the GPU
+// batch path: the block bookkeeping is the embedded reference manager's own (blockStatuses,
+// newBlock, addSourceSymbol / addRepairSymbol, isComplete / isRecoverable, NextSSID,
+// HandleSourceSymbolFrame, all unchanged); only `m.scheme.repairSymbols(bS.block)`
+// (manager.go:145) becomes BatchSender.Submit and `m.scheme.recoverSymbolPayloads(bS.block)`
+// (manager.go:182) becomes BatchReceiver.Submit. Results come back through RepairPoller /
+// RecoveredPoller (fec_poll.go), which the packer and connection hooks poll
+// (go/patches/packet_packer.go.diff, connection.go.diff). One per connection, driven by its run
+// loop only (connection.go:525), like the reference manager; it owns its library encoder /
+// decoder, so different connections never share a device context.
+type batchManager struct {
+	*manager
+	tx      *BatchSender
+	rx      *BatchReceiver
+	pending int // receiver: blocks staged whose data has not been handed out yet
+}
+
+var (
+	_ Sender          = &batchManager{}
+	_ Receiver        = &batchManager{}
+	_ RepairPoller    = &batchManager{}
+	_ RecoveredPoller = &batchManager{}
+)
+
+func newBatchManager(id protocol.DecoderFECScheme, k, m int, send bool) (*batchManager, error) {
+	mgr, err := NewManager(nil, k, m) // no scheme: its two calls are the ones replaced below
+	if err != nil {
+		return nil, err
+	}
+	bm := &batchManager{manager: mgr}
+	if send {
+		bm.tx, err = NewBatchSender(id, k, m, hipBatchBlocks)
+	} else {
+		bm.rx, err = NewBatchReceiver(id, k, m, hipBatchBlocks)
+	}
+	if err != nil {
+		return nil, err
+	}
+	return bm, nil
+}
+
+// AddSourceSymbolFrame is manager.go:123-158 with repairSymbols (:145) replaced by a Submit of
+// the complete block; it returns no frames (they come from PollRepairFrames).
+func (m *batchManager) AddSourceSymbolFrame(f *wire.SourceSymbolFrame) ([]*wire.RepairFrame, error) {
+	blockID := m.sidToBlockID(f.SSID)
+	if _, exists := m.blockStatuses[blockID]; !exists {
+		m.blockStatuses[blockID] = blockStatus{
+			block:       newBlock(blockID, m.numTotSourceSymbols, m.numTotRepairSymbols),
+			isProcessed: false}
+	}
+	bS := m.blockStatuses[blockID]
+	if bS.isProcessed {
+		return nil, nil
+	}
+	if err := bS.block.addSourceSymbol(f); err != nil {
+		return nil, err
+	}
+	if bS.block.isComplete() {
+		if err := m.tx.Submit(bS.block); err != nil {
+			return nil, err
+		}
+		// the library copied the payloads: drop the block as manager.go:150-153 does
+		bS.block = nil
+		bS.isProcessed = true
+	}
+	m.blockStatuses[blockID] = bS
+	return nil, nil
+}
+
+// PollRepairFrames hands over the repair frames of finished blocks, whole blocks only, at most
+// maxFrames frames; the rest wait in the library. Also starts coding the staged blocks when no
+// batch is in flight (fec_go_encoder_poll), so a block is never left waiting for a full batch.
+func (m *batchManager) PollRepairFrames(maxFrames int) ([]*wire.RepairFrame, error) {
+	maxBlocks := 0
+	if maxFrames > 0 {
+		maxBlocks = maxFrames / m.tx.m
+	}
+	blocks, err := m.tx.Poll(false, maxBlocks)
+	if err != nil {
+		return nil, err
+	}
+	var out []*wire.RepairFrame
+	for _, fs := range blocks {
+		out = append(out, fs...)
+	}
+	return out, nil
+}
+
+// HandleRepairFrame is manager.go:160-198 with recoverSymbolPayloads (:182) replaced by a
+// Submit of the recoverable block; it returns no data (it comes from PollRecovered). A block
+// that is already complete is the reference's nil, nil: nothing is staged.
+func (m *batchManager) HandleRepairFrame(f *wire.RepairFrame) ([]byte, error) {
+	if _, exists := m.blockStatuses[f.Metadata.BlockID]; !exists {
+		m.blockStatuses[f.Metadata.BlockID] = blockStatus{
+			block:       newBlock(f.Metadata.BlockID, m.numTotSourceSymbols, m.numTotRepairSymbols),
+			isProcessed: false,
+		}
+	}
+	bS := m.blockStatuses[f.Metadata.BlockID]
+	if bS.isProcessed {
+		return nil, nil
+	}
+	if err := bS.block.addRepairSymbol(f); err != nil {
+		return nil, err
+	}
+	if bS.block.isRecoverable() {
+		staged, err := m.rx.Submit(bS.block)
+		if err != nil {
+			return nil, err
+		}
+		if staged {
+			m.pending++
+		}
+		bS.block = nil
+		bS.isProcessed = true
+	}
+	m.blockStatuses[f.Metadata.BlockID] = bS
+	return nil, nil
+}
+
+// PollRecovered hands over the block data of finished recoveries in staging order (wait: every
+// staged block). Also starts decoding the staged blocks when no batch is in flight.
+func (m *batchManager) PollRecovered(wait bool) ([][]byte, error) {
+	var out [][]byte
+	for m.pending > 0 {
+		rec, err := m.rx.Poll(wait)
+		if err != nil {
+			return out, err
+		}
+		for _, r := range rec {
+			out = append(out, r.Payloads)
+		}
+		m.pending -= len(rec)
+		if !wait || len(rec) == 0 {
+			break
+		}
+	}
+	return out, nil
+}
+
+func (m *batchManager) RecoveryPending() bool { return m.pending > 0 }

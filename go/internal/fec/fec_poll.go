@@ -1,0 +1,28 @@
+package fec
+
+import "github.com/quic-go/quic-go/internal/wire"
+
+// The asynchronous faces of Sender and Receiver (manager.go:13-22). No build tag: the packer
+// and connection hooks (go/patches/) type-assert these on every build, and only the GPU batch
+// managers (batch_manager_hip.go, build tag fechip) implement them, so on the default build the
+// assertions fail and the reference's synchronous path runs unchanged.
+
+// RepairPoller is a Sender whose repair frames are produced asynchronously: its
+// AddSourceSymbolFrame stages a block that becomes complete and returns no frames
+// (manager.go:144-154 returns them at once), and the frames of finished blocks come from
+// PollRepairFrames, whole blocks only, in submit order, at most maxFrames frames (the room
+// left in the connection's repair queue, which panics when full: repair_queue.go:46-53).
+type RepairPoller interface {
+	PollRepairFrames(maxFrames int) ([]*wire.RepairFrame, error)
+}
+
+// RecoveredPoller is a Receiver whose recoveries are produced asynchronously: its
+// HandleRepairFrame stages a block that becomes recoverable and returns no data
+// (manager.go:181-193 returns it at once), and the block data of finished blocks
+// (recoverSymbolPayloads' result, reed_solomon.go:128-133) comes from PollRecovered in staging
+// order. wait: start and wait for every staged block. RecoveryPending reports staged blocks
+// whose data has not been handed out yet.
+type RecoveredPoller interface {
+	PollRecovered(wait bool) ([][]byte, error)
+	RecoveryPending() bool
+}

@@ -39,9 +39,24 @@ func hipDevice() int {
 	return 0
 }
 
-// useHIP selects the GPU schemes in NewSender / NewReceiver (manager.go:50-94) when
-// FEC_HIP=1, so the default stays the CPU path.
-func useHIP() bool { return os.Getenv("FEC_HIP") == "1" }
+// hipMode selects the GPU path in NewSender / NewReceiver (manager.go:50-94, through the hooks
+// of go/patches/manager.go.diff):
+//   - FEC_HIP=1 or FEC_HIP=batch: the batched managers (batch_manager_hip.go), the path that pays
+//     off: blocks of a connection are coded many per kernel launch while the run loop carries on;
+//   - FEC_HIP=block: the per-block schemes (reed_solomon_hip.go, xor_hip.go), one synchronous
+//     FEC_HOST round trip per block; for wire-parity checks only, slower than the CPU per block;
+//   - unset: "", the reference's CPU path.
+func hipMode() string {
+	switch os.Getenv("FEC_HIP") {
+	case "1", "batch":
+		return "batch"
+	case "block":
+		return "block"
+	}
+	return ""
+}
+
+func useHIP() bool { return hipMode() != "" }
 
 // hipErr turns a fec_hip.h return code into an error (nil for 0).
 func hipErr(rc C.int) error {

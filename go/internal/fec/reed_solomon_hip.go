@@ -125,6 +125,9 @@ func (s *hipReedSolomonScheme) recoverSymbolPayloads(b *block) ([]byte, error) {
 	}
 	for pid, payload := range b.pidToRepairPayload {
 		i := k + int(pid)
+		if len(payload) == 0 {
+			continue // klauspost treats a zero-length shard as missing (as stageRecoverPayloads does)
+		}
 		if len(payload) != L {
 			return nil, errors.New("shard sizes do not match") // klauspost ErrShardSize
 		}

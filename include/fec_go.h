@@ -67,7 +67,9 @@ int fec_go_encoder_submit(fec_go_encoder *e, uint64_t block_id, const uint8_t *c
 int fec_go_encoder_flush(fec_go_encoder *e);
 /* Completed blocks, in commit order, up to max_blocks: block_ids[d], repair_len[d] (= its
  * biggest + 2), repair payload i of block d at repairs + (d * m + i) * FEC_GO_SLOT. wait != 0:
- * flush and wait for every staged block first. *nblocks = blocks written. */
+ * flush and wait for every staged block first; wait == 0: never blocks, and starts coding the
+ * staged blocks when no batch is in flight (so a block never waits for a full batch).
+ * *nblocks = blocks written; the rest stay for a later poll. */
 int fec_go_encoder_poll(fec_go_encoder *e, int wait, uint64_t *block_ids, uint32_t *repair_len, uint8_t *repairs,
                         size_t max_blocks, size_t *nblocks);
 
@@ -94,6 +96,7 @@ void fec_go_decoder_drop(fec_go_decoder *d, uint64_t block_id);
 int fec_go_decoder_flush(fec_go_decoder *d);
 /* Recovered blocks, in commit order: block_ids[d], its payload (recoverSymbolPayloads' result)
  * at out + offsets[d], lens[d] bytes; stops before max_blocks or when out_cap would overflow.
+ * wait as fec_go_encoder_poll.
  * When the next payload alone is larger than out_cap: FEC_ERR_INVALID_ARG with the needed size
  * in fec_last_error(), nothing is taken (poll again with a larger buffer). */
 int fec_go_decoder_poll(fec_go_decoder *d, int wait, uint64_t *block_ids, uint32_t *lens, uint64_t *offsets,
