@@ -392,6 +392,12 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
     const size_t lds = fk::recon_lds_bytes(G, k, maxe, lay);
     const bool wave = fk::wave_recon_applies(cps, k, maxe, lay.stride);
     const bool fused = wave && fk::g_tune.dec_fused;
+    // two-tier rebuild (fec_decode.hip): waves needing many rows go through the worklist
+    const bool tiered = wave && sorted && !fused && fk::tier_recon_applies(k, maxe, cps);
+    if (tiered) {
+        const int rc = grow_hard(ctx, (per_launch * cps + 63) / 64);
+        if (rc) return rc;
+    }
     for (size_t b0 = 0; b0 < nblocks; b0 += per_launch) {
         const size_t nb = std::min(per_launch, nblocks - b0);
         fk::PlanArgs p{};
@@ -456,6 +462,14 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
             a.m = m;
             a.max_out = p.max_out;
             HIP_TRY(fk::launch_rs_recover_fused(a, ctx->stream));
+            continue;
+        }
+        if (tiered) {
+            a.err = err;
+            a.hard = ctx->work->d_hard;
+            a.hard_cap = (uint32_t)(ctx->work->hard_cap - fk::kHardList);
+            a.list_grid = (uint32_t)ctx->ncu * 4;
+            HIP_TRY(fk::launch_rs_reconstruct_tiered(a, ctx->stream));
             continue;
         }
         if (wave) {
@@ -1045,7 +1059,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 24 ? &fk::g_tune.dec_sorted : key == 25 ? &fk::g_tune.dec_fixk
               : key == 26 ? &fk::g_tune.host_chunk : key == 27 ? &fk::g_tune.dir_wpc
               : key == 28 ? &fk::g_tune.dir_nt : key == 29 ? &fk::g_tune.dec_pseg
-              : key == 30 ? &fk::g_tune.enc_bits : key == 31 ? &fk::g_tune.enc_bwpc : nullptr;
+              : key == 30 ? &fk::g_tune.enc_bits : key == 31 ? &fk::g_tune.enc_bwpc
+              : key == 32 ? &fk::g_tune.dec_tier : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

@@ -361,6 +361,142 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
     }
 }
 
+// ------------------------------------------------------------------ tiered rebuild
+// A wave's registers are sized for the largest row count its kernel can meet (RS(20,30): ten
+// rebuilt rows, 208 VGPRs, 2 waves per SIMD), even when almost every wave rebuilds one or two
+// rows. So the rebuild runs in two launches: tier A carries row bodies 1..RT only (RT = knob
+// dec_tier), with a rolling load window, at more resident waves; a wave whose blocks rebuild
+// more than RT rows goes on the worklist (a.hard, as the direct decode's hard waves) and a
+// persistent tier-B launch with every row body rebuilds those waves. A single-erasure batch
+// never reaches tier B (its grid finds an empty list and exits).
+//
+// One wave's rebuild of the 64 items from i0, plans from the (sorted) plan buffer: stage the
+// blocks' records, expand the PermTabs of the rows they rebuild, one item per lane. RT > 0:
+// waves needing more rows are deferred to the worklist instead.
+template <int MAXE, int POL, int K, int W, int RT>
+__device__ __forceinline__ void tier_wave(const ReconArgs& a, uint8_t* slice, uint32_t i0, uint32_t lane) {
+    constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
+    constexpr uint32_t WB = W > 0 ? 2u : kWaveBlocks;
+    // PermTab rows per block in the slice: tier A never expands more than RT
+    const uint32_t k = K, maxe = RT > 0 ? (uint32_t)RT : a.maxe;
+    const PlanLayout lay = a.lay;
+    gf::PermTab* tabs = reinterpret_cast<gf::PermTab*>(slice);
+    uint8_t* plans = slice + (size_t)WB * maxe * k * sizeof(gf::PermTab);
+    const uint32_t total = a.nblocks * a.cps;
+    const uint32_t bfirst = fdiv(i0, a.div_cps);
+    const uint32_t nb = fdiv(min(i0 + 63u, total - 1u), a.div_cps) - bfirst + 1;   // <= WB
+    {
+        const uint32_t nw = nb * lay.stride / 16;
+        const uint4* src = reinterpret_cast<const uint4*>(a.plans + (uint64_t)bfirst * lay.stride);
+        if (lane < nw) reinterpret_cast<uint4*>(plans)[lane] = src[lane];
+    }
+    wave_sync();
+    const uint32_t n0 = plans[lay.nout_off];
+    const uint32_t n1 = nb > 1 ? plans[lay.stride + lay.nout_off] : 0u;
+    const uint32_t n2 = (WB > 2 && nb > 2) ? plans[2 * lay.stride + lay.nout_off] : 0u;
+    if constexpr (RT > 0) {
+        if (max(n0, max(n1, n2)) > (uint32_t)RT) {   // wave-uniform: the whole wave goes to tier B
+            if (lane == 0) {
+                const uint32_t slot = atomicAdd(a.hard, 1u);
+                if (slot < a.hard_cap) a.hard[kHardList + slot] = i0;
+                else atomicOr(a.err, 4);   // never expected: the list holds one entry per wave
+            }
+            return;
+        }
+    }
+    {
+        // only the rows the blocks rebuild: entry i of c0 + c1 + c2 (c_g = nout_g * k)
+        const uint32_t c0 = n0 * k, c1 = n1 * k, c2 = n2 * k;
+        for (uint32_t i = lane; i < c0 + c1 + c2; i += 64) {
+            const uint32_t g = (i >= c0) + (i >= c0 + c1);
+            const uint32_t rem = i - (g == 0 ? 0u : g == 1 ? c0 : c0 + c1);
+            const uint32_t r = rem / k, j = rem - r * k;
+            const uint8_t* P = plans + g * lay.stride;
+            tabs[g * maxe * k + rem] = gf::make_permtab_fast(P[lay.coef_off + r * k + j]);
+        }
+    }
+    wave_sync();
+    const uint32_t item = i0 + lane;
+    const bool inr = item < total;
+    const uint32_t blk = inr ? fdiv(item, a.div_cps) : bfirst;
+    const uint32_t g = blk - bfirst;
+    const uint32_t c = item - blk * a.cps;
+    const uint8_t* P = plans + g * lay.stride;
+    const uint32_t nout = inr ? P[lay.nout_off] : 0;
+    const uint32_t rows = wave_rows<MAXE>(nout);
+    if (nout == 0) return;
+    const uint32_t rb = a.sorted ? *reinterpret_cast<const uint32_t*>(P + lay.blk_off) : blk;
+    if constexpr (W > 0) recon_item_roll<K, MAXE, W, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
+    else recon_item_k<K, MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
+}
+
+// Tier A: flat grid, one wave per 64 items, row bodies 1..RT.
+template <int RT, int POL, int K, int W>
+__global__ __launch_bounds__(kThreads) void rs_reconstruct_tier_kernel(ReconArgs a) {
+    constexpr uint32_t WB = W > 0 ? 2u : kWaveBlocks;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint8_t* slice = smem + (size_t)wave * wave_slice_bytes(K, RT, a.lay.stride, WB);
+    const uint32_t i0 = xcd_order(a.swz) * kThreads + (wave << 6);
+    if (i0 >= a.nblocks * a.cps) return;
+    tier_wave<RT, POL, K, W, RT>(a, slice, i0, lane);
+}
+
+// Tier B: a persistent grid of waves takes the deferred waves in turn, every row body; with an
+// empty list every wave exits at once. The last workgroup to finish rewinds the list.
+template <int MAXE, int POL, int K, int W>
+__global__ __launch_bounds__(kThreads) void rs_reconstruct_list_kernel(ReconArgs a) {
+    constexpr uint32_t WB = W > 0 ? 2u : kWaveBlocks;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint8_t* slice = smem + (size_t)wave * wave_slice_bytes(K, a.maxe, a.lay.stride, WB);
+    const uint32_t count = min(__hip_atomic_load(a.hard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.hard_cap);
+    const uint32_t nw = gridDim.x * (kThreads / 64);
+    for (uint32_t t = blockIdx.x * (kThreads / 64) + wave; t < count; t += nw) {
+        wave_sync();   // the previous wave's reads of the slice are done
+        tier_wave<MAXE, POL, K, W, 0>(a, slice, a.hard[kHardList + t], lane);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(a.hard + kHardDone, 1u) == gridDim.x - 1) {
+            atomicExch(a.hard, 0u);
+            atomicExch(a.hard + kHardDone, 0u);
+        }
+    }
+}
+
+template <int K, int MAXE, int WA, int WB_, int POL>
+static hipError_t tier_launch(const ReconArgs& a, uint32_t rt, hipStream_t s) {
+    const uint64_t total = (uint64_t)a.nblocks * a.cps;
+    const int grid = (int)((total + kThreads - 1) / kThreads);
+    if (grid == 0) return hipSuccess;
+    const size_t ldsB = 4 * wave_slice_bytes(K, a.maxe, a.lay.stride, WB_ > 0 ? 2 : 3);
+#define FEC_TIER_A(R)                                                                                          \
+    hipLaunchKernelGGL((rs_reconstruct_tier_kernel<R, POL, K, WA>), dim3(grid), dim3(kThreads),                \
+                       occupancy_lds(g_tune.dec_wpc, 4 * wave_slice_bytes(K, R, a.lay.stride, WA > 0 ? 2 : 3)), s, \
+                       a)
+    if (rt <= 1) FEC_TIER_A(1);
+    else if (rt <= 2) FEC_TIER_A(2);
+    else FEC_TIER_A(4);
+#undef FEC_TIER_A
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((rs_reconstruct_list_kernel<MAXE, POL, K, WB_>), dim3(a.list_grid), dim3(kThreads), ldsB, s, a);
+    return hipGetLastError();
+}
+
+bool tier_recon_applies(uint32_t k, uint32_t maxe, uint32_t cps) {
+    return g_tune.dec_tier > 0 && g_tune.dec_fixk && (g_tune.dec_nt & 3) && cps >= 64 &&
+           ((k == 16 && maxe == 8) || (k == 20 && maxe == 10));
+}
+
+hipError_t launch_rs_reconstruct_tiered(const ReconArgs& a, hipStream_t s) {
+    const uint32_t rt = (uint32_t)g_tune.dec_tier;
+    if (a.k == 16) return tier_launch<16, 8, 8, 8, 3>(a, rt, s);
+    return tier_launch<20, 16, 8, 0, 3>(a, rt, s);
+}
+
 hipError_t launch_rs_plan(const PlanArgs& a, hipStream_t s) {
     const int grid = (int)((a.nblocks + kPlanThreads - 1) / kPlanThreads);
     if (grid == 0) return hipSuccess;

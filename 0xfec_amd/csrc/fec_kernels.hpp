@@ -108,6 +108,7 @@ struct ReconArgs {
     const uint32_t* single_coef_host;   // host copy of single_coef (passed as a kernel argument when small)
     uint32_t* hard;            // multi-erasure worklist: [0] count, [kHardDone] done, [kHardList..] wave items
     uint32_t hard_cap;         // entries the worklist holds (a count past it is reported, never written)
+    uint32_t list_grid;        // workgroups of the persistent worklist kernels (tier B)
 };
 
 constexpr uint32_t kHardDone = 32, kHardList = 64;   // worklist words (own 128-byte lines)
@@ -174,6 +175,8 @@ struct Tuning {
                               // (enc_select.py, one box): RS(16,24) 5.35 -> 6.36 TB/s; RS(8,12)
                               // 6.42 vs 6.51 for the dyadic perm body (off); streamed -0.2 % (off)
     int enc_bwpc = 0;         // its residency (workgroups per CU, 0 uncapped)
+    int dec_tier = 0;         // RS(16,24) / RS(20,30) rebuild in two tiers: waves of <= dec_tier rows
+                              // (1, 2 or 4) in a small-register launch, the rest from a worklist (0: off)
 };
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):
@@ -208,6 +211,10 @@ hipError_t launch_rs_plan_sorted(const PlanArgs& a, hipStream_t s);
 hipError_t launch_rs_reconstruct(const ReconArgs& a, int grid, hipStream_t s);
 bool wave_recon_applies(uint32_t cps, uint32_t k, uint32_t maxe, uint32_t stride);
 hipError_t launch_rs_reconstruct_wave(const ReconArgs& a, hipStream_t s);
+// Tiered form of the RS(16,24) / RS(20,30) rebuild (fec_decode.hip): needs a.hard / a.hard_cap /
+// a.err / a.list_grid.
+bool tier_recon_applies(uint32_t k, uint32_t maxe, uint32_t cps);
+hipError_t launch_rs_reconstruct_tiered(const ReconArgs& a, hipStream_t s);
 hipError_t launch_rs_recover_fused(const ReconArgs& a, hipStream_t s);
 // Direct form (fec_recover.hip): applies when the single-erasure tables of (k, m) fit in LDS.
 bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t stride);

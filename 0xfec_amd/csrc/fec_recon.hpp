@@ -139,9 +139,9 @@ __device__ __forceinline__ void recon_item_k(const ReconArgs& a, const uint8_t* 
     static_assert(R <= 10, "row bodies 1..10");
     switch (rows) {   // wave-uniform
         case 1: recon_rows_k<K, 1, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
-        case 2: recon_rows_k<K, 2, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
-        case 3: recon_rows_k<K, 3, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
-        case 4: recon_rows_k<K, 4, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 2: if constexpr (R >= 2) recon_rows_k<K, 2, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 3: if constexpr (R >= 3) recon_rows_k<K, 3, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 4: if constexpr (R >= 4) recon_rows_k<K, 4, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
         case 5: if constexpr (R >= 5) recon_rows_k<K, 5, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
         case 6: if constexpr (R >= 6) recon_rows_k<K, 6, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
         case 7: if constexpr (R >= 7) recon_rows_k<K, 7, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
@@ -213,9 +213,9 @@ __device__ __forceinline__ void recon_item_roll(const ReconArgs& a, const uint8_
 #define FEC_ROLL_ROWS(N) recon_rows_roll<K, N, W, NTL, NTS>(a, P, T, dblk, pbase, oblk, c, nout)
     switch (rows) {   // wave-uniform
         case 1: FEC_ROLL_ROWS(1); break;
-        case 2: FEC_ROLL_ROWS(2); break;
-        case 3: FEC_ROLL_ROWS(3); break;
-        case 4: FEC_ROLL_ROWS(4); break;
+        case 2: if constexpr (R >= 2) FEC_ROLL_ROWS(2); break;
+        case 3: if constexpr (R >= 3) FEC_ROLL_ROWS(3); break;
+        case 4: if constexpr (R >= 4) FEC_ROLL_ROWS(4); break;
         case 5: if constexpr (R >= 5) FEC_ROLL_ROWS(5); break;
         case 6: if constexpr (R >= 6) FEC_ROLL_ROWS(6); break;
         case 7: if constexpr (R >= 7) FEC_ROLL_ROWS(7); break;

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=1 << 20)
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--tiers", action="store_true", help="A/B the two-tier rebuild (knob dec_tier) only")
     ap.add_argument("--multi", type=int, default=0,
                     help="e ~ U{1..multi} erasures uniform over all n shards (config_bench's RS(16,24) mix)")
     args = ap.parse_args()
@@ -50,7 +51,7 @@ def main():
     dp, pp, op = data.data_ptr(), par.data_ptr(), out.data_ptr()
     # every knob any variant sets, at its default: tune(D) must undo each variant completely
     D = dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=1, dec_ipl=0, dec_direct=1, dec_nt=3, dir_wpc=-1, dir_nt=-1,
-             dec_fixk=2, dec_sorted=1, dec_pseg=0)
+             dec_fixk=2, dec_sorted=1, dec_pseg=0, dec_tier=0)
     variants = {"direct (default)": D,
                 "direct, PermTab rows by vector load": dict(D, dec_direct=2),
                 "direct noswz": dict(D, dec_swz=0),
@@ -72,6 +73,11 @@ def main():
         for ps in (1, 2, 4, 8, 16):
             variants["plan segs %d" % ps] = dict(D, dec_pseg=ps)
         variants["default + status array"] = dict(D, _status=1)
+    if args.tiers:
+        variants = {"default": D}
+        for rt in (1, 2, 4):
+            variants["tier %d" % rt] = dict(D, dec_tier=rt)
+            variants["tier %d wpc4" % rt] = dict(D, dec_tier=rt, dec_wpc=4)
     base = codec.set_tuning(**D)
     use_status = [False]
 
