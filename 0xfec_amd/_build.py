@@ -26,6 +26,18 @@ CFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall",
           "-mllvm", "-amdgpu-atomic-optimizer-strategy=None", "-I", INCLUDE]
 
 
+def source_hash(tu):
+    """sha256 (first 16 hex digits) over what the kernels of translation unit `tu` are compiled
+    from: its source, the device headers and the compile flags. A PMC traffic profile records it
+    (tools/pmc_traffic.py) and bench.py reports the profile's traffic only while it still matches."""
+    import hashlib
+    h = hashlib.sha256(" ".join(CFLAGS[:-2]).encode())
+    for f in [os.path.join(CSRC, tu)] + [os.path.join(CSRC, x) for x in HEADERS]:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def _hipcc():
     for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
         if c and (os.path.sep not in c or os.path.exists(c)):

@@ -172,7 +172,25 @@ static int get_code(fec_ctx* ctx, int k, int m, Code** out) {
         // single-erasure plans: data shard E0 lost, parity R0 the first present one; inputs are
         // the other data shards in order, then parity R0 (the first k present shards):
         // x_E0 = inv(A[R0][E0]) * (p_R0 ^ sum_{j != E0} A[R0][j] x_j)   (reed_solomon.go:124)
+        if (k + m <= FEC_MAX_DECODE_SHARDS) {
+            // the coefficient bytes of every single-erasure plan (small for every decodable code:
+            // RS(20,30) 4 KB): the direct decode reads a wave's rows by scalar loads
+            const size_t kw = ((size_t)k + 3) / 4;
+            std::vector<uint32_t> sc((size_t)k * m * kw, 0);
+            for (int e0 = 0; e0 < k; ++e0)
+                for (int r0 = 0; r0 < m; ++r0) {
+                    const uint8_t* row = c.matrix.data() + (size_t)(k + r0) * k;
+                    const uint8_t inv = gf::inv(row[e0]);
+                    uint8_t* dst = reinterpret_cast<uint8_t*>(&sc[((size_t)e0 * m + r0) * kw]);
+                    for (int j = 0, pos = 0; j <= k; ++j)
+                        if (j != e0) dst[pos++] = j < k ? gf::mul(inv, row[j]) : inv;
+                }
+            c.single_coef = sc;
+            HIP_TRY(hipMalloc(&c.d_single_coef, sc.size() * 4));
+            HIP_TRY(hipMemcpy(c.d_single_coef, sc.data(), sc.size() * 4, hipMemcpyHostToDevice));
+        }
         if (k + m <= FEC_MAX_DECODE_SHARDS && fk::direct_table_words((uint32_t)k, (uint32_t)m) * 4 <= 16 * 1024) {
+            // the same plans expanded to PermTabs (k*m*k*32 bytes; small codes only)
             std::vector<uint32_t> st(fk::direct_table_words((uint32_t)k, (uint32_t)m), 0);
             for (int e0 = 0; e0 < k; ++e0)
                 for (int r0 = 0; r0 < m; ++r0) {
@@ -188,19 +206,6 @@ static int get_code(fec_ctx* ctx, int k, int m, Code** out) {
                 }
             HIP_TRY(hipMalloc(&c.d_single, st.size() * 4));
             HIP_TRY(hipMemcpy(c.d_single, st.data(), st.size() * 4, hipMemcpyHostToDevice));
-            const size_t kw = ((size_t)k + 3) / 4;
-            std::vector<uint32_t> sc((size_t)k * m * kw, 0);
-            for (int e0 = 0; e0 < k; ++e0)
-                for (int r0 = 0; r0 < m; ++r0) {
-                    const uint8_t* row = c.matrix.data() + (size_t)(k + r0) * k;
-                    const uint8_t inv = gf::inv(row[e0]);
-                    uint8_t* dst = reinterpret_cast<uint8_t*>(&sc[((size_t)e0 * m + r0) * kw]);
-                    for (int j = 0, pos = 0; j <= k; ++j)
-                        if (j != e0) dst[pos++] = j < k ? gf::mul(inv, row[j]) : inv;
-                }
-            c.single_coef = sc;
-            HIP_TRY(hipMalloc(&c.d_single_coef, sc.size() * 4));
-            HIP_TRY(hipMemcpy(c.d_single_coef, sc.data(), sc.size() * 4, hipMemcpyHostToDevice));
         }
         if (k + m <= FEC_MAX_DECODE_SHARDS) {
             uint8_t dall[FEC_MAX_DECODE_SHARDS] = {};
@@ -377,7 +382,7 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
     const fk::PlanLayout lay0 = fk::plan_layout(k, maxe);
     // direct form: no plan kernel (single-erasure tables of the code; multi-erasure waves plan
     // in-wave), fec_recover.hip
-    const bool direct = code->d_single && fk::direct_recon_applies(k, m, cps, lay0.stride);
+    const bool direct = code->d_single_coef && fk::direct_recon_applies(k, m, cps, lay0.stride);
     // sorted parallel plans for the plan + wave path (fec_plan.hip)
     const bool sorted = !direct && fk::g_tune.dec_sorted && !fk::g_tune.dec_fused && !fk::g_tune.dec_diag &&
                         fk::wave_recon_applies(cps, k, maxe, fk::plan_layout(k, maxe, true).stride);
@@ -1060,7 +1065,7 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 26 ? &fk::g_tune.host_chunk : key == 27 ? &fk::g_tune.dir_wpc
               : key == 28 ? &fk::g_tune.dir_nt : key == 29 ? &fk::g_tune.dec_pseg
               : key == 30 ? &fk::g_tune.enc_bits : key == 31 ? &fk::g_tune.enc_bwpc
-              : key == 32 ? &fk::g_tune.dec_tier : nullptr;
+              : key == 32 ? &fk::g_tune.dec_tier : key == 33 ? &fk::g_tune.dec_direct20 : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

@@ -175,6 +175,8 @@ struct Tuning {
                               // (enc_select.py, one box): RS(16,24) 5.35 -> 6.36 TB/s; RS(8,12)
                               // 6.42 vs 6.51 for the dyadic perm body (off); streamed -0.2 % (off)
     int enc_bwpc = 0;         // its residency (workgroups per CU, 0 uncapped)
+    int dec_direct20 = 0;     // direct single-erasure decode for RS(20,30) too (rows by scalar loads from
+                              // the device coefficient table; multi-erasure waves to the worklist)
     int dec_tier = 0;         // RS(16,24) / RS(20,30) rebuild in two tiers: waves of <= dec_tier rows
                               // (1, 2 or 4) in a small-register launch, the rest from a worklist (0: off)
 };

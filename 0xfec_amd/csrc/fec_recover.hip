@@ -53,7 +53,10 @@ struct CoefWords {
 // K: compile-time data shard count (0: runtime a.k). TAB: how a wave gets the PermTabs of its
 // blocks' rows: 0 copies them from the code's PermTab table (one vector load per wave, L1/L2
 // hits); 1 reads the rows' coefficient bytes from the kernel arguments (scalar loads, off the
-// vector memory path) and expands them on the lanes (gf::make_permtab).
+// vector memory path) and expands them on the lanes (gf::make_permtab); 2 as 1 with the bytes
+// read from the code's coefficient table in device memory (a.single_coef, through the constant
+// address space: scalar loads), for codes whose rows do not fit the argument (RS(20,30): 1000
+// dwords).
 template <int K, int POL, int TAB>
 __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a, CoefWords cwords) {
     constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
@@ -146,8 +149,10 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
     // lane l < nb*k expands coefficient j = l % k of block g = l / k into wt[l]
     constexpr uint32_t KW = K > 0 ? (K + 3) / 4 : 8;   // coefficient dwords per row (k <= 32)
     uint32_t cw[kWaveBlocks][KW];
-    if constexpr (TAB == 1) {
-        const uint32_t* ct = cwords.w;   // a kernel argument: read with scalar loads
+    if constexpr (TAB >= 1) {
+        // a kernel argument, or device memory read as constant: scalar loads either way
+        typedef __attribute__((address_space(4))) const uint32_t ConstU32;
+        ConstU32* ct = TAB == 1 ? (ConstU32*)cwords.w : (ConstU32*)a.single_coef;
         const uint32_t kw = (k + 3) / 4;
 #pragma unroll
         for (uint32_t g = 0; g < kWaveBlocks; ++g)
@@ -191,7 +196,7 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
         // unconditional loads (a lane with nothing to rebuild reads one L2-resident table line
         // instead): no branch around them, so the row pieces' LDS writes wait for the row loads
         // only (vmcnt counts in order), not for the data
-        const uint8_t* idle = reinterpret_cast<const uint8_t*>(a.single);
+        const uint8_t* idle = reinterpret_cast<const uint8_t*>(TAB == 2 ? a.single_coef : a.single);
         const uint64_t ss = work ? a.ss : 0;
         const uint8_t* d0 = work ? dblk : idle;
         const uint8_t* p0 = work ? par : idle;
@@ -311,9 +316,11 @@ size_t direct_table_words(uint32_t k, uint32_t m) { return (size_t)k * m * k * 8
 
 bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t stride) {
     if (!g_tune.dec_direct || m == 0 || k + m > 32 || cps < 32) return false;
-    if ((size_t)k * m * k * sizeof(gf::PermTab) > kDirectTableBytes) return false;
+    // small codes (their PermTab table fits), or RS(20,30) with its rows read from device memory
+    const bool small = (size_t)k * m * k * sizeof(gf::PermTab) <= kDirectTableBytes;
+    if (!small && !(k == 20 && m == 10 && g_tune.dec_direct20)) return false;
     const uint32_t maxe = std::max<uint32_t>(1, std::min(k, m));
-    return 4 * hard_wave_bytes(m, k, maxe, stride) <= 64 * 1024;
+    return 4 * hard_wave_bytes(m, k, maxe, stride) <= g_max_lds;
 }
 
 template <int K, int POL, int TAB>
@@ -342,7 +349,9 @@ static hipError_t direct_dispatch(const ReconArgs& a, int ncu, hipStream_t s) {
     const size_t kw = (a.k + 3) / 4, words = (size_t)a.k * a.m * kw;
     const bool by_arg = g_tune.dec_direct != 2 && a.single_coef_host && words <= kCoefWords;
     if (by_arg) memcpy(cw.w, a.single_coef_host, words * 4);
-    if (!by_arg)
+    if (a.k == 20)   // RS(20,30): rows from the device coefficient table
+        e = direct_launch<20, POL, 2>(a, cw, s);
+    else if (!by_arg)
         e = a.k == 2 ? direct_launch<2, POL, 0>(a, cw, s) : a.k == 8 ? direct_launch<8, POL, 0>(a, cw, s)
                                                                      : direct_launch<0, POL, 0>(a, cw, s);
     else

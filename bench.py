@@ -38,8 +38,9 @@ SHARD_LEN = PAYLOAD + 2          # + big-endian uint16 length trailer
 SHARD_STRIDE = 1216              # 16-byte aligned device slot per shard
 HBM_PEAK = 8.0e12                # MI355X HBM3E spec, bytes/s (MI355X_MICROARCH.md)
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of this bench (separate passes, tools/pmc_traffic.py,
-# gfx950 FETCH_SIZE x2 correction): HBM bytes per launch of each codec kernel
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02", "pmc_traffic_r02h.json")
+# gfx950 FETCH_SIZE x2 correction): HBM bytes per launch of each codec kernel, with the source
+# hash of the kernel's translation unit at profiling time (tools/gpu_round.sh refreshes it)
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
 
 
 def encode_kernel_name(k, m):
@@ -50,17 +51,30 @@ def encode_kernel_name(k, m):
     return "rs_encode_kernel<"
 
 
-def committed_traffic(kernel_prefix):
-    """HBM bytes per launch of the kernel from the committed PMC profile, or None."""
+def committed_traffic(kernel_prefix, tu):
+    """HBM bytes per launch of the kernel from the committed PMC profile, or None when there is
+    none or when the profile was taken from other kernel sources than the ones built now (its
+    recorded source hash differs: the number would describe a different kernel)."""
+    sys.path.insert(0, os.path.join(ROOT, "0xfec_amd"))
+    try:
+        import _build
+        now = _build.source_hash(tu)
+    finally:
+        sys.path.pop(0)
     try:
         with open(TRAFFIC_JSON) as fh:
             prof = json.load(fh)
     except (OSError, ValueError):
-        return None, None
+        return None, {"source": None, "note": "no PMC profile committed"}
     for name, rec in prof.items():
         if kernel_prefix in name and rec.get("traffic_bytes"):
-            return rec["traffic_bytes"], os.path.relpath(TRAFFIC_JSON, ROOT)
-    return None, None
+            info = {"source": os.path.relpath(TRAFFIC_JSON, ROOT), "profile_source_hash": rec.get("source_hash"),
+                    "built_source_hash": now}
+            if rec.get("source_hash") != now:
+                info["note"] = "stale: the kernel's sources changed since this profile; traffic not reported"
+                return None, info
+            return rec["traffic_bytes"], info
+    return None, {"source": os.path.relpath(TRAFFIC_JSON, ROOT), "note": "kernel not in the profile"}
 
 
 def parse():
@@ -409,10 +423,10 @@ def main():
     enc_kernel = encode_kernel_name(k, m)
     if enc_ms >= dec_ms:
         dominant, dom_bw, dom_bytes = enc_kernel + ">", enc_bw, enc_bytes
-        traffic, traffic_src = committed_traffic(enc_kernel)
+        traffic, traffic_src = committed_traffic(enc_kernel, "fec_encode.hip")
     else:
         dominant, dom_bw, dom_bytes = "rs_recover_direct_kernel<%d" % k, dec_bw, dec_bytes
-        traffic, traffic_src = committed_traffic("rs_recover_direct_kernel")
+        traffic, traffic_src = committed_traffic("rs_recover_direct_kernel", "fec_recover.hip")
 
     if rank == 0:
         out = {
@@ -439,7 +453,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(dom_bw / 1e9, 1), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(dom_bw / HBM_PEAK, 4),
                          "traffic": None if traffic is None else round(traffic / 1e9, 3),
-                         "traffic_unit": "GB per launch", "traffic_source": traffic_src,
+                         "traffic_unit": "GB per launch", "traffic_profile": traffic_src,
                          "kernel": dominant, "algorithmic_bytes_per_launch": dom_bytes},
             "kernels": {
                 # read_frac: the HBM-read roofline of SURVEY.md 8(d) (reads alone: k shards per block)

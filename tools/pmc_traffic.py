@@ -6,6 +6,9 @@ request of a wide coalesced streaming read, i.e. half the bytes; so read bytes =
 2 * FETCH_SIZE * 1024. WRITE_SIZE (KiB) is exact for 16-B-per-lane streaming stores.
 
 usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON
+
+Each kernel's record carries the source hash of its translation unit (0xfec_amd/_build.py
+source_hash), so bench.py can tell whether the profile still describes the kernel it runs.
 """
 import csv
 import glob
@@ -45,6 +48,10 @@ def main():
     fdir, wdir, dst = sys.argv[1:4]
     fetch, nf, grid = per_kernel(fdir, "FETCH_SIZE")
     write, nw, _ = per_kernel(wdir, "WRITE_SIZE")
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "0xfec_amd"))
+    import _build
+    tu_of = {"rs_encode": "fec_encode.hip", "rs_recover": "fec_recover.hip", "rs_reconstruct": "fec_decode.hip",
+             "rs_plan": "fec_plan.hip", "xor_": "fec_xor.hip"}
     res = {}
     for k in sorted(set(fetch) | set(write)):
         if not k.startswith("void fk::"):
@@ -58,6 +65,9 @@ def main():
             "write_bytes": None if w_kb is None else w_kb * 1024,
             "traffic_bytes": None if (f_kb is None or w_kb is None) else 2 * f_kb * 1024 + w_kb * 1024,
         }
+        tu = next((v for pre, v in tu_of.items() if k.startswith("void fk::" + pre)), None)
+        if tu:
+            res[k]["source_hash"] = _build.source_hash(tu)
     with open(dst, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))
