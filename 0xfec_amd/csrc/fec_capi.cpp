@@ -83,8 +83,9 @@ struct Work {
     uint32_t* d_hard = nullptr;   // fk::kHardList + waves words; count and done rewound by the kernel
     size_t hard_cap = 0;
     uint32_t* d_ctr = nullptr;    // fk::kCtrWords ticket counters, self-rewinding
+    uint32_t* d_gate = nullptr;   // fk::kGateWords: the decode path rs_classify_kernel picked, its counters
     void release() {
-        for (void* q : {(void*)d_plans, (void*)d_hard, (void*)d_ctr})
+        for (void* q : {(void*)d_plans, (void*)d_hard, (void*)d_ctr, (void*)d_gate})
             if (q) (void)hipFree(q);
         *this = Work{};
     }
@@ -276,6 +277,16 @@ static int ensure_ctr(fec_ctx* ctx) {
     return FEC_OK;
 }
 
+// The classify kernel's gate words of the current stream's workspace (zeroed once; the kernel
+// rewinds its counters).
+static int ensure_gate(fec_ctx* ctx) {
+    Work& w = *ctx->work;
+    if (w.d_gate) return FEC_OK;
+    HIP_TRY(hipMalloc(&w.d_gate, fk::kGateWords * sizeof(uint32_t)));
+    HIP_TRY(hipMemsetAsync(w.d_gate, 0, fk::kGateWords * sizeof(uint32_t), ctx->stream));
+    return FEC_OK;
+}
+
 static int grow_stage(fec_ctx* ctx, size_t bytes) {
     if (bytes <= ctx->stage_cap) return FEC_OK;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -383,14 +394,22 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
     // direct form: no plan kernel (single-erasure tables of the code; multi-erasure waves plan
     // in-wave), fec_recover.hip
     const bool direct = code->d_single_coef && fk::direct_recon_applies(k, m, cps, lay0.stride);
+    const bool sorted_ok = fk::g_tune.dec_sorted && !fk::g_tune.dec_fused && !fk::g_tune.dec_diag &&
+                           fk::wave_recon_applies(cps, k, maxe, fk::plan_layout(k, maxe, true).stride);
+    // both, gated on the device (RS(16,24), RS(20,30): their worklist path is slow, so a batch with
+    // more than dec_gate_pm per mille of multi-erasure blocks takes the plan path instead)
+    const bool gated = direct && sorted_ok && fk::g_tune.dec_gate &&
+                       (size_t)k * m * k * sizeof(gf::PermTab) > 16 * 1024;
     // sorted parallel plans for the plan + wave path (fec_plan.hip)
-    const bool sorted = !direct && fk::g_tune.dec_sorted && !fk::g_tune.dec_fused && !fk::g_tune.dec_diag &&
-                        fk::wave_recon_applies(cps, k, maxe, fk::plan_layout(k, maxe, true).stride);
+    const bool sorted = (gated || !direct) && sorted_ok;
     const fk::PlanLayout lay = sorted ? fk::plan_layout(k, maxe, true) : lay0;
-    size_t per_launch = std::min<size_t>(direct ? nblocks : kPlanBytes / lay.stride, (size_t)(kMaxItems / cps));
+    size_t per_launch =
+        std::min<size_t>(direct && !gated ? nblocks : kPlanBytes / lay.stride, (size_t)(kMaxItems / cps));
     per_launch = std::max<size_t>(1, std::min(per_launch, nblocks));
     {
-        int rc = direct ? grow_hard(ctx, (per_launch * cps + 63) / 64) : grow_plans(ctx, per_launch * lay.stride);
+        int rc = direct ? grow_hard(ctx, (per_launch * cps + 63) / 64) : FEC_OK;
+        if (!rc && (!direct || gated)) rc = grow_plans(ctx, per_launch * lay.stride);
+        if (!rc && gated) rc = ensure_gate(ctx);
         if (rc) return rc;
     }
     const uint32_t G = fk::pick_tile_blocks(cps, k, maxe, lay);
@@ -418,6 +437,12 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         p.lay = lay;
         p.max_out = out ? out_slots : 0;
         p.dall = code->d_dall;
+        if (gated) {
+            HIP_TRY(fk::launch_rs_classify(p.masks, (uint32_t)nb, k, m, p.max_out, ctx->work->d_gate,
+                                           (uint32_t)fk::g_tune.dec_gate_pm, ctx->ncu, ctx->stream));
+            p.gate = ctx->work->d_gate;
+            p.gate_want = 2;
+        }
         if (sorted) HIP_TRY(fk::launch_rs_plan_sorted(p, ctx->stream));
         else if (!fused && !direct) HIP_TRY(fk::launch_rs_plan(p, ctx->stream));
         fk::ReconArgs a{};
@@ -456,8 +481,11 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
             a.single_coef_host = code->single_coef.data();
             a.hard = ctx->work->d_hard;
             a.hard_cap = (uint32_t)(ctx->work->hard_cap - fk::kHardList);
+            a.gate = gated ? ctx->work->d_gate : nullptr;
+            a.gate_want = 1;
             HIP_TRY(fk::launch_rs_recover_direct(a, ctx->ncu, ctx->stream));
-            continue;
+            if (!gated) continue;
+            a.gate_want = 2;   // and the plan path, which runs only if the classify kernel picked it
         }
         if (fused) {
             a.masks = p.masks;
@@ -1065,7 +1093,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 26 ? &fk::g_tune.host_chunk : key == 27 ? &fk::g_tune.dir_wpc
               : key == 28 ? &fk::g_tune.dir_nt : key == 29 ? &fk::g_tune.dec_pseg
               : key == 30 ? &fk::g_tune.enc_bits : key == 31 ? &fk::g_tune.enc_bwpc
-              : key == 32 ? &fk::g_tune.dec_tier : key == 33 ? &fk::g_tune.dec_direct20 : nullptr;
+              : key == 32 ? &fk::g_tune.dec_tier : key == 33 ? &fk::g_tune.dec_direct_big
+              : key == 34 ? &fk::g_tune.dec_gate : key == 35 ? &fk::g_tune.dec_gate_pm : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

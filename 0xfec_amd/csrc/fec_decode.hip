@@ -262,6 +262,7 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
     // 64 consecutive items span at most 2 blocks (smaller slices: more workgroups per CU)
     constexpr uint32_t WB = W > 0 ? 2u : kWaveBlocks;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (a.gate && *a.gate != a.gate_want) return;   // the classify kernel picked the direct path
     const uint32_t k = a.k, maxe = a.maxe;
     const PlanLayout lay = a.lay;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -435,6 +436,7 @@ template <int RT, int POL, int K, int W>
 __global__ __launch_bounds__(kThreads) void rs_reconstruct_tier_kernel(ReconArgs a) {
     constexpr uint32_t WB = W > 0 ? 2u : kWaveBlocks;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (a.gate && *a.gate != a.gate_want) return;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint8_t* slice = smem + (size_t)wave * wave_slice_bytes(K, RT, a.lay.stride, WB);
     const uint32_t i0 = xcd_order(a.swz) * kThreads + (wave << 6);
@@ -482,7 +484,9 @@ static hipError_t tier_launch(const ReconArgs& a, uint32_t rt, hipStream_t s) {
 #undef FEC_TIER_A
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((rs_reconstruct_list_kernel<MAXE, POL, K, WB_>), dim3(a.list_grid), dim3(kThreads), ldsB, s, a);
+    const void* fb = (const void*)rs_reconstruct_list_kernel<MAXE, POL, K, WB_>;
+    const int gridB = std::max<int>(1, (int)a.list_grid / 4) * resident_per_cu(fb, ldsB);   // list_grid: 4 x CUs
+    hipLaunchKernelGGL((rs_reconstruct_list_kernel<MAXE, POL, K, WB_>), dim3(gridB), dim3(kThreads), ldsB, s, a);
     return hipGetLastError();
 }
 

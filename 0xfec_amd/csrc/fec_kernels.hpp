@@ -66,6 +66,8 @@ struct PlanArgs {
     PlanLayout lay;
     uint32_t max_out;          // recover: output slots per block (0: in place, unlimited)
     const uint8_t* dall;       // sorted plans: per shard index s < n, sum_{t < n, t != s} log(s ^ t) mod 255
+    const uint32_t* gate;      // nullable: run only when gate[0] == gate_want
+    uint32_t gate_want;
 };
 
 // Sorted plans (fec_plan.hip): lanes per block and blocks per 256-thread workgroup for k.
@@ -109,6 +111,8 @@ struct ReconArgs {
     uint32_t* hard;            // multi-erasure worklist: [0] count, [kHardDone] done, [kHardList..] wave items
     uint32_t hard_cap;         // entries the worklist holds (a count past it is reported, never written)
     uint32_t list_grid;        // workgroups of the persistent worklist kernels (tier B)
+    const uint32_t* gate;      // nullable: run only when gate[0] == gate_want (rs_classify_kernel's pick)
+    uint32_t gate_want;
 };
 
 constexpr uint32_t kHardDone = 32, kHardList = 64;   // worklist words (own 128-byte lines)
@@ -175,14 +179,22 @@ struct Tuning {
                               // (enc_select.py, one box): RS(16,24) 5.35 -> 6.36 TB/s; RS(8,12)
                               // 6.42 vs 6.51 for the dyadic perm body (off); streamed -0.2 % (off)
     int enc_bwpc = 0;         // its residency (workgroups per CU, 0 uncapped)
-    int dec_direct20 = 0;     // direct single-erasure decode for RS(20,30) too (rows by scalar loads from
-                              // the device coefficient table; multi-erasure waves to the worklist)
+    int dec_direct_big = 0;   // direct single-erasure decode for RS(16,24) and RS(20,30) too (rows by scalar
+                              // loads from the device coefficient table; multi-erasure waves to the worklist)
+    int dec_gate = 0;         // with dec_direct_big: a classify kernel picks, on the device, per batch, the
+                              // direct path (few multi-erasure blocks) or the plan + rebuild path; the
+                              // other path's kernels exit at once
+    int dec_gate_pm = 10;     // multi-erasure blocks (per mille) above which the plan path is taken
     int dec_tier = 0;         // RS(16,24) / RS(20,30) rebuild in two tiers: waves of <= dec_tier rows
                               // (1, 2 or 4) in a small-register launch, the rest from a worklist (0: off)
 };
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):
 // halfway between 160K/(wpc+1) and 160K/wpc, never below what the kernel itself needs.
+// Workgroups of `kernel` (kThreads each, `lds` dynamic LDS) resident on one CU at once, by the
+// runtime's occupancy calculator; cached per (kernel, lds). At least 1.
+int resident_per_cu(const void* kernel, size_t lds);
+
 inline size_t occupancy_lds(int wpc, size_t own) {
     if (wpc <= 0) return own;
     const size_t cu = 160u * 1024u;
@@ -222,6 +234,12 @@ hipError_t launch_rs_recover_fused(const ReconArgs& a, hipStream_t s);
 bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t stride);
 size_t direct_table_words(uint32_t k, uint32_t m);
 hipError_t launch_rs_recover_direct(const ReconArgs& a, int ncu, hipStream_t s);
+// Pick the decode path of a batch on the device (fec_recover.hip): gate[0] = 1 (direct: at most
+// thr_pm per mille of the blocks rebuild two or more data shards) or 2 (plan + rebuild). gate:
+// kGateWords zeroed words; the kernel rewinds its counters.
+constexpr uint32_t kGateCount = 32, kGateDone = 64, kGateWords = 96;
+hipError_t launch_rs_classify(const uint32_t* masks, uint32_t nblocks, uint32_t k, uint32_t m, uint32_t max_out,
+                              uint32_t* gate, uint32_t thr_pm, int ncu, hipStream_t s);
 hipError_t launch_xor_encode(const XorArgs& a, int grid, hipStream_t s);
 hipError_t launch_xor_reconstruct(const XorArgs& a, int grid, hipStream_t s);
 

@@ -41,6 +41,7 @@ template <uint32_t LPB>
 __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanArgs a, uint32_t segs) {
     constexpr uint32_t G = kPlanSortThreads / LPB;   // blocks per workgroup segment
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (a.gate && *a.gate != a.gate_want) return;   // the classify kernel picked the direct path
     const PlanLayout lay = a.lay;
     const SortLds L = sort_lds(a.m, a.k, G, lay.stride);
     uint8_t* s_exp = smem;

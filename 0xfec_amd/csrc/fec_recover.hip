@@ -61,6 +61,7 @@ template <int K, int POL, int TAB>
 __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a, CoefWords cwords) {
     constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (a.gate && *a.gate != a.gate_want) return;   // the classify kernel picked the plan path
     const uint32_t k = K ? (uint32_t)K : a.k, m = a.m;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint8_t* slice = smem + (size_t)wave * direct_wave_bytes(k);
@@ -318,7 +319,7 @@ bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t stride)
     if (!g_tune.dec_direct || m == 0 || k + m > 32 || cps < 32) return false;
     // small codes (their PermTab table fits), or RS(20,30) with its rows read from device memory
     const bool small = (size_t)k * m * k * sizeof(gf::PermTab) <= kDirectTableBytes;
-    if (!small && !(k == 20 && m == 10 && g_tune.dec_direct20)) return false;
+    if (!small && !(((k == 20 && m == 10) || (k == 16 && m == 8)) && g_tune.dec_direct_big)) return false;
     const uint32_t maxe = std::max<uint32_t>(1, std::min(k, m));
     return 4 * hard_wave_bytes(m, k, maxe, stride) <= g_max_lds;
 }
@@ -337,7 +338,10 @@ static hipError_t direct_launch(const ReconArgs& a, const CoefWords& cw, hipStre
 template <int MAXE, int POL>
 static hipError_t hard_launch(const ReconArgs& a, int ncu, hipStream_t s) {
     const size_t lds = 4 * hard_wave_bytes(a.m, a.k, a.maxe, a.lay.stride);
-    hipLaunchKernelGGL((rs_recover_hard_kernel<MAXE, POL>), dim3(ncu * 4), dim3(kThreads), lds, s, a);
+    // a persistent grid of exactly the workgroups that are resident at once: more would wait
+    // for a second round behind the first
+    const int grid = ncu * resident_per_cu((const void*)rs_recover_hard_kernel<MAXE, POL>, lds);
+    hipLaunchKernelGGL((rs_recover_hard_kernel<MAXE, POL>), dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 
@@ -349,8 +353,10 @@ static hipError_t direct_dispatch(const ReconArgs& a, int ncu, hipStream_t s) {
     const size_t kw = (a.k + 3) / 4, words = (size_t)a.k * a.m * kw;
     const bool by_arg = g_tune.dec_direct != 2 && a.single_coef_host && words <= kCoefWords;
     if (by_arg) memcpy(cw.w, a.single_coef_host, words * 4);
-    if (a.k == 20)   // RS(20,30): rows from the device coefficient table
+    if (a.k == 20)   // RS(20,30), RS(16,24): rows from the device coefficient table
         e = direct_launch<20, POL, 2>(a, cw, s);
+    else if (a.k == 16)
+        e = direct_launch<16, POL, 2>(a, cw, s);
     else if (!by_arg)
         e = a.k == 2 ? direct_launch<2, POL, 0>(a, cw, s) : a.k == 8 ? direct_launch<8, POL, 0>(a, cw, s)
                                                                      : direct_launch<0, POL, 0>(a, cw, s);
@@ -364,6 +370,43 @@ static hipError_t direct_dispatch(const ReconArgs& a, int ncu, hipStream_t s) {
     if (a.maxe <= 4) return hard_launch<4, POL>(a, ncu, s);
     if (a.maxe <= 8) return hard_launch<8, POL>(a, ncu, s);
     return hard_launch<16, POL>(a, ncu, s);
+}
+
+// One lane per block (grid-stride): count the blocks the direct decode would send to the
+// worklist (two or more erased data shards, recoverable, within the output slots); the last
+// workgroup to finish turns the count into the batch's path and rewinds the counters.
+__global__ __launch_bounds__(kThreads) void rs_classify_kernel(const uint32_t* masks, uint32_t nblocks, uint32_t k,
+                                                               uint32_t m, uint32_t max_out, uint32_t* gate,
+                                                               uint32_t thr_pm) {
+    const uint32_t all = low_mask(k + m), kmask = low_mask(k);
+    uint32_t multi = 0;
+    for (uint32_t b = blockIdx.x * kThreads + threadIdx.x; b < nblocks; b += gridDim.x * kThreads) {
+        const uint32_t mask = masks[b] & all;
+        const uint32_t e = k - __popc(mask & kmask);
+        multi += e >= 2 && (uint32_t)__popc(mask) >= k && !(max_out && e > max_out);
+    }
+    // wave sum, then one atomic per wave
+    for (int o = 32; o > 0; o >>= 1) multi += __shfl_xor(multi, o);
+    if ((threadIdx.x & 63) == 0 && multi) atomicAdd(gate + kGateCount, multi);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(gate + kGateDone, 1u) == gridDim.x - 1) {
+            const uint32_t n = atomicAdd(gate + kGateCount, 0u);
+            atomicExch(gate, (uint64_t)n * 1000u > (uint64_t)nblocks * thr_pm ? 2u : 1u);
+            atomicExch(gate + kGateCount, 0u);
+            atomicExch(gate + kGateDone, 0u);
+        }
+    }
+}
+
+hipError_t launch_rs_classify(const uint32_t* masks, uint32_t nblocks, uint32_t k, uint32_t m, uint32_t max_out,
+                              uint32_t* gate, uint32_t thr_pm, int ncu, hipStream_t s) {
+    const uint32_t need = (nblocks + kThreads - 1) / kThreads;
+    const int grid = (int)std::max<uint32_t>(1, std::min<uint32_t>(need, (uint32_t)ncu * 4));
+    hipLaunchKernelGGL(rs_classify_kernel, dim3(grid), dim3(kThreads), 0, s, masks, nblocks, k, m, max_out, gate,
+                       thr_pm);
+    return hipGetLastError();
 }
 
 hipError_t launch_rs_recover_direct(const ReconArgs& a, int ncu, hipStream_t s) {

@@ -51,7 +51,7 @@ def main():
     dp, pp, op = data.data_ptr(), par.data_ptr(), out.data_ptr()
     # every knob any variant sets, at its default: tune(D) must undo each variant completely
     D = dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=1, dec_ipl=0, dec_direct=1, dec_nt=3, dir_wpc=-1, dir_nt=-1,
-             dec_fixk=2, dec_sorted=1, dec_pseg=0, dec_tier=0, dec_direct20=0)
+             dec_fixk=2, dec_sorted=1, dec_pseg=0, dec_tier=0, dec_direct_big=0, dec_gate=0, dec_gate_pm=10)
     variants = {"direct (default)": D,
                 "direct, PermTab rows by vector load": dict(D, dec_direct=2),
                 "direct noswz": dict(D, dec_swz=0),
@@ -75,12 +75,12 @@ def main():
         variants["default + status array"] = dict(D, _status=1)
     if args.tiers:
         variants = {"default": D}
-        for rt in (1, 2, 4):
+        for rt in (2, 4):
             variants["tier %d" % rt] = dict(D, dec_tier=rt)
-            variants["tier %d wpc4" % rt] = dict(D, dec_tier=rt, dec_wpc=4)
-        if k == 20:
+        if k in (16, 20):
             for w in (0, 4, 3):
-                variants["direct20 wpc%d" % w] = dict(D, dec_direct20=1, dir_wpc=w)
+                variants["direct_big wpc%d" % w] = dict(D, dec_direct_big=1, dir_wpc=w)
+                variants["gated wpc%d" % w] = dict(D, dec_direct_big=1, dec_gate=1, dir_wpc=w)
     base = codec.set_tuning(**D)
     use_status = [False]
 

@@ -16,6 +16,8 @@ timeout -k 10 200 python -u tools/dec_select.py --tiers --k 20 --m 10 --blocks 5
 tail -1 "$O/tiers_2030_multi.log"
 timeout -k 10 200 python -u tools/dec_select.py --tiers --k 16 --m 8 --blocks 524288 --multi 8 --rounds 5 > "$O/tiers_1624_multi.log" 2>&1
 tail -1 "$O/tiers_1624_multi.log"
+timeout -k 10 200 python -u tools/dec_select.py --tiers --k 16 --m 8 --blocks 524288 --rounds 5 > "$O/tiers_1624_single.log" 2>&1
+tail -1 "$O/tiers_1624_single.log"
 timeout -k 10 200 python -u bench.py --gpus 2 --rehearse-one-gpu --steps 10 --warmup 3 --no-cpu-baseline --host-blocks 0 > "$O/bench_n2_rehearse.log" 2>&1
 tail -1 "$O/bench_n2_rehearse.log"
 set +e
