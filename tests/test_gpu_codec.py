@@ -525,6 +525,9 @@ def test_stream_switch_orders_shared_workspace(fec, torch):
             rng = np.random.default_rng(0x57 + i)
             sh = torch.zeros((B, n, S), dtype=torch.uint8, device="cuda")
             sh[:, :k, :L] = torch.from_numpy(rng.integers(0, 256, (B, k, L), dtype=np.uint8)).cuda()
+            # the data was written on torch's stream; the codec's streams are non-blocking and do
+            # not order after it (the first batch was only saved by the table upload's device sync)
+            torch.cuda.synchronize()
             c.set_stream(streams[i].cuda_stream)
             c.rs_encode(k, m, sh, shard_len=L)
             c.sync()

@@ -10,7 +10,7 @@ TAG=${1:?tag}
 R=$(pwd)
 O=$R/gpurun_out/$TAG
 mkdir -p "$O"
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$O/pytest_gpu.log" 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu --maxfail=3 -q --timeout 120 --timeout-method thread > "$O/pytest_gpu.log" 2>&1
 tail -2 "$O/pytest_gpu.log"
 timeout -k 10 120 python -u -c 'import __graft_entry__ as g; g.smoke(); print("smoke ok")' > "$O/smoke.log" 2>&1
 tail -1 "$O/smoke.log"

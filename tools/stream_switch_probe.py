@@ -30,6 +30,7 @@ def main():
             rng = np.random.default_rng(0x57 + i)
             sh = torch.zeros((B, n, S), dtype=torch.uint8, device="cuda")
             sh[:, :k, :L] = torch.from_numpy(rng.integers(0, 256, (B, k, L), dtype=np.uint8)).cuda()
+            torch.cuda.synchronize()   # written on torch's stream: order it before the codec's
             c.set_stream(streams[i].cuda_stream)
             c.rs_encode(k, m, sh, shard_len=L)
             c.sync()
