@@ -192,7 +192,8 @@ class Codec:
                    "enc_qwpc": 15, "enc_qdepth": 16, "dec_wave": 17, "enc_diag": 18, "dec_fused": 19, "dec_ipl": 20, "dec_diag": 21,
                    "enc_dyadic": 22, "dec_direct": 23, "dec_sorted": 24, "dec_fixk": 25, "host_chunk": 26,
                    "dir_wpc": 27, "dir_nt": 28, "dec_pseg": 29, "enc_bits": 30, "enc_bwpc": 31,
-                   "dec_tier": 32, "dec_direct_big": 33, "dec_gate": 34, "dec_gate_pm": 35}
+                   "dec_tier": 32, "dec_direct_big": 33, "dec_gate": 34, "dec_gate_pm": 35,
+                   "host_gather": 36}
 
     def set_tuning(self, **knobs):
         """Set kernel-selection knobs; returns the previous values (pass them back to restore)."""

@@ -8,6 +8,7 @@
 #include <algorithm>
 
 #include "../../include/fec_hip.h"
+#include "fec_kernels.hpp"
 
 namespace fec {
 
@@ -66,6 +67,68 @@ Error hip_error(hipError_t e, const char* what) {
 Error codec_rc(int rc) { return rc ? Error{fec_strerror(rc), rc} : Error::nil(); }
 }  // namespace
 
+// ------------------------------------------------------------------ PacketPool
+
+namespace {
+struct PoolEntry {
+    uintptr_t lo, hi;
+    uint64_t dev;
+    std::weak_ptr<PacketPool> pool;
+};
+std::mutex g_pool_mu;
+std::vector<PoolEntry> g_pools;
+}  // namespace
+
+Error PacketPool::New(size_t nbuf, std::shared_ptr<PacketPool>* out) {
+    out->reset();
+    if (nbuf == 0 || nbuf > (size_t(1) << 26)) return Error::text("packet pool size out of range");
+    std::shared_ptr<PacketPool> p(new PacketPool());
+    p->bytes_ = nbuf * kSlot;
+    void* base = nullptr;
+    hipError_t h = hipHostMalloc(&base, p->bytes_, hipHostMallocMapped | hipHostMallocPortable);
+    if (h != hipSuccess) return hip_error(h, "hipHostMalloc");
+    p->base_ = static_cast<uint8_t*>(base);
+    memset(p->base_, 0, p->bytes_);
+    void* dev = nullptr;
+    if ((h = hipHostGetDevicePointer(&dev, base, 0)) != hipSuccess) return hip_error(h, "hipHostGetDevicePointer");
+    p->dev_ = (uint64_t)(uintptr_t)dev;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        g_pools.push_back(PoolEntry{(uintptr_t)p->base_, (uintptr_t)p->base_ + p->bytes_, p->dev_, p});
+    }
+    *out = std::move(p);
+    return Error::nil();
+}
+
+PacketPool::~PacketPool() {
+    Unregister();
+    if (base_) (void)hipHostFree(base_);
+}
+
+void PacketPool::Unregister() {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (auto it = g_pools.begin(); it != g_pools.end(); ++it)
+        if (it->lo == (uintptr_t)base_) {
+            g_pools.erase(it);
+            break;
+        }
+}
+
+uint64_t PacketPool::Lookup(const uint8_t* p, size_t len, std::shared_ptr<PacketPool>* pool) {
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (const PoolEntry& e : g_pools)
+        if (a >= e.lo && a <= e.hi && len <= e.hi - a) {   // the same test as DevAddr
+            std::shared_ptr<PacketPool> sp = e.pool.lock();
+            if (!sp) return 0;
+            *pool = std::move(sp);
+            return e.dev + (a - e.lo);
+        }
+    return 0;
+}
+
+// ------------------------------------------------------------------ BatchEncoder
+
 Error BatchEncoder::New(DecoderFECScheme scheme, int k, int m, size_t maxBlocks, std::shared_ptr<Engine> engine,
                         std::unique_ptr<BatchEncoder>* out) {
     out->reset();
@@ -93,6 +156,8 @@ BatchEncoder::~BatchEncoder() {
         if (s.h_out) (void)hipHostFree(s.h_out);
         if (s.d_in) (void)hipFree(s.d_in);
         if (s.d_out) (void)hipFree(s.d_out);
+        if (s.h_desc) (void)hipHostFree(s.h_desc);
+        if (s.d_desc) (void)hipFree(s.d_desc);
     }
 }
 
@@ -108,6 +173,14 @@ Error BatchEncoder::init() {
         if ((h = hipHostMalloc(&s.h_out, out_bytes, hipHostMallocDefault)) != hipSuccess) return hip_error(h, "hipHostMalloc");
         if ((h = hipMalloc(&s.d_in, in_bytes)) != hipSuccess) return hip_error(h, "hipMalloc");
         if ((h = hipMalloc(&s.d_out, out_bytes)) != hipSuccess) return hip_error(h, "hipMalloc");
+        const size_t desc_bytes = maxBlocks_ * (size_t)k_ * sizeof(fk::GatherDesc);
+        if ((h = hipHostMalloc(&s.h_desc, desc_bytes, hipHostMallocDefault)) != hipSuccess)
+            return hip_error(h, "hipHostMalloc");
+        if ((h = hipMalloc(&s.d_desc, desc_bytes)) != hipSuccess) return hip_error(h, "hipMalloc");
+        void* in_dev = nullptr;
+        if ((h = hipHostGetDevicePointer(&in_dev, s.h_in, 0)) != hipSuccess)
+            return hip_error(h, "hipHostGetDevicePointer");
+        s.in_dev = (uint64_t)(uintptr_t)in_dev;
         hipEvent_t ev;
         if ((h = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hip_error(h, "hipEventCreate");
         s.done = ev;
@@ -139,6 +212,10 @@ Error BatchEncoder::Submit(Block& b, RepairQueue* q) {
     e = rs_ ? rs_->stageRepairInput(b, dst, s->slot, &L) : xor_->stageRepairInput(b, dst, s->slot, &L, &count);
     if (!e.ok()) return e;
     if (xor_ && count != k_) return Error::text("block does not match the encoder's source symbol count");
+    // the framed shards as gather descriptors too, in case a referenced block joins this batch
+    fk::GatherDesc* desc = static_cast<fk::GatherDesc*>(s->h_desc) + s->blocks.size() * (size_t)k_;
+    for (int i = 0; i < k_; ++i)
+        desc[i] = fk::GatherDesc{s->in_dev + (uint64_t)(dst - s->h_in) + (uint64_t)i * s->slot, (uint32_t)L, fk::kNoFrame};
     s->blocks.push_back(Pending{q, q ? q->token() : nullptr, b.id, L});
     s->maxLen = std::max(s->maxLen, L);
     return Error::nil();
@@ -156,6 +233,7 @@ Error BatchEncoder::slotFor(size_t want, Set** out) {
         Error e = retire(*s);
         if (!e.ok()) return e;
     }
+    if (holding_ == cur_) spill(*s);
     if (!s->blocks.empty() && (s->blocks.size() >= maxBlocks_ || std::max<size_t>(want, 16) > s->slot)) {
         Error e = flushImpl(nullptr);
         if (!e.ok()) return e;
@@ -175,12 +253,50 @@ Error BatchEncoder::SubmitPayloads(BlockID id, const uint8_t* const* payloads, c
     size_t biggest = 0;
     for (int i = 0; i < count; ++i) biggest = std::max(biggest, lens[i]);
     if (biggest > kMaxFECPacketBufferSize) return errTooBig((int)biggest);
-    const size_t L = biggest + kRepairPayloadMetadataLen;
     Set* s = nullptr;
-    Error e = slotFor(round16(L), &s);
+    Error e = slotFor(round16(biggest + kRepairPayloadMetadataLen), &s);
     if (!e.ok()) return e;
+    return stageBlock(s, id, payloads, lens, biggest, false, q);
+}
+
+Error BatchEncoder::SubmitRefs(BlockID id, const uint8_t* const* payloads, const size_t* lens, int count,
+                               RepairQueue* q) {
+    if (count < 0 || (count && (!payloads || !lens))) return Error::text("invalid payload list");
+    if (count != k_) return errIncomplete();   // the same checks, in the same order, as SubmitPayloads
+    size_t biggest = 0;
+    for (int i = 0; i < count; ++i) biggest = std::max(biggest, lens[i]);
+    if (biggest > kMaxFECPacketBufferSize) return errTooBig((int)biggest);
+    Set* s = nullptr;
+    Error e = slotFor(round16(biggest + kRepairPayloadMetadataLen), &s);
+    if (!e.ok()) return e;
+    return stageBlock(s, id, payloads, lens, biggest, true, q);
+}
+
+// One validated block into set s: each payload either framed into its pinned slot here, or (refs,
+// and it lies in a registered pool) left where it is, to be gathered and framed by the device.
+// Every shard gets a gather descriptor, so a batch is gathered as a whole once any shard needs it.
+Error BatchEncoder::stageBlock(Set* s, BlockID id, const uint8_t* const* payloads, const size_t* lens, size_t biggest,
+                               bool refs, RepairQueue* q) {
+    const size_t L = biggest + kRepairPayloadMetadataLen;
     uint8_t* dst = s->h_in + s->blocks.size() * (size_t)k_ * s->slot;
-    for (int i = 0; i < count; ++i) {
+    fk::GatherDesc* desc = static_cast<fk::GatherDesc*>(s->h_desc) + s->blocks.size() * (size_t)k_;
+    for (int i = 0; i < k_; ++i) {
+        if (refs && lens[i]) {
+            // the pools this batch already holds first (no lock, no reference count traffic: the
+            // senders of many connections share one pool), the registry only on a miss
+            uint64_t dev = 0;
+            for (const auto& pool : s->pools)
+                if ((dev = pool->DevAddr(payloads[i], lens[i]))) break;
+            if (!dev) {
+                std::shared_ptr<PacketPool> pool;
+                if ((dev = PacketPool::Lookup(payloads[i], lens[i], &pool))) s->pools.push_back(std::move(pool));
+            }
+            if (dev) {
+                desc[i] = fk::GatherDesc{dev, (uint32_t)lens[i], (uint32_t)biggest};
+                s->gather = true;
+                continue;
+            }
+        }
         uint8_t* slot = dst + (size_t)i * s->slot;
         if (lens[i]) memcpy(slot, payloads[i], lens[i]);
         memset(slot + lens[i], 0, round16(L) - lens[i]);
@@ -188,6 +304,7 @@ Error BatchEncoder::SubmitPayloads(BlockID id, const uint8_t* const* payloads, c
         // BE16 XORed in (xor.go:49-53), which for one framed payload is the same bytes
         slot[biggest] = (uint8_t)(lens[i] >> 8);
         slot[biggest + 1] = (uint8_t)(lens[i] & 0xFF);
+        desc[i] = fk::GatherDesc{s->in_dev + (uint64_t)(slot - s->h_in), (uint32_t)L, fk::kNoFrame};
     }
     s->blocks.push_back(Pending{q, q ? q->token() : nullptr, id, L});
     s->maxLen = std::max(s->maxLen, L);
@@ -196,11 +313,52 @@ Error BatchEncoder::SubmitPayloads(BlockID id, const uint8_t* const* payloads, c
 
 Error BatchEncoder::Flush() { return flushImpl(nullptr); }
 
-bool BatchEncoder::PopRaw(RawBlock* out) {
-    if (raw_.empty()) return false;
-    *out = std::move(raw_.front());
-    raw_.pop_front();
+bool BatchEncoder::PeekRaw(RawView* out) {
+    if (!raw_.empty()) {
+        const RawBlock& r = raw_.front();
+        *out = RawView{r.id, r.len, r.bytes.data(), r.len};
+        return true;
+    }
+    if (holding_ < 0) return false;
+    const Set& s = sets_[holding_];
+    const Pending& p = s.blocks[s.rawNext];
+    *out = RawView{p.id, p.len, s.h_out + s.rawNext * (size_t)m_ * s.slot, s.slot};
     return true;
+}
+
+void BatchEncoder::PopRaw() {
+    if (!raw_.empty()) {
+        raw_.pop_front();
+        return;
+    }
+    if (holding_ < 0) return;
+    Set& s = sets_[holding_];
+    if (++s.rawNext < s.blocks.size()) return;
+    s.blocks.clear();
+    s.maxLen = 0;
+    s.rawNext = 0;
+    holding_ = -1;
+}
+
+size_t BatchEncoder::RawLen() const {
+    return raw_.size() + (holding_ >= 0 ? sets_[holding_].blocks.size() - sets_[holding_].rawNext : 0);
+}
+
+void BatchEncoder::spill(Set& s) {
+    for (size_t i = s.rawNext; i < s.blocks.size(); ++i) {
+        const Pending& p = s.blocks[i];
+        RawBlock rb;
+        rb.id = p.id;
+        rb.len = p.len;
+        rb.bytes.resize((size_t)m_ * p.len);
+        for (int j = 0; j < m_; ++j)
+            memcpy(rb.bytes.data() + (size_t)j * p.len, s.h_out + (i * (size_t)m_ + j) * s.slot, p.len);
+        raw_.push_back(std::move(rb));
+    }
+    s.blocks.clear();
+    s.maxLen = 0;
+    s.rawNext = 0;
+    holding_ = -1;
 }
 
 Error BatchEncoder::flushImpl(size_t* delivered) {
@@ -215,8 +373,18 @@ Error BatchEncoder::flushImpl(size_t* delivered) {
     if (!e.ok()) return e;
     hipStream_t st = (hipStream_t)fec_ctx_stream(ctx);
     const size_t B = s.blocks.size();
-    hipError_t h = hipMemcpyAsync(s.d_in, s.h_in, B * (size_t)k_ * s.slot, hipMemcpyHostToDevice, st);
-    if (h != hipSuccess) return hip_error(h, "hipMemcpyAsync H2D");
+    hipError_t h;
+    if (s.gather) {   // referenced payloads: the device pulls every shard of the batch itself
+        if ((h = hipMemcpyAsync(s.d_desc, s.h_desc, B * (size_t)k_ * sizeof(fk::GatherDesc), hipMemcpyHostToDevice,
+                                st)) != hipSuccess)
+            return hip_error(h, "hipMemcpyAsync H2D");
+        if ((h = hipSetDevice(engine_->device())) != hipSuccess) return hip_error(h, "hipSetDevice");
+        if ((h = fk::launch_gather_desc(static_cast<const fk::GatherDesc*>(s.d_desc), (uint32_t)(B * (size_t)k_), s.d_in,
+                                        s.slot, st)) != hipSuccess)
+            return hip_error(h, "gather launch");
+    } else if ((h = hipMemcpyAsync(s.d_in, s.h_in, B * (size_t)k_ * s.slot, hipMemcpyHostToDevice, st)) != hipSuccess) {
+        return hip_error(h, "hipMemcpyAsync H2D");
+    }
     int rc;
     if (rs_)
         rc = fec_rs_encode_batch(ctx, k_, m_, s.maxLen, B, s.d_in, (size_t)k_ * s.slot, s.d_out, (size_t)m_ * s.slot,
@@ -235,6 +403,7 @@ Error BatchEncoder::flushImpl(size_t* delivered) {
     if (next.inFlight) {
         if (!(e = retire(next)).ok()) return e;
     }
+    if (holding_ == cur_) spill(next);
     pump(delivered);   // a full queue is not a failure of this flush
     return Error::nil();
 }
@@ -247,6 +416,18 @@ Error BatchEncoder::waitSet(Set& s) {
 Error BatchEncoder::retire(Set& s) {
     Error e = waitSet(s);
     if (!e.ok()) return e;
+    s.pools.clear();   // the device has read every referenced payload
+    s.gather = false;
+    s.inFlight = false;
+    bool raw_only = !s.blocks.empty();
+    for (const Pending& p : s.blocks) raw_only = raw_only && !p.q;
+    if (raw_only) {   // hand the blocks out of h_out in place (PeekRaw); an older holder goes first
+        const int idx = (int)(&s - sets_);
+        if (holding_ >= 0 && holding_ != idx) spill(sets_[holding_]);
+        holding_ = idx;
+        s.rawNext = 0;
+        return Error::nil();
+    }
     for (size_t i = 0; i < s.blocks.size(); ++i) {
         const Pending& p = s.blocks[i];
         if (!p.q) {   // no queue: keep the payloads, back to back, for PopRaw

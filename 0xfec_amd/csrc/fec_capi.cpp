@@ -852,13 +852,25 @@ static int host_reconstruct_rs(fec_ctx* ctx, Code* code, int k, int m, size_t le
             slots = std::max(slots, (size_t)e);
         }
         uint8_t* d_par = s.d_in + nb * k * ssd;   // parity planes [P][nb][ssd]
+        HIP_TRY(hipMemcpyAsync(s.d_masks, s.h_masks, nb * 4, hipMemcpyHostToDevice, s.s));
         if (pinned) {
             const size_t draw = span_bytes(nb, k, dbs, ss, len);
             if ((rc = host_raw_grow(s, draw + span_bytes(nb, m, pbs, ss, len) + 16))) return rc;
             if ((rc = pinned_up(s, s.d_in, (size_t)k * ssd, ssd, data + b0 * dbs, dbs, ss, nb, k, len, s.d_raw, k)))
                 return rc;
-            if (P && (rc = pinned_up(s, d_par, ssd, nb * ssd, parity + b0 * pbs, pbs, ss, nb, P, len,
-                                     s.d_raw + ((draw + 15) & ~size_t(15)), m)))
+            // parity: the device reads exactly the planes each block's mask needs straight out of
+            // the caller's pinned buffer (fec_pack.hip gather_planes_kernel), instead of the whole
+            // [nb][m] span riding one linear DMA; a buffer the runtime cannot map takes the DMA
+            const uint8_t* dpar = nullptr;
+            const bool mapped = P && fk::g_tune.host_gather &&
+                                hipHostGetDevicePointer((void**)&dpar, (void*)(parity + b0 * pbs), 0) == hipSuccess &&
+                                dpar;
+            if (P && !mapped) (void)hipGetLastError();
+            if (mapped)
+                HIP_TRY(fk::launch_gather_planes(dpar, pbs, ss, (uint32_t)len, s.d_masks, (uint32_t)nb, (uint32_t)P,
+                                                 (uint32_t)k, d_par, ssd, s.s));
+            else if (P && (rc = pinned_up(s, d_par, ssd, nb * ssd, parity + b0 * pbs, pbs, ss, nb, P, len,
+                                          s.d_raw + ((draw + 15) & ~size_t(15)), m)))
                 return rc;
         } else {
             parallel_for(nb, [&](size_t lo, size_t hi) {
@@ -875,7 +887,6 @@ static int host_reconstruct_rs(fec_ctx* ctx, Code* code, int k, int m, size_t le
             });
             HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, (nb * k + P * nb) * ssd, hipMemcpyHostToDevice, s.s));
         }
-        HIP_TRY(hipMemcpyAsync(s.d_masks, s.h_masks, nb * 4, hipMemcpyHostToDevice, s.s));
         rc = on_stream(ctx, s, [&] {
             return rs_reconstruct_device(ctx, code, len, nb, s.d_in, (size_t)k * ssd, d_par, ssd, ssd, s.d_masks,
                                          s.d_status, ctx->d_err + 1, s.d_out, slots * ssd, (uint32_t)slots, nb * ssd);
@@ -1094,7 +1105,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 28 ? &fk::g_tune.dir_nt : key == 29 ? &fk::g_tune.dec_pseg
               : key == 30 ? &fk::g_tune.enc_bits : key == 31 ? &fk::g_tune.enc_bwpc
               : key == 32 ? &fk::g_tune.dec_tier : key == 33 ? &fk::g_tune.dec_direct_big
-              : key == 34 ? &fk::g_tune.dec_gate : key == 35 ? &fk::g_tune.dec_gate_pm : nullptr;
+              : key == 34 ? &fk::g_tune.dec_gate : key == 35 ? &fk::g_tune.dec_gate_pm
+              : key == 36 ? &fk::g_tune.host_gather : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

@@ -255,7 +255,7 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
 
 // K: compile-time data shard count for the IPL = 1 body (0: runtime a.k); W > 0: that body with a
 // rolling window of W loaded inputs (recon_item_roll) instead of all K up front.
-template <int MAXE, int POL, bool FUSED, int IPL, int K = 0, int W = 0>
+template <int MAXE, int POL, bool FUSED, int IPL, int K = 0, int W = 0, bool RP = false>
 __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs a) {
     constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     // blocks per wave slice: the rolling form is launched for shards of 64+ chunks only, where
@@ -342,7 +342,8 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
         const uint32_t rows = wave_rows<MAXE>(nout);
         if (nout == 0) return;
         const uint32_t rb = a.sorted ? *reinterpret_cast<const uint32_t*>(P + lay.blk_off) : blk;
-        if constexpr (K > 0 && W > 0) recon_item_roll<K, MAXE, W, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
+        if constexpr (K > 0 && W > 0)
+            recon_item_roll<K, MAXE, W, NTL, NTS, RP>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
         else if constexpr (K > 0) recon_item_k<K, MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
         else recon_item<MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
     } else {
@@ -551,7 +552,10 @@ static hipError_t recon_wave_dispatch(const ReconArgs& a, hipStream_t s) {
         const bool roll = g_tune.dec_fixk == 2 && a.cps >= 64;
         const size_t lds2 = occupancy_lds(g_tune.dec_wpc, 4 * wave_slice_bytes(a.k, a.maxe, a.lay.stride, 2));
         if (a.k == 16 && a.maxe == 8 && g_tune.dec_fixk) {
-            if (roll)
+            if (roll && g_tune.dec_fixk == 3)
+                hipLaunchKernelGGL((rs_reconstruct_wave_kernel<8, POL, false, 1, 16, 8, true>), dim3(grid),
+                                   dim3(kThreads), lds2, s, a);
+            else if (roll)
                 hipLaunchKernelGGL((rs_reconstruct_wave_kernel<8, POL, false, 1, 16, 8>), dim3(grid), dim3(kThreads),
                                    lds2, s, a);
             else
@@ -562,6 +566,12 @@ static hipError_t recon_wave_dispatch(const ReconArgs& a, hipStream_t s) {
         // the reference's own receiver code RS(20,30) (manager.go:80-90)
         if (a.k == 20 && a.maxe == 10 && g_tune.dec_fixk) {
             // (the rolling window measured -0.8 % here: 203 VGPRs, still 2 waves/SIMD)
+            if (g_tune.dec_fixk == 3 && a.cps >= 64) {   // rolling window + row-pipelined table reads
+                hipLaunchKernelGGL((rs_reconstruct_wave_kernel<16, POL, false, 1, 20, 8, true>), dim3(grid),
+                                   dim3(kThreads), occupancy_lds(g_tune.dec_wpc, 4 * wave_slice_bytes(a.k, a.maxe, a.lay.stride, 2)),
+                                   s, a);
+                return hipGetLastError();
+            }
             hipLaunchKernelGGL((rs_reconstruct_wave_kernel<16, POL, false, 1, 20>), dim3(grid), dim3(kThreads), lds,
                                s, a);
             return hipGetLastError();

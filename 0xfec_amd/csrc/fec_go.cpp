@@ -100,6 +100,32 @@ int fec_go_encoder_submit(fec_go_encoder* e, uint64_t block_id, const uint8_t* c
     return report(e->enc->SubmitPayloads(block_id, payloads, lens, count, nullptr));
 }
 
+int fec_go_encoder_submit_ref(fec_go_encoder* e, uint64_t block_id, const uint8_t* const* payloads,
+                              const size_t* lens, int count) {
+    if (!e) return FEC_ERR_INVALID_ARG;
+    return report(e->enc->SubmitRefs(block_id, payloads, lens, count, nullptr));
+}
+
+struct fec_go_pool {
+    std::shared_ptr<fec::PacketPool> p;
+};
+
+fec_go_pool* fec_go_pool_new(size_t nbuf, uint8_t** base, int* err) {
+    if (base) *base = nullptr;
+    std::unique_ptr<fec_go_pool> gp(new fec_go_pool());
+    const int rc = report(fec::PacketPool::New(nbuf, &gp->p));
+    if (err) *err = rc;
+    if (rc) return nullptr;
+    if (base) *base = gp->p->base();
+    return gp.release();
+}
+
+void fec_go_pool_free(fec_go_pool* p) {
+    if (!p) return;
+    p->p->Unregister();   // no new references; the memory goes with the last batch that reads it
+    delete p;
+}
+
 int fec_go_encoder_flush(fec_go_encoder* e) { return e ? report(e->enc->Flush()) : FEC_ERR_INVALID_ARG; }
 
 int fec_go_encoder_poll(fec_go_encoder* e, int wait, uint64_t* block_ids, uint32_t* repair_len, uint8_t* repairs,
@@ -112,13 +138,13 @@ int fec_go_encoder_poll(fec_go_encoder* e, int wait, uint64_t* block_ids, uint32
     if (err.ok() && !wait && e->enc->InFlight() == 0 && e->enc->Staged() > 0) err = e->enc->Flush();
     if (!err.ok()) return report(err);
     size_t d = 0;
-    fec::BatchEncoder::RawBlock rb;
-    for (; d < max_blocks && e->enc->PopRaw(&rb); ++d) {
-        block_ids[d] = rb.id;
-        repair_len[d] = (uint32_t)rb.len;
-        const size_t c = std::min(rb.len, (size_t)FEC_GO_SLOT);
+    fec::BatchEncoder::RawView rv;
+    for (; d < max_blocks && e->enc->PeekRaw(&rv); ++d, e->enc->PopRaw()) {   // one copy, out of pinned memory
+        block_ids[d] = rv.id;
+        repair_len[d] = (uint32_t)rv.len;
+        const size_t c = std::min(rv.len, (size_t)FEC_GO_SLOT);
         for (int i = 0; i < e->m; ++i)
-            memcpy(repairs + (d * (size_t)e->m + (size_t)i) * FEC_GO_SLOT, rb.bytes.data() + (size_t)i * rb.len, c);
+            memcpy(repairs + (d * (size_t)e->m + (size_t)i) * FEC_GO_SLOT, rv.base + (size_t)i * rv.stride, c);
     }
     if (nblocks) *nblocks = d;
     return report(fec::Error::nil());

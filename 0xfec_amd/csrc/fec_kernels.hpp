@@ -187,6 +187,8 @@ struct Tuning {
     int dec_gate_pm = 10;     // multi-erasure blocks (per mille) above which the plan path is taken
     int dec_tier = 0;         // RS(16,24) / RS(20,30) rebuild in two tiers: waves of <= dec_tier rows
                               // (1, 2 or 4) in a small-register launch, the rest from a worklist (0: off)
+    int host_gather = 1;      // FEC_HOST_PINNED reconstruct: the parity planes each block reads are pulled by
+                              // the device straight from the caller's pinned buffer (0: whole span by DMA)
 };
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):
@@ -249,6 +251,23 @@ hipError_t launch_span_to_stage(uint8_t* stage, uint64_t st_bs, uint64_t st_ss, 
                                 uint64_t src_ss, uint32_t nb, uint32_t cols, uint32_t len, hipStream_t s);
 hipError_t launch_stage_to_packed(uint8_t* packed, const uint8_t* stage, uint64_t st_bs, uint64_t st_ss, uint32_t nb,
                                   uint32_t cols, uint32_t len, hipStream_t s);
+
+// Device-side gathers out of pinned, device-mapped host memory (fec_pack.hip). A descriptor
+// names one payload or framed shard: `len` bytes at `src` (a device-visible address), and
+// `frame` = the block's biggest payload length, at which BE16(len) is written
+// (reed_solomon.go:77-87), or kNoFrame for bytes copied verbatim. Shard i is written to
+// dst + i * slot, all slot bytes (zeros past the content).
+constexpr uint32_t kNoFrame = 0xFFFFFFFFu;
+struct GatherDesc {
+    uint64_t src;
+    uint32_t len;
+    uint32_t frame;
+};
+hipError_t launch_gather_desc(const GatherDesc* desc, uint32_t n, uint8_t* dst, uint64_t slot, hipStream_t s);
+// The parity planes [0, planes) of nb blocks (block b, plane r at base + b*bs + r*ss) that each
+// block's present mask makes it read, to dst + (r*nb + b)*slot; the others are skipped.
+hipError_t launch_gather_planes(const uint8_t* base, uint64_t bs, uint64_t ss, uint32_t len, const uint32_t* masks,
+                                uint32_t nb, uint32_t planes, uint32_t k, uint8_t* dst, uint64_t slot, hipStream_t s);
 
 // Blocks per decode tile for shard chunk count `cps`, bounded by LDS.
 uint32_t pick_tile_blocks(uint32_t cps, uint32_t k, uint32_t maxe, const PlanLayout& lay);

@@ -151,14 +151,53 @@ __device__ __forceinline__ void recon_item_k(const ReconArgs& a, const uint8_t* 
     }
 }
 
+// acc[r] ^= T[r][j] x_a ^ T[r][j+1] x_b for the ROWS rows, with each row's PermTab words read from
+// LDS one row ahead of their use (scheduling barriers keep the reads of row r + 2 behind row r's
+// products). Left to itself the compiler issues every row's table reads of the pair at once to
+// hide LDS latency: 10 words per row, 100 VGPRs at 10 rows (RS(20,30)), which is what held the
+// K = 20 rebuild at 2 waves per SIMD; here 20 are live, and other waves hide the latency.
+template <int K, int ROWS>
+__device__ __forceinline__ void mac2_rows_pipe(uint32_t (&acc)[ROWS][4], const Idx (&ia)[4], const Idx (&ib)[4],
+                                               const gf::PermTab* t, int j) {
+    uint4 la = *reinterpret_cast<const uint4*>(t + j), lb = *reinterpret_cast<const uint4*>(t + j + 1);
+    uint32_t a2 = t[j].t2, b2 = t[j + 1].t2;
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+        uint4 na = la, nb = lb;
+        uint32_t na2 = a2, nb2 = b2;
+        if (r + 1 < ROWS) {
+            const gf::PermTab* tn = t + (r + 1) * K + j;
+            na = *reinterpret_cast<const uint4*>(tn);
+            nb = *reinterpret_cast<const uint4*>(tn + 1);
+            na2 = tn[0].t2;
+            nb2 = tn[1].t2;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const Prod3 p = gprod(ia[d], la, a2);
+            const Prod3 q = gprod(ib[d], lb, b2);
+            acc[r][d] = xor3(xor3(xor3(acc[r][d], p.p0, p.p1), p.p2, q.p0), q.p1, q.p2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        la = na, lb = nb, a2 = na2, b2 = nb2;
+    }
+}
+
 // recon_rows_k with a rolling load window (dec_fixk = 2): W inputs are loaded up front, and each
 // folded pair's registers take the loads of the pair W inputs ahead, so at most W inputs are
-// live instead of K (K = 16: 64 -> 32 data VGPRs), for more resident waves per SIMD.
-template <int K, int ROWS, int W, bool NTL, bool NTS>
+// live instead of K (K = 16: 64 -> 32 data VGPRs), for more resident waves per SIMD. RP: the
+// rows' table reads pipelined one row ahead (mac2_rows_pipe, dec_fixk = 3).
+template <int K, int ROWS, int W, bool NTL, bool NTS, bool RP = false>
 __device__ __forceinline__ void recon_rows_roll(const ReconArgs& a, const uint8_t* P, const gf::PermTab* T,
                                                 uint8_t* dblk, const uint8_t* pbase, uint8_t* oblk, uint32_t c,
                                                 uint32_t nout) {
     static_assert(K % 2 == 0 && W % 2 == 0 && W <= K, "inputs are folded and loaded in pairs");
+    // A body that starts like no other: the row bodies of recon_item_roll's switch share their
+    // opening (the window's loads, the first pair's splits, row 0's products), and the compiler
+    // hoists an identical opening into the block before the switch, where it is live across
+    // every body at once (RS(20,30): ~96 VGPRs of split indices, 193 in all).
+    if constexpr (RP) asm volatile("; rows %0" ::"n"(ROWS));
     constexpr int NS = (K + 7) / 8;   // the slot area is rounded up to 8 bytes
     uint2 sl[NS];
 #pragma unroll
@@ -189,8 +228,12 @@ __device__ __forceinline__ void recon_rows_roll(const ReconArgs& a, const uint8_
             x[j + W] = load(j + W);
             x[j + W + 1] = load(j + W + 1);
         }
+        if constexpr (RP) {
+            mac2_rows_pipe<K, ROWS>(acc, ia, ib, t, j);
+        } else {
 #pragma unroll
-        for (int r = 0; r < ROWS; ++r) mac2(acc[r], ia, ib, t + r * K + j, t + r * K + j + 1);
+            for (int r = 0; r < ROWS; ++r) mac2(acc[r], ia, ib, t + r * K + j, t + r * K + j + 1);
+        }
     }
     const uint32_t nb = a.len - c * kChunk;
     const uint8_t* out_idx = P + a.lay.out_off;
@@ -201,7 +244,7 @@ __device__ __forceinline__ void recon_rows_roll(const ReconArgs& a, const uint8_
                              nb, a.pad_zero);
 }
 
-template <int K, int MAXE, int W, bool NTL, bool NTS>
+template <int K, int MAXE, int W, bool NTL, bool NTS, bool RP = false>
 __device__ __forceinline__ void recon_item_roll(const ReconArgs& a, const uint8_t* P, const gf::PermTab* T,
                                                 uint32_t blk, uint32_t c, uint32_t rows, uint32_t nout) {
     uint8_t* dblk = a.data + (uint64_t)blk * a.dbs + (uint64_t)c * kChunk;
@@ -210,7 +253,7 @@ __device__ __forceinline__ void recon_item_roll(const ReconArgs& a, const uint8_
     uint8_t* oblk = a.out ? a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk : nullptr;
     constexpr int R = MAXE < K ? (MAXE <= 8 ? MAXE : 10) : K;
     static_assert(R <= 10, "row bodies 1..10");
-#define FEC_ROLL_ROWS(N) recon_rows_roll<K, N, W, NTL, NTS>(a, P, T, dblk, pbase, oblk, c, nout)
+#define FEC_ROLL_ROWS(N) recon_rows_roll<K, N, W, NTL, NTS, RP>(a, P, T, dblk, pbase, oblk, c, nout)
     switch (rows) {   // wave-uniform
         case 1: FEC_ROLL_ROWS(1); break;
         case 2: if constexpr (R >= 2) FEC_ROLL_ROWS(2); break;

@@ -237,11 +237,14 @@ def host_resident(torch, fec, codec, k, m, blocks, seed, reps=3):
     src[:, :, PAYLOAD + 1] = PAYLOAD & 0xFF
     erased = shard.synth_single_erasures(seed, 0, blocks, k)
     masks = (((1 << n) - 1) & ~(1 << erased)).astype(np.uint32)
-    # PCIe bytes of a step: encode k up + m down; reconstruct k data shards + the parity planes
-    # read up (pinned: the whole parity span rides one linear DMA), the rebuilt shard down
+    # PCIe bytes of a step: encode k up + m down; reconstruct the k data shards up (one linear DMA
+    # of the span), the one parity plane each block reads (pageable: staged by the host; pinned:
+    # pulled by the device straight from the caller's buffer, fec_pack.hip gather_planes_kernel),
+    # the rebuilt shard down
     out = {"blocks": blocks, "layout": "packed host [B][k][1202] + [B][m][1202]",
            "pcie_bytes_per_step": blocks * (k + m + k + 1 + 1) * L,
-           "pcie_bytes_note": "pageable: k+m+k+1+1 shards per block; pinned: k+m+k+m+1 (whole parity span up)"}
+           "pcie_bytes_note": "k+m+k+1+1 shards per block in both forms (pinned: parity planes gathered by the "
+                              "device, only the plane each block reads; round 2 moved the whole parity span, k+m+k+m+1)"}
     for form in ("pinned", "pageable"):
         if form == "pinned":
             data = torch.from_numpy(src.copy()).pin_memory()

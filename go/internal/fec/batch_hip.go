@@ -72,7 +72,14 @@ func (s *BatchSender) Close() {
 
 // Submit replaces `m.scheme.repairSymbols(bS.block)` (manager.go:145): the same validation and
 // error texts, reported now; the frames arrive from Poll.
-func (s *BatchSender) Submit(b *block) error {
+func (s *BatchSender) Submit(b *block) error { return s.submit(b, false) }
+
+// SubmitRef is Submit by reference (fec_go_encoder_submit_ref): payloads in a PacketPool are read
+// by the device when the batch is coded, so the caller keeps them unchanged until Poll returns the
+// block; other payloads are copied now, as Submit.
+func (s *BatchSender) SubmitRef(b *block) error { return s.submit(b, true) }
+
+func (s *BatchSender) submit(b *block, byRef bool) error {
 	defer lockThread()()
 	var pin runtime.Pinner
 	defer pin.Unpin()
@@ -114,6 +121,9 @@ func (s *BatchSender) Submit(b *block) error {
 			}
 			add(p)
 		}
+	}
+	if byRef {
+		return goErr(C.fec_go_encoder_submit_ref(s.e, C.uint64_t(b.id), (**C.uint8_t)(unsafe.Pointer(s.ptrs)), s.lens, C.int(n)))
 	}
 	return goErr(C.fec_go_encoder_submit(s.e, C.uint64_t(b.id), (**C.uint8_t)(unsafe.Pointer(s.ptrs)), s.lens, C.int(n)))
 }

@@ -95,13 +95,18 @@ type batchManager struct {
 	tx      *BatchSender
 	rx      *BatchReceiver
 	pending int // receiver: blocks staged whose data has not been handed out yet
+	// sender with a registered packet-buffer pool (FEC_HIP_POOL): payloads of blocks submitted by
+	// reference, held until their frames are polled, then returned to the pool
+	pool *PacketPool
+	held map[protocol.BlockID][][]byte
 }
 
 var (
-	_ Sender          = &batchManager{}
-	_ Receiver        = &batchManager{}
-	_ RepairPoller    = &batchManager{}
-	_ RecoveredPoller = &batchManager{}
+	_ Sender           = &batchManager{}
+	_ Receiver         = &batchManager{}
+	_ RepairPoller     = &batchManager{}
+	_ RecoveredPoller  = &batchManager{}
+	_ PayloadAllocator = &batchManager{}
 )
 
 func newBatchManager(id protocol.DecoderFECScheme, k, m int, send bool) (*batchManager, error) {
@@ -112,6 +117,9 @@ func newBatchManager(id protocol.DecoderFECScheme, k, m int, send bool) (*batchM
 	bm := &batchManager{manager: mgr}
 	if send {
 		bm.tx, err = NewBatchSender(id, k, m, hipBatchBlocks)
+		if bm.pool = hipPacketPool(); bm.pool != nil {
+			bm.held = make(map[protocol.BlockID][][]byte)
+		}
 	} else {
 		bm.rx, err = NewBatchReceiver(id, k, m, hipBatchBlocks)
 	}
@@ -138,10 +146,23 @@ func (m *batchManager) AddSourceSymbolFrame(f *wire.SourceSymbolFrame) ([]*wire.
 		return nil, err
 	}
 	if bS.block.isComplete() {
-		if err := m.tx.Submit(bS.block); err != nil {
-			return nil, err
+		if m.pool == nil {
+			if err := m.tx.Submit(bS.block); err != nil {
+				return nil, err
+			}
+		} else {
+			// by reference: the device reads the pool buffers when the batch is coded, so they
+			// stay out of the pool until PollRepairFrames returns this block
+			if err := m.tx.SubmitRef(bS.block); err != nil {
+				return nil, err
+			}
+			ps := make([][]byte, 0, len(bS.block.ssidToSourcePayload))
+			for _, p := range bS.block.ssidToSourcePayload {
+				ps = append(ps, p)
+			}
+			m.held[blockID] = ps
 		}
-		// the library copied the payloads: drop the block as manager.go:150-153 does
+		// the library holds what it needs: drop the block as manager.go:150-153 does
 		bS.block = nil
 		bS.isProcessed = true
 	}
@@ -164,8 +185,25 @@ func (m *batchManager) PollRepairFrames(maxFrames int) ([]*wire.RepairFrame, err
 	var out []*wire.RepairFrame
 	for _, fs := range blocks {
 		out = append(out, fs...)
+		if m.pool != nil && len(fs) > 0 {
+			id := fs[0].Metadata.BlockID
+			for _, p := range m.held[id] {
+				m.pool.Put(p)
+			}
+			delete(m.held, id)
+		}
 	}
 	return out, nil
+}
+
+// SourcePayloadBuffer is the packer's buffer for the next SOURCE_SYMBOL payload: a registered
+// packet buffer when this sender has a pool (nil otherwise, or when the pool is exhausted: the
+// packer then makes one as the reference does and SubmitRef copies it).
+func (m *batchManager) SourcePayloadBuffer() []byte {
+	if m.pool == nil {
+		return nil
+	}
+	return m.pool.Get()
 }
 
 // HandleRepairFrame is manager.go:160-198 with recoverSymbolPayloads (:182) replaced by a

@@ -26,3 +26,11 @@ type RecoveredPoller interface {
 	PollRecovered(wait bool) ([][]byte, error)
 	RecoveryPending() bool
 }
+
+// PayloadAllocator is a Sender that wants SOURCE_SYMBOL payloads built in buffers of its own (the
+// GPU batch sender's registered packet-buffer pool, read by the device in place). The packer's
+// hook (go/patches/packet_packer.go.diff, at packet_packer.go:984) asks it first; nil means
+// "make one as the reference does".
+type PayloadAllocator interface {
+	SourcePayloadBuffer() []byte
+}

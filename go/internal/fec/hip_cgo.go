@@ -58,6 +58,16 @@ func hipMode() string {
 
 func useHIP() bool { return hipMode() != "" }
 
+// hipPoolBuffers is the size of the registered packet-buffer pool the batch senders build
+// SOURCE_SYMBOL payloads in (FEC_HIP_POOL, packet_pool_hip.go); 0 (unset): no pool, payloads are
+// copied into the library's pinned staging at submit.
+func hipPoolBuffers() int {
+	if v, err := strconv.Atoi(os.Getenv("FEC_HIP_POOL")); err == nil && v > 0 {
+		return v
+	}
+	return 0
+}
+
 // hipErr turns a fec_hip.h return code into an error (nil for 0).
 func hipErr(rc C.int) error {
 	if rc == 0 {

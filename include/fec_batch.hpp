@@ -81,6 +81,40 @@ private:
     std::shared_ptr<QueueToken> token_ = std::make_shared<QueueToken>();
 };
 
+// A slab of packet buffers in pinned, device-mapped host memory (the Go ABI's opt-in registered
+// pool, include/fec_go.h fec_go_pool_new; the reference allocates each source-symbol payload as
+// make([]byte, 0, MaxPacketBufferSize), packet_packer.go:984). A payload built in one of these
+// buffers can be handed to BatchEncoder::SubmitRefs by address: the device reads it over PCIe
+// when the batch is coded (fec_pack.hip gather_desc_kernel), with no host copy. A pool stays
+// alive while any staged batch references it, whatever its owner does meanwhile.
+class PacketPool {
+public:
+    static constexpr size_t kSlot = 1456;   // protocol.MaxPacketBufferSize rounded up to 16 bytes
+    static Error New(size_t nbuf, std::shared_ptr<PacketPool>* out);
+    ~PacketPool();
+    PacketPool(const PacketPool&) = delete;
+    PacketPool& operator=(const PacketPool&) = delete;
+    uint8_t* base() const { return base_; }
+    size_t bytes() const { return bytes_; }
+    // Registered pools hold [p, p + len): its device address and the pool, else 0 / null (under
+    // the registry's lock: the batch coder asks only for the first payload of each pool per batch).
+    static uint64_t Lookup(const uint8_t* p, size_t len, std::shared_ptr<PacketPool>* pool);
+    // This pool's device address of [p, p + len), or 0 when the range is not inside it.
+    uint64_t DevAddr(const uint8_t* p, size_t len) const {
+        const uintptr_t a = (uintptr_t)p, lo = (uintptr_t)base_;
+        return (a >= lo && a - lo <= bytes_ && len <= bytes_ - (a - lo)) ? dev_ + (a - lo) : 0;
+    }
+    // Stop handing this pool out to lookups (the owner is done with it); the memory goes when the
+    // last batch referencing it retires.
+    void Unregister();
+
+private:
+    PacketPool() = default;
+    uint8_t* base_ = nullptr;
+    uint64_t dev_ = 0;
+    size_t bytes_ = 0;
+};
+
 class BatchEncoder {
 public:
     // scheme: ReedSolomonFECScheme (k, m) or XORFECScheme (k, 1). maxBlocks: blocks per batch.
@@ -99,15 +133,24 @@ public:
     // these payloads.
     // q == nullptr: the block's payloads are kept for PopRaw instead of going to a queue.
     Error SubmitPayloads(BlockID id, const uint8_t* const* payloads, const size_t* lens, int count, RepairQueue* q);
+    // By-reference form: a payload lying in a registered PacketPool is not copied, only its
+    // address is recorded, and the device gathers and frames it when the batch is coded; the
+    // caller keeps it unchanged until the block comes back (PeekRaw / its queue). Any other
+    // payload is copied now, as SubmitPayloads. Same checks and errors.
+    Error SubmitRefs(BlockID id, const uint8_t* const* payloads, const size_t* lens, int count, RepairQueue* q);
     // Encoded blocks submitted without a queue (the Go ABI, include/fec_go.h, whose caller keeps
-    // its own queue), in submission order: the m repair payloads back to back, len bytes each.
-    struct RawBlock {
+    // its own queue), in submission order: repair payload i of the block is len bytes at
+    // base + i * stride. The view points into the completed batch's pinned output (no copy) and
+    // stays valid until PopRaw or any other call on the encoder.
+    struct RawView {
         BlockID id = 0;
         size_t len = 0;
-        std::vector<uint8_t> bytes;
+        const uint8_t* base = nullptr;
+        size_t stride = 0;
     };
-    bool PopRaw(RawBlock* out);
-    size_t RawLen() const { return raw_.size(); }
+    bool PeekRaw(RawView* out);
+    void PopRaw();
+    size_t RawLen() const;
     // Start encoding the staged blocks (asynchronous). No-op when nothing is staged.
     Error Flush();
     // Deliver the frames of every completed batch (non-blocking); *blocks = blocks delivered.
@@ -140,13 +183,29 @@ private:
         uint8_t* h_out = nullptr;   // pinned [maxBlocks][m][kSlotMax]
         uint8_t* d_in = nullptr;
         uint8_t* d_out = nullptr;
+        void* h_desc = nullptr;     // pinned [maxBlocks][k] gather descriptors (fk::GatherDesc)
+        void* d_desc = nullptr;
+        uint64_t in_dev = 0;        // device address of h_in (pinned, mapped)
         void* done = nullptr;       // hipEvent_t
         std::vector<Pending> blocks;
+        std::vector<std::shared_ptr<PacketPool>> pools;   // pools the batch's references point into
         size_t slot = 0;            // S of this batch (16-byte multiple)
         size_t maxLen = 0;          // largest L of this batch
+        bool gather = false;        // some payload is referenced: the device gathers the batch
         bool inFlight = false;
+        size_t rawNext = 0;         // holding (completed, raw blocks kept in h_out): next to hand out
     };
-    std::deque<RawBlock> raw_;
+    struct RawBlock {               // a raw block copied out of a set that had to be reused
+        BlockID id = 0;
+        size_t len = 0;
+        std::vector<uint8_t> bytes;
+    };
+    std::deque<RawBlock> raw_;      // older than any holding set's blocks
+    int holding_ = -1;              // the set whose completed raw blocks are handed out in place
+    // Copy a holding set's blocks not yet handed out to raw_ and free the set for staging.
+    void spill(Set& s);
+    Error stageBlock(Set* s, BlockID id, const uint8_t* const* payloads, const size_t* lens, size_t biggest, bool refs,
+                     RepairQueue* q);
     struct Ready {                  // an encoded block whose frames wait for queue room
         RepairQueue* q;
         std::shared_ptr<QueueToken> tok;

@@ -18,6 +18,8 @@
  *   fec_go_encoder_submit       the same with the k payload pointers in one C array (Go 1.21
  *                               runtime.Pinner pins the payloads for the call; the array itself
  *                               must be C memory)
+ *   fec_go_encoder_submit_ref   the same by reference, for payloads in a registered pool
+ *                               (fec_go_pool_new): the device gathers them, no host copy
  *   fec_go_encoder_poll         the frames repairSymbols returns, for every completed block
  *   fec_go_decoder_add_*        block.addSourceSymbol / addRepairSymbol  block.go:56-85
  *   fec_go_decoder_commit       recoverSymbolPayloads for one recoverable block
@@ -63,6 +65,21 @@ int fec_go_encoder_commit(fec_go_encoder *e, uint64_t block_id);
 /* add x k + commit in one call; payloads[i] pinned by the caller for the call's duration. */
 int fec_go_encoder_submit(fec_go_encoder *e, uint64_t block_id, const uint8_t *const *payloads, const size_t *lens,
                           int count);
+/* Registered packet buffers (opt-in; buffer_pool.go:87 allocates each packet buffer as
+ * make([]byte, 0, protocol.MaxPacketBufferSize), and packet_packer.go:984 each source-symbol
+ * payload likewise): nbuf buffers of FEC_GO_POOL_SLOT bytes, back to back from *base, in pinned
+ * host memory mapped into the GPU's address space. Memory without Go pointers: Go slices it with
+ * unsafe.Slice. fec_go_pool_free stops new references at once; the memory is released when the
+ * last batch that reads it completes. */
+#define FEC_GO_POOL_SLOT 1456
+typedef struct fec_go_pool fec_go_pool;
+fec_go_pool *fec_go_pool_new(size_t nbuf, uint8_t **base, int *err);
+void fec_go_pool_free(fec_go_pool *p);
+/* fec_go_encoder_submit by reference: a payload lying in a pool is not copied; the device reads
+ * and frames it when the batch is coded, so the caller keeps it unchanged until poll returns
+ * block_id. Payloads elsewhere are copied now. Same checks and errors as fec_go_encoder_submit. */
+int fec_go_encoder_submit_ref(fec_go_encoder *e, uint64_t block_id, const uint8_t *const *payloads,
+                              const size_t *lens, int count);
 /* Start coding the staged blocks (asynchronous). */
 int fec_go_encoder_flush(fec_go_encoder *e);
 /* Completed blocks, in commit order, up to max_blocks: block_ids[d], repair_len[d] (= its

@@ -255,8 +255,15 @@ static int xor_recover_direct(fec_ctx *ctx, Case *c) {
 
 /* ---------------------------------------------------------------- batch_hip.go */
 
+/* batchref: the sender's packet-buffer pool (fec_go_pool_new; batch_hip.go PacketPool): source
+ * payloads are built in registered buffers and submitted by reference (SubmitRef) */
+static int g_ref;
+static fec_go_pool *g_pool;
+static uint8_t *g_pool_base;
+
 static int batch_repair(Case *c, int scheme) {
     int rc = 0;
+    if (g_ref && !g_pool && !(g_pool = fec_go_pool_new(2 * MAX_SYM, &g_pool_base, &rc))) return go_err(rc);
     /* NewBatchSender(id, k, m): XOR senders are (k, 1), manager.go:54-56 */
     fec_go_encoder *e = fec_go_encoder_new(scheme, c->k, scheme == FEC_SCHEME_XOR ? 1 : c->m, 64, 0, &rc);
     if (!e) return go_err(rc);
@@ -302,7 +309,14 @@ static int batch_repair(Case *c, int scheme) {
         fec_go_encoder_free(e);
         return fail("%s", bad);
     }
-    if ((rc = fec_go_encoder_submit(e, c->id, ptrs, lens, n))) {
+    if (g_ref)   /* the packer writes the frame straight into a pool buffer (packet_packer.go:984) */
+        for (int i = 0; i < n; ++i)
+            if (lens[i] <= FEC_GO_POOL_SLOT) {
+                uint8_t *buf = g_pool_base + (size_t)i * FEC_GO_POOL_SLOT;
+                memcpy(buf, ptrs[i], lens[i]);
+                ptrs[i] = buf;
+            }
+    if ((rc = g_ref ? fec_go_encoder_submit_ref(e, c->id, ptrs, lens, n) : fec_go_encoder_submit(e, c->id, ptrs, lens, n))) {
         fec_go_encoder_free(e);
         return go_err(rc);
     }
@@ -420,10 +434,11 @@ static int run_case(Case *c, int batch) {
 
 int main(int argc, char **argv) {
     if (argc != 3) {
-        fprintf(stderr, "usage: %s <fixture> direct|batch\n", argv[0]);
+        fprintf(stderr, "usage: %s <fixture> direct|batch|batchref\n", argv[0]);
         return 2;
     }
-    const int batch = !strcmp(argv[2], "batch");
+    g_ref = !strcmp(argv[2], "batchref");
+    const int batch = g_ref || !strcmp(argv[2], "batch");
     FILE *f = fopen(argv[1], "r");
     if (!f) {
         perror(argv[1]);
@@ -463,6 +478,7 @@ int main(int argc, char **argv) {
         }
     }
     fclose(f);
+    if (g_pool) fec_go_pool_free(g_pool);
     /* leave without running the HIP runtime's shared-library finalizers: under the host-ASan
      * build, ASan's interception of the HSA allocator trips a check in the runtime's teardown
      * (libamdhip64 __cxa_finalize), after all work is done and checked */

@@ -245,7 +245,9 @@ def test_block_and_manager_fields_exist_in_the_reference():
         for fld in re.findall(r"\bbS\.(\w+)", code):
             assert fld in bstat, "%s: bS.%s not in blockStatus (manager.go:35-39)" % (path, fld)
     bm = ours[os.path.join(GO, "batch_manager_hip.go")]
-    own = set(re.findall(r"func \(m \*batchManager\) (\w+)\(", bm)) | {"manager", "tx", "rx", "pending"}
+    own = set(re.findall(r"func \(m \*batchManager\) (\w+)\(", bm)) | _ref_struct_fields(
+        os.path.join(GO, "batch_manager_hip.go"), "batchManager")
+    assert {"manager", "tx", "rx", "pending", "pool", "held"} <= own
     for fld in re.findall(r"\bm\.(\w+)", bm):
         assert fld in own or fld in mgr, "batch_manager_hip.go: m.%s is neither its own nor manager.go's" % fld
 

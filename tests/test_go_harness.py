@@ -10,7 +10,9 @@ line (same checks, buffer layout, strides, present masks and FEC_HOST flags) and
     layer (oracle/oracle.py, restating reed_solomon.go / xor.go).
 
 `direct` mode = the per-block schemes (hipReedSolomonScheme / hipXorScheme); `batch` mode =
-BatchSender / BatchReceiver over include/fec_go.h. CPU: the harness compiles, links the library
+BatchSender / BatchReceiver over include/fec_go.h; `batchref` = the same with the sender's source
+payloads in a registered packet-buffer pool, submitted by reference (BatchSender.SubmitRef:
+gathered by the device). CPU: the harness compiles, links the library
 and the batch mode reports every validation error the reference reports with no device touched;
 GPU: every case, bit-exact, plus the reference's error texts in direct mode.
 """
@@ -189,14 +191,14 @@ def test_harness_builds_and_validates_without_device(harness, golden, oracle, fe
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["direct", "batch"])
+@pytest.mark.parametrize("mode", ["direct", "batch", "batchref"])
 def test_go_call_sequence_golden(harness, golden, oracle, mode, tmp_path):
     cases = _with_oracle_texts(_golden_cases(golden), oracle)
     _check(_run(harness, cases, mode, tmp_path), cases, texts=(mode == "direct"))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["direct", "batch"])
+@pytest.mark.parametrize("mode", ["direct", "batch", "batchref"])
 def test_go_call_sequence_synthetic(harness, oracle, mode, tmp_path):
     cases = _synthetic_cases(oracle)
     _check(_run(harness, cases, mode, tmp_path), cases, texts=(mode == "direct"))

@@ -345,8 +345,9 @@ def test_rs_encode_kernel_variants_match_oracle(codec, oracle, torch, variant, k
 # the worklist; RS(16,24) and RS(20,30) with shards of 64+ chunks, else as 1); 13 is 7 with the
 # RS(16,24) / RS(20,30) direct form too (coefficient rows by scalar loads from device memory);
 # 14 is 13 gated on the device (rs_classify_kernel picks the direct or the plan path per batch),
-# 15 the same with the threshold at 100 % (always the direct path and its worklist kernel)
-@pytest.mark.parametrize("wave", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
+# 15 the same with the threshold at 100 % (always the direct path and its worklist kernel); 16 is
+# 1 with the row-pipelined rolling rebuild (dec_fixk 3: RS(16,24) / RS(20,30), shards of 64+ chunks)
+@pytest.mark.parametrize("wave", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16])
 @pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10)])
 # L = 1008 / 1017: shards of 63 / 64 chunks, the edge of the two-block wave slices (rolling window)
 @pytest.mark.parametrize("L", [513, 1008, 1017, 1202, 1436])
@@ -369,7 +370,7 @@ def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, 
                            dec_direct=1 if wave in (7, 13, 14, 15) else 0,
                            dec_direct_big=1 if wave in (13, 14, 15) else 0, dec_gate=1 if wave in (14, 15) else 0,
                            dec_gate_pm=1000 if wave == 15 else 10,
-                           dec_sorted=0 if wave == 8 else 1, dec_fixk=1 if wave == 9 else 2,
+                           dec_sorted=0 if wave == 8 else 1, dec_fixk={9: 1, 16: 3}.get(wave, 2),
                            dec_tier={10: 1, 11: 2, 12: 4}.get(wave, 0))
     try:
         out = torch.full((B, m, S), 0xEE, dtype=torch.uint8, device="cuda")

@@ -65,6 +65,7 @@ def main():
         variants = {"default": D}
         variants["wave runtime k"] = dict(D, dec_fixk=0)
         variants["compile-time k, all k loads up front"] = dict(D, dec_fixk=1)
+        variants["rolling window + row-pipelined tables (fixk 3)"] = dict(D, dec_fixk=3)
         for w in (3, 4):
             variants["rolling window wpc%d" % w] = dict(D, dec_wpc=w)
         for w in (2, 3):

@@ -6,8 +6,12 @@
  * their own encoder and decoder over their own blocks, as T connection run loops would; the
  * rate is all blocks over the wall time of the slowest thread.
  *
- *   usage: go_batch_bench rs|xor k m blocks max_blocks [payload_len] [threads]
+ *   usage: go_batch_bench rs|xor k m blocks max_blocks [payload_len] [threads] [copy|ref]
  * prints one JSON line: encode and decode payload GB/s and blocks/s.
+ *
+ * ref: every source payload sits in a registered packet buffer (fec_go_pool_new, one buffer per
+ * payload, written before the timed region as the packer would write the frame into it) and is
+ * submitted with fec_go_encoder_submit_ref: the device gathers it, the host copies nothing in.
  */
 #define _GNU_SOURCE
 #include <pthread.h>
@@ -30,6 +34,7 @@ typedef struct {
     int scheme, k, m, nb;
     size_t maxb, len;
     const uint8_t *pay;     /* this thread's nb * k payloads */
+    int ref;                /* submit by reference from a registered pool */
     uint8_t *reps;          /* nb * m * FEC_GO_SLOT */
     pthread_barrier_t *bar;
     double te, td;
@@ -53,6 +58,18 @@ static void *run(void *arg) {
     if (!e || !d) {
         fprintf(stderr, "new: %d %s\n", rc, fec_last_error());
         j->fail = 1;
+    }
+    /* ref: the payloads, one per registered packet buffer */
+    fec_go_pool *pool = NULL;
+    uint8_t *pbase = NULL;
+    if (j->ref && !j->fail) {
+        pool = fec_go_pool_new((size_t)nb * k, &pbase, &rc);
+        if (!pool) {
+            fprintf(stderr, "pool: %d %s\n", rc, fec_last_error());
+            j->fail = 1;
+        } else {
+            for (size_t i = 0; i < (size_t)nb * k; ++i) memcpy(pbase + i * FEC_GO_POOL_SLOT, j->pay + i * len, len);
+        }
     }
     /* warm-up outside the timed region: the first submit of an encoder / decoder allocates its
      * pinned staging sets (tens of ms), which a connection pays once */
@@ -81,10 +98,11 @@ static void *run(void *arg) {
     int polled = 0;
     for (int b = 0; b < nb && !j->fail; ++b) {
         for (int i = 0; i < k; ++i) {
-            ptrs[i] = j->pay + ((size_t)b * k + i) * len;
+            ptrs[i] = j->ref ? pbase + ((size_t)b * k + i) * FEC_GO_POOL_SLOT : j->pay + ((size_t)b * k + i) * len;
             lens[i] = len;
         }
-        if (fec_go_encoder_submit(e, (uint64_t)b, ptrs, lens, k)) {
+        if (j->ref ? fec_go_encoder_submit_ref(e, (uint64_t)b, ptrs, lens, k)
+                   : fec_go_encoder_submit(e, (uint64_t)b, ptrs, lens, k)) {
             fprintf(stderr, "submit: %s\n", fec_last_error());
             j->fail = 1;
         }
@@ -141,8 +159,29 @@ static void *run(void *arg) {
     }
     j->td = now() - t0;
     if (done != (size_t)nb) j->fail = 1;
+    /* ref: the encoded repairs must equal the copy path's: spot-check block 0 and nb-1 against a
+       fresh copy-mode encode (the encode loop above already checked the decode round trip) */
+    if (j->ref && !j->fail) {
+        for (int b = 0; b < nb; b += nb - 1 > 0 ? nb - 1 : 1) {
+            for (int i = 0; i < k; ++i) {
+                ptrs[i] = j->pay + ((size_t)b * k + i) * len;
+                lens[i] = len;
+            }
+            size_t got = 0;
+            int same = !fec_go_encoder_submit(e, ~1ull, ptrs, lens, k) && !fec_go_encoder_poll(e, 1, ids, rl, rp, maxb, &got) &&
+                       got == 1;
+            for (int p = 0; same && p < m; ++p)
+                same = !memcmp(rp + (size_t)p * FEC_GO_SLOT, j->reps + ((size_t)b * m + p) * FEC_GO_SLOT, rl[0]);
+            if (!same) {
+                fprintf(stderr, "ref encode differs from copy encode at block %d\n", b);
+                j->fail = 1;
+            }
+            if (nb == 1) break;
+        }
+    }
     if (e) fec_go_encoder_free(e);
     if (d) fec_go_decoder_free(d);
+    if (pool) fec_go_pool_free(pool);
     free(ptrs), free(lens), free(ids), free(offs), free(rl), free(rp), free(out);
     return NULL;
 }
@@ -156,6 +195,7 @@ int main(int argc, char **argv) {
     const int k = atoi(argv[2]), m = xr ? 1 : atoi(argv[3]), nb = atoi(argv[4]);
     const size_t maxb = (size_t)atoi(argv[5]), len = argc > 6 ? (size_t)atoi(argv[6]) : 1200;
     const int T = argc > 7 ? atoi(argv[7]) : 1;
+    const int ref = argc > 8 && !strcmp(argv[8], "ref");
     const int per = nb / T;
     uint8_t *pay = malloc((size_t)T * per * k * len);
     uint64_t x = 0x0FEC;
@@ -171,7 +211,7 @@ int main(int argc, char **argv) {
         pthread_t *th = malloc((size_t)T * sizeof *th);
         for (int t = 0; t < T; ++t) {
             jobs[t] = (Job){xr ? FEC_SCHEME_XOR : FEC_SCHEME_REED_SOLOMON, k, m, per, maxb, len,
-                            pay + (size_t)t * per * k * len, malloc((size_t)per * m * FEC_GO_SLOT), &bar, 0, 0, 0};
+                            pay + (size_t)t * per * k * len, ref, calloc((size_t)per * m, FEC_GO_SLOT), &bar, 0, 0, 0};
             pthread_create(&th[t], NULL, run, &jobs[t]);
         }
         double te = 0, td = 0;
@@ -192,10 +232,10 @@ int main(int argc, char **argv) {
         best_d = td < best_d ? td : best_d;
     }
     const double blocks = (double)T * per, bytes = blocks * k * len;
-    printf("{\"scheme\": \"%s(%d,%d)\", \"host_threads\": %d, \"blocks\": %.0f, \"max_blocks\": %zu, "
+    printf("{\"scheme\": \"%s(%d,%d)\", \"submit\": \"%s\", \"host_threads\": %d, \"blocks\": %.0f, \"max_blocks\": %zu, "
            "\"payload_len\": %zu, \"encode_GBps\": %.3f, \"encode_blocks_per_s\": %.0f, \"decode_GBps\": %.3f, "
            "\"decode_blocks_per_s\": %.0f}\n",
-           xr ? "XOR" : "RS", k, xr ? 1 : k + m, T, blocks, maxb, len, bytes / best_e / 1e9, blocks / best_e,
+           xr ? "XOR" : "RS", k, xr ? 1 : k + m, ref ? "ref (registered pool, device gather)" : "copy", T, blocks, maxb, len, bytes / best_e / 1e9, blocks / best_e,
            bytes / best_d / 1e9, blocks / best_d);
     fflush(stdout);
     _exit(0);
