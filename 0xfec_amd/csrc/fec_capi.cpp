@@ -469,6 +469,7 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         a.sorted = sorted ? 1u : 0u;
         a.out = out ? out + b0 * out_bs : nullptr;
         a.out_bs = out_bs;
+        a.persist_ncu = gated ? (uint32_t)ctx->ncu : 0u;   // both paths persistent: the loser exits in one round
         if (direct) {
             a.masks = p.masks;
             a.status = p.status;

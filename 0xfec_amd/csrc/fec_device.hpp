@@ -29,12 +29,20 @@ __device__ __forceinline__ uint32_t rotate_chunk(uint32_t c, uint32_t cps, uint3
 // XCDs (MI355X_MICROARCH.md, workgroup dispatch); with swz the workgroups one XCD receives take
 // one contiguous eighth of the grid, so each XCD streams its own contiguous address range
 // (speed only: any bijection is correct). Workgroups past the last multiple of 8 keep their index.
-__device__ __forceinline__ uint32_t xcd_order(uint32_t swz) {
-    const uint32_t wg = blockIdx.x, G = gridDim.x;
+__device__ __forceinline__ uint32_t xcd_order_of(uint32_t wg, uint32_t G, uint32_t swz) {
     if (!swz) return wg;
     const uint32_t full = G & ~7u;
     if (wg >= full) return wg;
     return (wg & 7u) * (full >> 3) + (wg >> 3);
+}
+__device__ __forceinline__ uint32_t xcd_order(uint32_t swz) { return xcd_order_of(blockIdx.x, gridDim.x, swz); }
+
+// Workgroup wg of a virtual grid of G (a persistent grid walks wg = blockIdx.x, + gridDim.x, ...;
+// gridDim.x a multiple of 8 keeps every virtual workgroup on its physical one's XCD).
+template <class Body>
+__device__ __forceinline__ void for_virtual_blocks(uint32_t vgrid, Body body) {
+    const uint32_t G = vgrid ? vgrid : gridDim.x;
+    for (uint32_t wg = blockIdx.x; wg < G; wg += gridDim.x) body(wg, G);
 }
 
 struct Idx {

@@ -64,6 +64,16 @@ int resident_per_cu(const void* kernel, size_t lds) {
     return per;
 }
 
+int flat_or_persistent(ReconArgs* a, const void* kernel, size_t lds, int flat) {
+    a->vgrid = 0;
+    if (!a->persist_ncu || flat <= 8) return flat;
+    int g = resident_per_cu(kernel, lds) * (int)a->persist_ncu;
+    g = std::max(8, g & ~7);
+    if (g >= flat) return flat;
+    a->vgrid = (uint32_t)flat;
+    return g;
+}
+
 int occupancy_grid(int device, int which, uint32_t sel, size_t lds) {
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0)

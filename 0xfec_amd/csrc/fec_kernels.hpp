@@ -113,7 +113,17 @@ struct ReconArgs {
     uint32_t list_grid;        // workgroups of the persistent worklist kernels (tier B)
     const uint32_t* gate;      // nullable: run only when gate[0] == gate_want (rs_classify_kernel's pick)
     uint32_t gate_want;
+    // gated launches: the flat grid's workgroups as virtual ones [0, vgrid) walked by a persistent
+    // grid, so the path the classify kernel did not pick exits after one round of workgroups
+    // instead of dispatching the whole flat grid (0: flat launch)
+    uint32_t vgrid;
+    uint32_t persist_ncu;      // host side: nonzero asks the launcher for that persistent form (CUs)
 };
+
+// Launch geometry for a flat grid of `flat` workgroups of `kernel` (lds bytes each): the flat grid
+// (a->persist_ncu == 0), or the workgroups resident at once on persist_ncu CUs (a multiple of 8, at
+// most flat) walking it, with a->vgrid = flat.
+int flat_or_persistent(ReconArgs* a, const void* kernel, size_t lds, int flat);
 
 constexpr uint32_t kHardDone = 32, kHardList = 64;   // worklist words (own 128-byte lines)
 
@@ -164,8 +174,9 @@ struct Tuning {
                               // copied by a vector load); multi-erasure waves go to a worklist kernel
     int host_chunk = 0;       // host-resident path: blocks per staging chunk (0: 128 MiB worth)
     int dec_fixk = 2;         // RS(16,24) / RS(20,30) rebuild with k at compile time (1: all k loads in
-                              // flight; 2: RS(16,24) with a rolling window of 8 loaded inputs, shards of
-                              // 64+ chunks)
+                              // flight; 2: a rolling window of 8 loaded inputs, shards of 64+ chunks,
+                              // RS(20,30) also with the rows' table reads pipelined one row ahead;
+                              // 3: both codes pipelined)
     int dec_sorted = 1;       // multi-erasure codes (plan path, shards of 32+ chunks): sorted parallel plans
     int dec_ipl = 0;          // wave-form reconstruct items per lane: 1; 2 loaded together; 3: 2 one
                               // after the other (one plan stage); 0: 2 for k <= 4, else 1

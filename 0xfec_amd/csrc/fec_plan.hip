@@ -199,6 +199,7 @@ hipError_t sorted_launch(const PlanArgs& a, hipStream_t s) {
     // segments per workgroup (knob dec_pseg, 0: by batch size): enough workgroups to fill the
     // chip several times over, each staging the tables once for all its segments
     uint32_t segs = g_tune.dec_pseg > 0 ? (uint32_t)g_tune.dec_pseg : std::max<uint32_t>(1, nseg / 4096);
+    if (a.gate) segs = 64;   // gated: a small grid, cheap to exit when the direct path was picked
     segs = std::min<uint32_t>(segs, 64);
     const uint32_t grid = (nseg + segs - 1) / segs;
     const size_t lds = sort_lds(a.m, a.k, G, a.lay.stride).total;

@@ -62,194 +62,198 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
     constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     if (a.gate && *a.gate != a.gate_want) return;   // the classify kernel picked the plan path
-    const uint32_t k = K ? (uint32_t)K : a.k, m = a.m;
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    uint8_t* slice = smem + (size_t)wave * direct_wave_bytes(k);
-    const uint32_t total = a.nblocks * a.cps;
-    const uint32_t all = low_mask(k + m), kmask = low_mask(k);
-    // Statuses (recover: e rebuilt; in place: 0; failures as rs_plan_kernel reports them) and
-    // failure flags of blocks [64 w, 64 w + 64), w = this wave's launch index: one coalesced mask
-    // load and one coalesced status store per 64 blocks. (Stored by the waves of each block, the
-    // 4-byte statuses of neighbouring blocks were scattered partial-line stores from different
-    // waves: RS(2,3) 45 -> 57 us with a status array.)
-    {
-        const uint32_t w = blockIdx.x * (kThreads / 64) + wave;
-        if (w * 64u < a.nblocks) {   // wave-uniform
-            const uint32_t b = w * 64u + lane;
-            uint32_t bad = 0;
-            if (b < a.nblocks) {
-                const uint32_t mask = a.masks[b] & all;
-                const uint32_t e = k - __popc(mask & kmask);
-                int32_t st = a.max_out ? (int32_t)e : 0;
-                if (e != 0 && (uint32_t)__popc(mask) < k) {
-                    st = -4;   // FEC_ERR_TOO_FEW_SHARDS
-                    bad = 1;
-                } else if (a.max_out && e > a.max_out) {
-                    st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
-                    bad = 2;
+    // one flat workgroup per pass (vgrid 0), or the flat grid's workgroups walked by a persistent
+    // grid when gated (the losing path then exits after one round)
+    for_virtual_blocks(a.vgrid, [&](uint32_t vb, uint32_t G) {
+        const uint32_t k = K ? (uint32_t)K : a.k, m = a.m;
+        const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        uint8_t* slice = smem + (size_t)wave * direct_wave_bytes(k);
+        const uint32_t total = a.nblocks * a.cps;
+        const uint32_t all = low_mask(k + m), kmask = low_mask(k);
+        // Statuses (recover: e rebuilt; in place: 0; failures as rs_plan_kernel reports them) and
+        // failure flags of blocks [64 w, 64 w + 64), w = this wave's launch index: one coalesced mask
+        // load and one coalesced status store per 64 blocks. (Stored by the waves of each block, the
+        // 4-byte statuses of neighbouring blocks were scattered partial-line stores from different
+        // waves: RS(2,3) 45 -> 57 us with a status array.)
+        {
+            const uint32_t w = vb * (kThreads / 64) + wave;
+            if (w * 64u < a.nblocks) {   // wave-uniform
+                const uint32_t b = w * 64u + lane;
+                uint32_t bad = 0;
+                if (b < a.nblocks) {
+                    const uint32_t mask = a.masks[b] & all;
+                    const uint32_t e = k - __popc(mask & kmask);
+                    int32_t st = a.max_out ? (int32_t)e : 0;
+                    if (e != 0 && (uint32_t)__popc(mask) < k) {
+                        st = -4;   // FEC_ERR_TOO_FEW_SHARDS
+                        bad = 1;
+                    } else if (a.max_out && e > a.max_out) {
+                        st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
+                        bad = 2;
+                    }
+                    if (a.status) a.status[b] = st;
                 }
-                if (a.status) a.status[b] = st;
+                const bool f1 = __ballot(bad == 1) != 0, f2 = __ballot(bad == 2) != 0;
+                if (lane == 0 && (f1 || f2)) atomicOr(a.err, (f1 ? 1 : 0) | (f2 ? 2 : 0));
             }
-            const bool f1 = __ballot(bad == 1) != 0, f2 = __ballot(bad == 2) != 0;
-            if (lane == 0 && (f1 || f2)) atomicOr(a.err, (f1 ? 1 : 0) | (f2 ? 2 : 0));
         }
-    }
-    const uint32_t i0 = xcd_order(a.swz) * kThreads + (wave << 6);
-    if (i0 >= total) return;
-    const uint32_t bfirst = fdiv(i0, a.div_cps);
-    const uint32_t nb = fdiv(min(i0 + 63u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
-    const uint32_t mine = lane < nb ? a.masks[bfirst + lane] : 0u;   // the wave's masks in one load
+        const uint32_t i0 = xcd_order_of(vb, G, a.swz) * kThreads + (wave << 6);
+        if (i0 >= total) return;
+        const uint32_t bfirst = fdiv(i0, a.div_cps);
+        const uint32_t nb = fdiv(min(i0 + 63u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
+        const uint32_t mine = lane < nb ? a.masks[bfirst + lane] : 0u;   // the wave's masks in one load
 
-    // A block with two or more erasures (and enough shards) sends the whole wave to the
-    // worklist of rs_recover_hard_kernel.
-    bool hard = false;
-    for (uint32_t g = 0; g < nb; ++g) {
-        const uint32_t mask = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)g) & all;
-        const uint32_t e = k - __popc(mask & kmask);
-        if (e >= 2 && (uint32_t)__popc(mask) >= k && !(a.max_out && e > a.max_out)) hard = true;
-    }
-    if (hard) {
-        if (lane == 0) {
-            const uint32_t slot = atomicAdd(a.hard, 1u);
-            if (slot < a.hard_cap) a.hard[kHardList + slot] = i0;
-            else atomicOr(a.err, 4);   // never expected: the worklist holds one entry per wave
+        // A block with two or more erasures (and enough shards) sends the whole wave to the
+        // worklist of rs_recover_hard_kernel.
+        bool hard = false;
+        for (uint32_t g = 0; g < nb; ++g) {
+            const uint32_t mask = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)g) & all;
+            const uint32_t e = k - __popc(mask & kmask);
+            if (e >= 2 && (uint32_t)__popc(mask) >= k && !(a.max_out && e > a.max_out)) hard = true;
         }
-        return;
-    }
-    // Per block (uniform): the table row (E0 * m + R0) of a single-erasure block.
-    uint32_t row[kWaveBlocks] = {0, 0, 0};
-#pragma unroll
-    for (uint32_t g = 0; g < kWaveBlocks; ++g) {
-        if (g >= nb) break;
-        const uint32_t mask = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)g) & all;
-        const uint32_t e = k - __popc(mask & kmask);
-        if (e == 1 && (uint32_t)__popc(mask) >= k && !(a.max_out && e > a.max_out))
-            row[g] = (__ffs(~mask & kmask) - 1) * m + (__ffs(mask >> k) - 1);   // m >= 1 here: k < 32
-    }
-    // The PermTab rows of the wave's blocks into its LDS slice, prepared while the data loads are
-    // in flight (vector loads return in order: LDS writes that wait for a row load wait for that
-    // load only, and scalar loads are counted apart).
-    gf::PermTab* wt = reinterpret_cast<gf::PermTab*>(slice);
-    // TAB 0: pieces per lane: 3 blocks * 2k 16-byte pieces (<= 64 for k <= 10, the compile-time shapes)
-    constexpr int NT = (K > 0 && K <= 10) ? 1 : 3;
-    uint4 tv[NT];
-    if constexpr (TAB == 0) {
-        // unconditional loads (a lane past the wave's pieces re-reads a valid piece): no branch,
-        // so nothing makes the compiler wait for them before the data loads
-        const uint4* src = reinterpret_cast<const uint4*>(a.single);
-        const uint32_t np = nb * 2 * k;
-#pragma unroll
-        for (int q = 0; q < NT; ++q) {
-            const uint32_t t = min(lane + 64u * q, np - 1u);
-            const uint32_t g = t / (2 * k), r = t - g * 2 * k;
-            const uint32_t rw = g == 0 ? row[0] : g == 1 ? row[1] : row[2];
-            tv[q] = src[(size_t)rw * 2 * k + r];
-        }
-    }
-    // TAB 1: the rows' coefficient words by scalar loads (uniform addresses, constant cache), then
-    // lane l < nb*k expands coefficient j = l % k of block g = l / k into wt[l]
-    constexpr uint32_t KW = K > 0 ? (K + 3) / 4 : 8;   // coefficient dwords per row (k <= 32)
-    uint32_t cw[kWaveBlocks][KW];
-    if constexpr (TAB >= 1) {
-        // a kernel argument, or device memory read as constant: scalar loads either way
-        typedef __attribute__((address_space(4))) const uint32_t ConstU32;
-        ConstU32* ct = TAB == 1 ? (ConstU32*)cwords.w : (ConstU32*)a.single_coef;
-        const uint32_t kw = (k + 3) / 4;
-#pragma unroll
-        for (uint32_t g = 0; g < kWaveBlocks; ++g)
-#pragma unroll
-            for (uint32_t q = 0; q < KW; ++q) {
-                // the index is wave-uniform; readfirstlane makes that visible, so the load is scalar
-                const uint32_t at = (uint32_t)__builtin_amdgcn_readfirstlane((int)(row[g] * kw + q));
-                cw[g][q] = q < kw ? ct[at] : 0u;
+        if (hard) {
+            if (lane == 0) {
+                const uint32_t slot = atomicAdd(a.hard, 1u);
+                if (slot < a.hard_cap) a.hard[kHardList + slot] = i0;
+                else atomicOr(a.err, 4);   // never expected: the worklist holds one entry per wave
             }
-    }
-    auto expand_rows = [&]() {
-        for (uint32_t l = lane; l < nb * k; l += 64) {
-            const uint32_t lg = l / k, lj = l - lg * k;
-            uint32_t coef = 0;
-#pragma unroll
+            return;
+        }
+        // Per block (uniform): the table row (E0 * m + R0) of a single-erasure block.
+        uint32_t row[kWaveBlocks] = {0, 0, 0};
+    #pragma unroll
+        for (uint32_t g = 0; g < kWaveBlocks; ++g) {
+            if (g >= nb) break;
+            const uint32_t mask = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)g) & all;
+            const uint32_t e = k - __popc(mask & kmask);
+            if (e == 1 && (uint32_t)__popc(mask) >= k && !(a.max_out && e > a.max_out))
+                row[g] = (__ffs(~mask & kmask) - 1) * m + (__ffs(mask >> k) - 1);   // m >= 1 here: k < 32
+        }
+        // The PermTab rows of the wave's blocks into its LDS slice, prepared while the data loads are
+        // in flight (vector loads return in order: LDS writes that wait for a row load wait for that
+        // load only, and scalar loads are counted apart).
+        gf::PermTab* wt = reinterpret_cast<gf::PermTab*>(slice);
+        // TAB 0: pieces per lane: 3 blocks * 2k 16-byte pieces (<= 64 for k <= 10, the compile-time shapes)
+        constexpr int NT = (K > 0 && K <= 10) ? 1 : 3;
+        uint4 tv[NT];
+        if constexpr (TAB == 0) {
+            // unconditional loads (a lane past the wave's pieces re-reads a valid piece): no branch,
+            // so nothing makes the compiler wait for them before the data loads
+            const uint4* src = reinterpret_cast<const uint4*>(a.single);
+            const uint32_t np = nb * 2 * k;
+    #pragma unroll
+            for (int q = 0; q < NT; ++q) {
+                const uint32_t t = min(lane + 64u * q, np - 1u);
+                const uint32_t g = t / (2 * k), r = t - g * 2 * k;
+                const uint32_t rw = g == 0 ? row[0] : g == 1 ? row[1] : row[2];
+                tv[q] = src[(size_t)rw * 2 * k + r];
+            }
+        }
+        // TAB 1: the rows' coefficient words by scalar loads (uniform addresses, constant cache), then
+        // lane l < nb*k expands coefficient j = l % k of block g = l / k into wt[l]
+        constexpr uint32_t KW = K > 0 ? (K + 3) / 4 : 8;   // coefficient dwords per row (k <= 32)
+        uint32_t cw[kWaveBlocks][KW];
+        if constexpr (TAB >= 1) {
+            // a kernel argument, or device memory read as constant: scalar loads either way
+            typedef __attribute__((address_space(4))) const uint32_t ConstU32;
+            ConstU32* ct = TAB == 1 ? (ConstU32*)cwords.w : (ConstU32*)a.single_coef;
+            const uint32_t kw = (k + 3) / 4;
+    #pragma unroll
             for (uint32_t g = 0; g < kWaveBlocks; ++g)
-#pragma unroll
-                for (uint32_t q = 0; q < KW; ++q)
-                    if (lg == g && (lj >> 2) == q) coef = (cw[g][q] >> (8 * (lj & 3))) & 0xFFu;
-            wt[l] = gf::make_permtab((uint8_t)coef);   // the lane form measured 0-1 % slower here
+    #pragma unroll
+                for (uint32_t q = 0; q < KW; ++q) {
+                    // the index is wave-uniform; readfirstlane makes that visible, so the load is scalar
+                    const uint32_t at = (uint32_t)__builtin_amdgcn_readfirstlane((int)(row[g] * kw + q));
+                    cw[g][q] = q < kw ? ct[at] : 0u;
+                }
         }
-        wave_sync();
-    };
-    const uint32_t item = i0 + lane;
-    const bool inr = item < total;
-    const uint32_t blk = inr ? fdiv(item, a.div_cps) : bfirst;
-    const uint32_t g = blk - bfirst;
-    const uint32_t c = item - blk * a.cps;
-    const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 0);
-    const uint32_t m1 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 1);
-    const uint32_t m2 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 2);
-    const uint32_t mask = (g == 0 ? m0 : g == 1 ? m1 : m2) & all;
-    const bool work = inr && k - __popc(mask & kmask) == 1 && (uint32_t)__popc(mask) >= k;
-    const uint32_t E0 = __ffs(~mask & kmask) - 1;
-    const uint32_t R0 = work ? __ffs(mask >> k) - 1 : 0;
-    const gf::PermTab* T = wt + g * k;
-    const uint8_t* dblk = a.data + (uint64_t)blk * a.dbs + (uint64_t)c * kChunk;
-    const uint8_t* par = a.parity + (uint64_t)blk * a.pbs + (uint64_t)R0 * a.pss + (uint64_t)c * kChunk;
-    uint32_t acc[4] = {0, 0, 0, 0};
-    if constexpr (K > 0) {
-        // unconditional loads (a lane with nothing to rebuild reads one L2-resident table line
-        // instead): no branch around them, so the row pieces' LDS writes wait for the row loads
-        // only (vmcnt counts in order), not for the data
-        const uint8_t* idle = reinterpret_cast<const uint8_t*>(TAB == 2 ? a.single_coef : a.single);
-        const uint64_t ss = work ? a.ss : 0;
-        const uint8_t* d0 = work ? dblk : idle;
-        const uint8_t* p0 = work ? par : idle;
-        uint4 x[K];
-#pragma unroll
-        for (int j = 0; j < K - 1; ++j) x[j] = ld16<NTL>(d0 + (uint64_t)(j + (j >= (int)E0)) * ss);
-        x[K - 1] = ld16<NTL>(p0);
-        if constexpr (TAB == 0) rows_to_lds(wt, tv, lane, nb * 2 * k);
-        else expand_rows();
-        if (!work) return;
-#pragma unroll
-        for (int j = 0; j < K; j += 2) {
-            Idx ia[4], ib[4];
-            split4(ia, x[j]);
-            if (j + 1 < K) {
-                split4(ib, x[j + 1]);
-                mac2(acc, ia, ib, T + j, T + j + 1);
-            } else {
-                mac1(acc, ia, T + j);
+        auto expand_rows = [&]() {
+            for (uint32_t l = lane; l < nb * k; l += 64) {
+                const uint32_t lg = l / k, lj = l - lg * k;
+                uint32_t coef = 0;
+    #pragma unroll
+                for (uint32_t g = 0; g < kWaveBlocks; ++g)
+    #pragma unroll
+                    for (uint32_t q = 0; q < KW; ++q)
+                        if (lg == g && (lj >> 2) == q) coef = (cw[g][q] >> (8 * (lj & 3))) & 0xFFu;
+                wt[l] = gf::make_permtab((uint8_t)coef);   // the lane form measured 0-1 % slower here
             }
-        }
-    } else {
-        if constexpr (TAB == 0) rows_to_lds(wt, tv, lane, nb * 2 * k);
-        else expand_rows();
-        if (!work) return;
-        for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
-            uint4 x[kInGroup];
-#pragma unroll
-            for (int jj = 0; jj < kInGroup; ++jj) {
-                const uint32_t j = j0 + jj;
-                x[jj] = j + 1 < k ? ld16<NTL>(dblk + (uint64_t)(j + (j >= E0)) * a.ss)
-                                  : (j + 1 == k ? ld16<NTL>(par) : make_uint4(0, 0, 0, 0));
-            }
-#pragma unroll
-            for (int jj = 0; jj < kInGroup; jj += 2) {
-                const uint32_t j = j0 + jj;
-                if (j + 1 < k) {
-                    Idx ia[4], ib[4];
-                    split4(ia, x[jj]);
-                    split4(ib, x[jj + 1]);
+            wave_sync();
+        };
+        const uint32_t item = i0 + lane;
+        const bool inr = item < total;
+        const uint32_t blk = inr ? fdiv(item, a.div_cps) : bfirst;
+        const uint32_t g = blk - bfirst;
+        const uint32_t c = item - blk * a.cps;
+        const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 0);
+        const uint32_t m1 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 1);
+        const uint32_t m2 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 2);
+        const uint32_t mask = (g == 0 ? m0 : g == 1 ? m1 : m2) & all;
+        const bool work = inr && k - __popc(mask & kmask) == 1 && (uint32_t)__popc(mask) >= k;
+        const uint32_t E0 = __ffs(~mask & kmask) - 1;
+        const uint32_t R0 = work ? __ffs(mask >> k) - 1 : 0;
+        const gf::PermTab* T = wt + g * k;
+        const uint8_t* dblk = a.data + (uint64_t)blk * a.dbs + (uint64_t)c * kChunk;
+        const uint8_t* par = a.parity + (uint64_t)blk * a.pbs + (uint64_t)R0 * a.pss + (uint64_t)c * kChunk;
+        uint32_t acc[4] = {0, 0, 0, 0};
+        if constexpr (K > 0) {
+            // unconditional loads (a lane with nothing to rebuild reads one L2-resident table line
+            // instead): no branch around them, so the row pieces' LDS writes wait for the row loads
+            // only (vmcnt counts in order), not for the data
+            const uint8_t* idle = reinterpret_cast<const uint8_t*>(TAB == 2 ? a.single_coef : a.single);
+            const uint64_t ss = work ? a.ss : 0;
+            const uint8_t* d0 = work ? dblk : idle;
+            const uint8_t* p0 = work ? par : idle;
+            uint4 x[K];
+    #pragma unroll
+            for (int j = 0; j < K - 1; ++j) x[j] = ld16<NTL>(d0 + (uint64_t)(j + (j >= (int)E0)) * ss);
+            x[K - 1] = ld16<NTL>(p0);
+            if constexpr (TAB == 0) rows_to_lds(wt, tv, lane, nb * 2 * k);
+            else expand_rows();
+            if (!work) return;
+    #pragma unroll
+            for (int j = 0; j < K; j += 2) {
+                Idx ia[4], ib[4];
+                split4(ia, x[j]);
+                if (j + 1 < K) {
+                    split4(ib, x[j + 1]);
                     mac2(acc, ia, ib, T + j, T + j + 1);
-                } else if (j < k) {
-                    Idx ia[4];
-                    split4(ia, x[jj]);
+                } else {
                     mac1(acc, ia, T + j);
                 }
             }
+        } else {
+            if constexpr (TAB == 0) rows_to_lds(wt, tv, lane, nb * 2 * k);
+            else expand_rows();
+            if (!work) return;
+            for (uint32_t j0 = 0; j0 < k; j0 += kInGroup) {
+                uint4 x[kInGroup];
+    #pragma unroll
+                for (int jj = 0; jj < kInGroup; ++jj) {
+                    const uint32_t j = j0 + jj;
+                    x[jj] = j + 1 < k ? ld16<NTL>(dblk + (uint64_t)(j + (j >= E0)) * a.ss)
+                                      : (j + 1 == k ? ld16<NTL>(par) : make_uint4(0, 0, 0, 0));
+                }
+    #pragma unroll
+                for (int jj = 0; jj < kInGroup; jj += 2) {
+                    const uint32_t j = j0 + jj;
+                    if (j + 1 < k) {
+                        Idx ia[4], ib[4];
+                        split4(ia, x[jj]);
+                        split4(ib, x[jj + 1]);
+                        mac2(acc, ia, ib, T + j, T + j + 1);
+                    } else if (j < k) {
+                        Idx ia[4];
+                        split4(ia, x[jj]);
+                        mac1(acc, ia, T + j);
+                    }
+                }
+            }
         }
-    }
-    uint8_t* dst = a.out ? a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk
-                         : const_cast<uint8_t*>(dblk) + (uint64_t)E0 * a.ss;
-    store_chunk<NTS>(dst, as_uint4(acc), a.len - c * kChunk, a.pad_zero);
+        uint8_t* dst = a.out ? a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk
+                             : const_cast<uint8_t*>(dblk) + (uint64_t)E0 * a.ss;
+        store_chunk<NTS>(dst, as_uint4(acc), a.len - c * kChunk, a.pad_zero);
+    });
 }
 
 // Waves the direct kernel found holding a multi-erasure block (worklist a.hard: [0] count,
@@ -325,12 +329,14 @@ bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t stride)
 }
 
 template <int K, int POL, int TAB>
-static hipError_t direct_launch(const ReconArgs& a, const CoefWords& cw, hipStream_t s) {
-    const uint64_t total = (uint64_t)a.nblocks * a.cps;
-    const int grid = (int)((total + kThreads - 1) / kThreads);
-    if (grid == 0) return hipSuccess;
-    const int wpc = g_tune.dir_wpc >= 0 ? g_tune.dir_wpc : (a.k >= 8 ? 4 : 0);
-    const size_t lds = occupancy_lds(wpc, 4 * direct_wave_bytes(a.k));
+static hipError_t direct_launch(const ReconArgs& a0, const CoefWords& cw, hipStream_t s) {
+    const uint64_t total = (uint64_t)a0.nblocks * a0.cps;
+    const int flat = (int)((total + kThreads - 1) / kThreads);
+    if (flat == 0) return hipSuccess;
+    const int wpc = g_tune.dir_wpc >= 0 ? g_tune.dir_wpc : (a0.k >= 8 ? 4 : 0);
+    const size_t lds = occupancy_lds(wpc, 4 * direct_wave_bytes(a0.k));
+    ReconArgs a = a0;
+    const int grid = flat_or_persistent(&a, (const void*)rs_recover_direct_kernel<K, POL, TAB>, lds, flat);
     hipLaunchKernelGGL((rs_recover_direct_kernel<K, POL, TAB>), dim3(grid), dim3(kThreads), lds, s, a, cw);
     return hipGetLastError();
 }

@@ -346,7 +346,7 @@ def test_rs_encode_kernel_variants_match_oracle(codec, oracle, torch, variant, k
 # RS(16,24) / RS(20,30) direct form too (coefficient rows by scalar loads from device memory);
 # 14 is 13 gated on the device (rs_classify_kernel picks the direct or the plan path per batch),
 # 15 the same with the threshold at 100 % (always the direct path and its worklist kernel); 16 is
-# 1 with the row-pipelined rolling rebuild (dec_fixk 3: RS(16,24) / RS(20,30), shards of 64+ chunks)
+# 1 with the row-pipelined rolling rebuild for RS(16,24) too (dec_fixk 3; RS(20,30) has it by default)
 @pytest.mark.parametrize("wave", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16])
 @pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10)])
 # L = 1008 / 1017: shards of 63 / 64 chunks, the edge of the two-block wave slices (rolling window)
