@@ -393,12 +393,15 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
     const fk::PlanLayout lay0 = fk::plan_layout(k, maxe);
     // direct form: no plan kernel (single-erasure tables of the code; multi-erasure waves plan
     // in-wave), fec_recover.hip
-    const bool direct = code->d_single_coef && fk::direct_recon_applies(k, m, cps, lay0.stride);
+    // one output slot per block (recover into a buffer): the direct kernel alone is always right,
+    // for the big codes too (RS(20,30) single erasure +15 % over plan + rebuild, r03h)
+    const bool single_slot = out && out_slots == 1;
+    const bool direct = code->d_single_coef && fk::direct_recon_applies(k, m, cps, lay0.stride, single_slot);
     const bool sorted_ok = fk::g_tune.dec_sorted && !fk::g_tune.dec_fused && !fk::g_tune.dec_diag &&
                            fk::wave_recon_applies(cps, k, maxe, fk::plan_layout(k, maxe, true).stride);
     // both, gated on the device (RS(16,24), RS(20,30): their worklist path is slow, so a batch with
     // more than dec_gate_pm per mille of multi-erasure blocks takes the plan path instead)
-    const bool gated = direct && sorted_ok && fk::g_tune.dec_gate &&
+    const bool gated = direct && !single_slot && sorted_ok && fk::g_tune.dec_gate &&
                        (size_t)k * m * k * sizeof(gf::PermTab) > 16 * 1024;
     // sorted parallel plans for the plan + wave path (fec_plan.hip)
     const bool sorted = (gated || !direct) && sorted_ok;

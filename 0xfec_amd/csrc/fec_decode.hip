@@ -286,56 +286,41 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
     }
     gf::PermTab* tabs = reinterpret_cast<gf::PermTab*>(slice);             // WB*maxe*k
     uint8_t* plans = slice + (size_t)WB * maxe * k * sizeof(gf::PermTab);  // WB*stride
-    // one flat workgroup (vgrid 0), or the flat grid's workgroups walked by a persistent grid
-    // when gated (the losing path then exits after one round of workgroups)
-    for_virtual_blocks(a.vgrid, [&](uint32_t vb, uint32_t G) {
-        const uint32_t total = a.nblocks * a.cps;
-        constexpr uint32_t NI = IPL < 0 ? -IPL : IPL;   // items per lane; IPL < 0: one after the other
-        const uint32_t i0 = (xcd_order_of(vb, G, a.swz) * kThreads + (wave << 6)) * NI;
-        if (i0 >= total) return;
-        const uint32_t bfirst = fdiv(i0, a.div_cps);
-        const uint32_t nb = fdiv(min(i0 + 64u * NI - 1u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
-        if constexpr (!FUSED) {
-            const uint32_t nw = nb * lay.stride / 16;
-            const uint4* src = reinterpret_cast<const uint4*>(a.plans + (a.diag ? 0 : (uint64_t)bfirst * lay.stride));
-            if (lane < nw) reinterpret_cast<uint4*>(plans)[lane] = src[lane];
-        } else {
-            // the wave's (<= 3) masks in one load, then broadcast
-            const uint32_t mine = lane < nb ? a.masks[bfirst + lane] : 0u;
-            build_wave_plans(a, plans, bfirst, nb, lane, mine, s_exp, s_log, s_prows);
+    const uint32_t total = a.nblocks * a.cps;
+    constexpr uint32_t NI = IPL < 0 ? -IPL : IPL;   // items per lane; IPL < 0: one after the other
+    const uint32_t i0 = (xcd_order(a.swz) * kThreads + (wave << 6)) * NI;
+    if (i0 >= total) return;
+    const uint32_t bfirst = fdiv(i0, a.div_cps);
+    const uint32_t nb = fdiv(min(i0 + 64u * NI - 1u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
+    if constexpr (!FUSED) {
+        const uint32_t nw = nb * lay.stride / 16;
+        const uint4* src = reinterpret_cast<const uint4*>(a.plans + (a.diag ? 0 : (uint64_t)bfirst * lay.stride));
+        if (lane < nw) reinterpret_cast<uint4*>(plans)[lane] = src[lane];
+    } else {
+        // the wave's (<= 3) masks in one load, then broadcast
+        const uint32_t mine = lane < nb ? a.masks[bfirst + lane] : 0u;
+        build_wave_plans(a, plans, bfirst, nb, lane, mine, s_exp, s_log, s_prows);
+    }
+    wave_sync();
+    {
+        // expand only the rows the blocks rebuild: entry i of c0 + c1 + c2 (c_g = nout_g * k)
+        const uint32_t c0 = plans[lay.nout_off] * k;
+        const uint32_t c1 = nb > 1 ? plans[lay.stride + lay.nout_off] * k : 0u;
+        const uint32_t c2 = nb > 2 ? plans[2 * lay.stride + lay.nout_off] * k : 0u;
+        const uint32_t kk = K > 0 ? (uint32_t)K : k;   // compile-time k: the division is a shift
+        for (uint32_t i = lane; i < c0 + c1 + c2; i += 64) {
+            const uint32_t g = (i >= c0) + (i >= c0 + c1);
+            const uint32_t rem = i - (g == 0 ? 0u : g == 1 ? c0 : c0 + c1);
+            const uint32_t r = rem / kk, j = rem - r * kk;
+            const uint8_t* P = plans + g * lay.stride;
+            tabs[g * maxe * k + rem] = gf::make_permtab_fast(P[lay.coef_off + r * k + j]);
         }
-        wave_sync();
-        {
-            // expand only the rows the blocks rebuild: entry i of c0 + c1 + c2 (c_g = nout_g * k)
-            const uint32_t c0 = plans[lay.nout_off] * k;
-            const uint32_t c1 = nb > 1 ? plans[lay.stride + lay.nout_off] * k : 0u;
-            const uint32_t c2 = nb > 2 ? plans[2 * lay.stride + lay.nout_off] * k : 0u;
-            const uint32_t kk = K > 0 ? (uint32_t)K : k;   // compile-time k: the division is a shift
-            for (uint32_t i = lane; i < c0 + c1 + c2; i += 64) {
-                const uint32_t g = (i >= c0) + (i >= c0 + c1);
-                const uint32_t rem = i - (g == 0 ? 0u : g == 1 ? c0 : c0 + c1);
-                const uint32_t r = rem / kk, j = rem - r * kk;
-                const uint8_t* P = plans + g * lay.stride;
-                tabs[g * maxe * k + rem] = gf::make_permtab_fast(P[lay.coef_off + r * k + j]);
-            }
-        }
-        wave_sync();
-        if constexpr (IPL < 0) {
-            // the wave's items one 64-item run after the other, behind one plan stage
-            for (uint32_t u = 0; u < NI; ++u) {
-                const uint32_t item = i0 + u * 64 + lane;
-                const bool inr = item < total;
-                const uint32_t blk = inr ? fdiv(item, a.div_cps) : bfirst;
-                const uint32_t g = blk - bfirst;
-                const uint32_t c = item - blk * a.cps;
-                const uint8_t* P = plans + g * lay.stride;
-                const uint32_t nout = inr ? P[lay.nout_off] : 0;
-                const uint32_t rows = wave_rows<MAXE>(nout);
-                const uint32_t rb = a.sorted ? *reinterpret_cast<const uint32_t*>(P + lay.blk_off) : blk;
-                if (nout) recon_item<MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
-            }
-        } else if constexpr (IPL == 1) {
-            const uint32_t item = i0 + lane;
+    }
+    wave_sync();
+    if constexpr (IPL < 0) {
+        // the wave's items one 64-item run after the other, behind one plan stage
+        for (uint32_t u = 0; u < NI; ++u) {
+            const uint32_t item = i0 + u * 64 + lane;
             const bool inr = item < total;
             const uint32_t blk = inr ? fdiv(item, a.div_cps) : bfirst;
             const uint32_t g = blk - bfirst;
@@ -343,28 +328,39 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
             const uint8_t* P = plans + g * lay.stride;
             const uint32_t nout = inr ? P[lay.nout_off] : 0;
             const uint32_t rows = wave_rows<MAXE>(nout);
-            if (nout == 0) return;
             const uint32_t rb = a.sorted ? *reinterpret_cast<const uint32_t*>(P + lay.blk_off) : blk;
-            if constexpr (K > 0 && W > 0)
-                recon_item_roll<K, MAXE, W, NTL, NTS, RP>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
-            else if constexpr (K > 0) recon_item_k<K, MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
-            else recon_item<MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
-        } else {
-            const uint32_t itA = i0 + lane, itB = itA + 64;
-            const bool inA = itA < total, inB = itB < total;
-            const uint32_t bA = inA ? fdiv(itA, a.div_cps) : bfirst;
-            const uint32_t bB = inB ? fdiv(itB, a.div_cps) : bfirst;
-            const uint8_t* PA = plans + (bA - bfirst) * lay.stride;
-            const uint8_t* PB = plans + (bB - bfirst) * lay.stride;
-            const uint32_t nA = inA ? PA[lay.nout_off] : 0, nB = inB ? PB[lay.nout_off] : 0;
-            const uint32_t rA = wave_rows<MAXE>(nA), rB = wave_rows<MAXE>(nB);
-            if ((nA | nB) == 0) return;
-            const uint32_t rbA = a.sorted ? *reinterpret_cast<const uint32_t*>(PA + lay.blk_off) : bA;
-            const uint32_t rbB = a.sorted ? *reinterpret_cast<const uint32_t*>(PB + lay.blk_off) : bB;
-            recon_pair<MAXE, NTL, NTS>(a, PA, tabs + (bA - bfirst) * maxe * k, rbA, itA - bA * a.cps, rA, nA, PB,
-                                       tabs + (bB - bfirst) * maxe * k, rbB, itB - bB * a.cps, rB, nB);
+            if (nout) recon_item<MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
         }
-    });
+    } else if constexpr (IPL == 1) {
+        const uint32_t item = i0 + lane;
+        const bool inr = item < total;
+        const uint32_t blk = inr ? fdiv(item, a.div_cps) : bfirst;
+        const uint32_t g = blk - bfirst;
+        const uint32_t c = item - blk * a.cps;
+        const uint8_t* P = plans + g * lay.stride;
+        const uint32_t nout = inr ? P[lay.nout_off] : 0;
+        const uint32_t rows = wave_rows<MAXE>(nout);
+        if (nout == 0) return;
+        const uint32_t rb = a.sorted ? *reinterpret_cast<const uint32_t*>(P + lay.blk_off) : blk;
+        if constexpr (K > 0 && W > 0)
+            recon_item_roll<K, MAXE, W, NTL, NTS, RP>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
+        else if constexpr (K > 0) recon_item_k<K, MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
+        else recon_item<MAXE, NTL, NTS>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
+    } else {
+        const uint32_t itA = i0 + lane, itB = itA + 64;
+        const bool inA = itA < total, inB = itB < total;
+        const uint32_t bA = inA ? fdiv(itA, a.div_cps) : bfirst;
+        const uint32_t bB = inB ? fdiv(itB, a.div_cps) : bfirst;
+        const uint8_t* PA = plans + (bA - bfirst) * lay.stride;
+        const uint8_t* PB = plans + (bB - bfirst) * lay.stride;
+        const uint32_t nA = inA ? PA[lay.nout_off] : 0, nB = inB ? PB[lay.nout_off] : 0;
+        const uint32_t rA = wave_rows<MAXE>(nA), rB = wave_rows<MAXE>(nB);
+        if ((nA | nB) == 0) return;
+        const uint32_t rbA = a.sorted ? *reinterpret_cast<const uint32_t*>(PA + lay.blk_off) : bA;
+        const uint32_t rbB = a.sorted ? *reinterpret_cast<const uint32_t*>(PB + lay.blk_off) : bB;
+        recon_pair<MAXE, NTL, NTS>(a, PA, tabs + (bA - bfirst) * maxe * k, rbA, itA - bA * a.cps, rA, nA, PB,
+                                   tabs + (bB - bfirst) * maxe * k, rbB, itB - bB * a.cps, rB, nB);
+    }
 }
 
 // ------------------------------------------------------------------ tiered rebuild
@@ -555,13 +551,9 @@ static hipError_t recon_wave_dispatch(const ReconArgs& a, hipStream_t s) {
         // 4 instead of 3 workgroups per CU; RS(16,24) +1.7 % (dec_select.py, interleaved A/B)
         const bool roll = g_tune.dec_fixk == 2 && a.cps >= 64;
         const size_t lds2 = occupancy_lds(g_tune.dec_wpc, 4 * wave_slice_bytes(a.k, a.maxe, a.lay.stride, 2));
-        // gated launches (a.persist_ncu): a persistent grid walking the flat one
-#define FEC_K_LAUNCH(KERN, L)                                                           \
-    do {                                                                                \
-        ReconArgs b = a;                                                                \
-        const int g = flat_or_persistent(&b, (const void*)KERN, L, grid);               \
-        hipLaunchKernelGGL(KERN, dim3(g), dim3(kThreads), L, s, b);                      \
-    } while (0)
+        // (always flat: wrapped in a persistent loop for gated launches, these bodies lost their
+        // register allocation, K = 20 248 VGPRs + 408 B/lane of scratch, 3.5x slower, r03h)
+#define FEC_K_LAUNCH(KERN, L) hipLaunchKernelGGL(KERN, dim3(grid), dim3(kThreads), L, s, a)
         if (a.k == 16 && a.maxe == 8 && g_tune.dec_fixk) {
             if (roll && g_tune.dec_fixk == 3)   // 130 VGPRs, 3 waves/SIMD: -2.6 % here (r03f)
                 FEC_K_LAUNCH((rs_reconstruct_wave_kernel<8, POL, false, 1, 16, 8, true>), lds2);

@@ -244,7 +244,7 @@ bool tier_recon_applies(uint32_t k, uint32_t maxe, uint32_t cps);
 hipError_t launch_rs_reconstruct_tiered(const ReconArgs& a, hipStream_t s);
 hipError_t launch_rs_recover_fused(const ReconArgs& a, hipStream_t s);
 // Direct form (fec_recover.hip): applies when the single-erasure tables of (k, m) fit in LDS.
-bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t stride);
+bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t stride, bool single_slot);
 size_t direct_table_words(uint32_t k, uint32_t m);
 hipError_t launch_rs_recover_direct(const ReconArgs& a, int ncu, hipStream_t s);
 // Pick the decode path of a batch on the device (fec_recover.hip): gate[0] = 1 (direct: at most

@@ -57,14 +57,15 @@ struct CoefWords {
 // read from the code's coefficient table in device memory (a.single_coef, through the constant
 // address space: scalar loads), for codes whose rows do not fit the argument (RS(20,30): 1000
 // dwords).
-template <int K, int POL, int TAB>
+template <int K, int POL, int TAB, bool PERSIST = false>
 __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a, CoefWords cwords) {
     constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     if (a.gate && *a.gate != a.gate_want) return;   // the classify kernel picked the plan path
-    // one flat workgroup per pass (vgrid 0), or the flat grid's workgroups walked by a persistent
-    // grid when gated (the losing path then exits after one round)
-    for_virtual_blocks(a.vgrid, [&](uint32_t vb, uint32_t G) {
+    // one flat workgroup, or (PERSIST: gated launches) the flat grid's workgroups walked by a
+    // persistent grid, so the losing path exits after one round (a separate instance: the loop
+    // costs the flat bodies registers, RS(8,12) 67 -> 76 VGPRs)
+    auto body = [&](uint32_t vb, uint32_t G) {
         const uint32_t k = K ? (uint32_t)K : a.k, m = a.m;
         const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
         uint8_t* slice = smem + (size_t)wave * direct_wave_bytes(k);
@@ -253,7 +254,9 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
         uint8_t* dst = a.out ? a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk
                              : const_cast<uint8_t*>(dblk) + (uint64_t)E0 * a.ss;
         store_chunk<NTS>(dst, as_uint4(acc), a.len - c * kChunk, a.pad_zero);
-    });
+    };
+    if constexpr (PERSIST) for_virtual_blocks(a.vgrid, body);
+    else body(blockIdx.x, gridDim.x);
 }
 
 // Waves the direct kernel found holding a multi-erasure block (worklist a.hard: [0] count,
@@ -319,11 +322,15 @@ __global__ __launch_bounds__(kThreads) void rs_recover_hard_kernel(ReconArgs a) 
 
 size_t direct_table_words(uint32_t k, uint32_t m) { return (size_t)k * m * k * 8; }
 
-bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t stride) {
+bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t stride, bool single_slot) {
     if (!g_tune.dec_direct || m == 0 || k + m > 32 || cps < 32) return false;
-    // small codes (their PermTab table fits), or RS(20,30) with its rows read from device memory
+    // small codes (their PermTab table fits), or RS(20,30) / RS(16,24) with their rows read from
+    // device memory: when the caller gave one output slot per block (no block can need the
+    // multi-erasure worklist: two or more erasures are an error the kernel reports itself), or
+    // by the knob (gated or not)
     const bool small = (size_t)k * m * k * sizeof(gf::PermTab) <= kDirectTableBytes;
-    if (!small && !(((k == 20 && m == 10) || (k == 16 && m == 8)) && g_tune.dec_direct_big)) return false;
+    const bool big = (k == 20 && m == 10) || (k == 16 && m == 8);
+    if (!small && !(big && (single_slot || g_tune.dec_direct_big))) return false;
     const uint32_t maxe = std::max<uint32_t>(1, std::min(k, m));
     return 4 * hard_wave_bytes(m, k, maxe, stride) <= g_max_lds;
 }
@@ -335,9 +342,15 @@ static hipError_t direct_launch(const ReconArgs& a0, const CoefWords& cw, hipStr
     if (flat == 0) return hipSuccess;
     const int wpc = g_tune.dir_wpc >= 0 ? g_tune.dir_wpc : (a0.k >= 8 ? 4 : 0);
     const size_t lds = occupancy_lds(wpc, 4 * direct_wave_bytes(a0.k));
-    ReconArgs a = a0;
-    const int grid = flat_or_persistent(&a, (const void*)rs_recover_direct_kernel<K, POL, TAB>, lds, flat);
-    hipLaunchKernelGGL((rs_recover_direct_kernel<K, POL, TAB>), dim3(grid), dim3(kThreads), lds, s, a, cw);
+    if constexpr (TAB == 2) {   // the gated big codes: the persistent instance when asked
+        if (a0.persist_ncu) {
+            ReconArgs a = a0;
+            const int grid = flat_or_persistent(&a, (const void*)rs_recover_direct_kernel<K, POL, TAB, true>, lds, flat);
+            hipLaunchKernelGGL((rs_recover_direct_kernel<K, POL, TAB, true>), dim3(grid), dim3(kThreads), lds, s, a, cw);
+            return hipGetLastError();
+        }
+    }
+    hipLaunchKernelGGL((rs_recover_direct_kernel<K, POL, TAB>), dim3(flat), dim3(kThreads), lds, s, a0, cw);
     return hipGetLastError();
 }
 

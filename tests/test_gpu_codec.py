@@ -420,6 +420,52 @@ def test_rs_32_0_fully_present_is_untouched(codec, torch, fec):
     assert np.array_equal(data.cpu().numpy(), data_np)
 
 
+@pytest.mark.parametrize("k,m", [(16, 8), (20, 10)])
+@pytest.mark.parametrize("L", [1017, 1202])
+def test_rs_recover_single_slot_big_codes(codec, oracle, torch, fec, k, m, L):
+    """fec_rs_recover_batch with one output slot on RS(16,24) / RS(20,30) runs the direct kernel
+    (rows by scalar loads from the device table) with no gate: blocks with one erased data shard
+    are rebuilt bit-exact against the oracle, complete blocks report 0 and leave the slot alone,
+    blocks with two or more erased data shards report FEC_ERR_INVALID_ARG (more erasures than
+    output slots, as the plan path reports them), too-few-shards blocks FEC_ERR_TOO_FEW_SHARDS."""
+    rng = np.random.default_rng(7 * k + L)
+    n, B = k + m, 611
+    S = (L + 15) // 16 * 16
+    sh = _rand_shards(rng, B, n, S, L)
+    oracle.rs_encode(k, m, sh)
+    kind = rng.integers(0, 10, B)            # 0-5 single data erasure (+ parity losses), 6 none, 7-8 multi, 9 too few
+    masks = np.empty(B, dtype=np.uint32)
+    for b in range(B):
+        lost = set()
+        if kind[b] <= 5:
+            lost = {int(rng.integers(0, k))} | set(int(x) for x in rng.choice(np.arange(k, n), int(kind[b] % 3), replace=False))
+        elif kind[b] in (7, 8):
+            lost = set(int(x) for x in rng.choice(k, int(rng.integers(2, min(k, m) + 1)), replace=False))
+        elif kind[b] == 9:
+            lost = set(int(x) for x in rng.choice(n, m + 1, replace=False)) | {0}
+        masks[b] = ((1 << n) - 1) & ~sum(1 << i for i in lost)
+    data = torch.from_numpy(np.ascontiguousarray(sh[:, :k])).cuda()
+    par = torch.from_numpy(np.ascontiguousarray(sh[:, k:])).cuda()
+    out = torch.full((B, 1, S), 0xEE, dtype=torch.uint8, device="cuda")
+    st = torch.full((B,), 99, dtype=torch.int32, device="cuda")
+    dm = torch.from_numpy(masks.view(np.int32)).cuda()
+    codec.rs_recover_split(k, m, data, par, dm, out, status=st, shard_len=L)
+    rc = codec.lib_sync_rc()
+    got, sts = out.cpu().numpy(), st.cpu().numpy()
+    for b in range(B):
+        erased = [i for i in range(k) if not (masks[b] >> i) & 1]
+        present = bin(int(masks[b])).count("1")
+        if erased and present < k:
+            assert sts[b] == fec.FEC_ERR_TOO_FEW_SHARDS, b
+        elif len(erased) >= 2:
+            assert sts[b] == fec.FEC_ERR_INVALID_ARG, b
+        elif len(erased) == 1:
+            assert sts[b] == 1 and np.array_equal(got[b, 0, :L], sh[b, erased[0], :L]), b
+        else:
+            assert sts[b] == 0 and (got[b] == 0xEE).all(), b
+    assert rc != 0   # the batch held failing blocks: the sticky error says so
+
+
 @pytest.mark.parametrize("pinned", [False, True])
 @pytest.mark.parametrize("chunk", [0, 7])
 @pytest.mark.parametrize("k,m,L", [(2, 1, 1202), (8, 4, 1202), (16, 8, 700), (20, 10, 1436), (8, 4, 33)])
