@@ -340,7 +340,9 @@ static hipError_t direct_launch(const ReconArgs& a0, const CoefWords& cw, hipStr
     const uint64_t total = (uint64_t)a0.nblocks * a0.cps;
     const int flat = (int)((total + kThreads - 1) / kThreads);
     if (flat == 0) return hipSuccess;
-    const int wpc = g_tune.dir_wpc >= 0 ? g_tune.dir_wpc : (a0.k >= 8 ? 4 : 0);
+    // residency by shape: RS(8,12) 4 workgroups/CU (+3.6 %), RS(16,24) / RS(20,30) 3 (+1 %, r03i),
+    // small codes uncapped
+    const int wpc = g_tune.dir_wpc >= 0 ? g_tune.dir_wpc : (a0.k >= 16 ? 3 : a0.k >= 8 ? 4 : 0);
     const size_t lds = occupancy_lds(wpc, 4 * direct_wave_bytes(a0.k));
     if constexpr (TAB == 2) {   // the gated big codes: the persistent instance when asked
         if (a0.persist_ncu) {
