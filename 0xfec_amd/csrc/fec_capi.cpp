@@ -510,7 +510,8 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
             continue;
         }
         if (wave) {
-            HIP_TRY(fk::launch_rs_reconstruct_wave(a, ctx->stream));
+            if (fk::rebuild_k_applies(k, maxe, cps)) HIP_TRY(fk::launch_rs_rebuild_k(a, ctx->stream));
+            else HIP_TRY(fk::launch_rs_reconstruct_wave(a, ctx->stream));
             continue;
         }
         int grid;
@@ -1110,7 +1111,7 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 30 ? &fk::g_tune.enc_bits : key == 31 ? &fk::g_tune.enc_bwpc
               : key == 32 ? &fk::g_tune.dec_tier : key == 33 ? &fk::g_tune.dec_direct_big
               : key == 34 ? &fk::g_tune.dec_gate : key == 35 ? &fk::g_tune.dec_gate_pm
-              : key == 36 ? &fk::g_tune.host_gather : nullptr;
+              : key == 36 ? &fk::g_tune.host_gather : key == 37 ? &fk::g_tune.dec_win : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

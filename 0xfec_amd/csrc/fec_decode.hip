@@ -549,7 +549,8 @@ static hipError_t recon_wave_dispatch(const ReconArgs& a, hipStream_t s) {
     if constexpr (IPL == 1 && !FUSED) {
         // rolling load window (dec_fixk 2): 120 instead of 163 VGPRs and 2-block wave slices, so
         // 4 instead of 3 workgroups per CU; RS(16,24) +1.7 % (dec_select.py, interleaved A/B)
-        const bool roll = g_tune.dec_fixk == 2 && a.cps >= 64;
+        // (dec_fixk 4, fec_rebuild.hip, falls back here for plain loads / stores: the window form)
+        const bool roll = (g_tune.dec_fixk == 2 || g_tune.dec_fixk == 4) && a.cps >= 64;
         const size_t lds2 = occupancy_lds(g_tune.dec_wpc, 4 * wave_slice_bytes(a.k, a.maxe, a.lay.stride, 2));
         // (always flat: wrapped in a persistent loop for gated launches, these bodies lost their
         // register allocation, K = 20 248 VGPRs + 408 B/lane of scratch, 3.5x slower, r03h)

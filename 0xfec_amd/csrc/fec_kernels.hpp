@@ -173,10 +173,11 @@ struct Tuning {
                               // lookup (1: rows expanded from scalar-loaded coefficients, 2: PermTab rows
                               // copied by a vector load); multi-erasure waves go to a worklist kernel
     int host_chunk = 0;       // host-resident path: blocks per staging chunk (0: 128 MiB worth)
-    int dec_fixk = 2;         // RS(16,24) / RS(20,30) rebuild with k at compile time (1: all k loads in
+    int dec_fixk = 4;         // RS(16,24) / RS(20,30) rebuild with k at compile time (1: all k loads in
                               // flight; 2: a rolling window of 8 loaded inputs, shards of 64+ chunks,
                               // RS(20,30) also with the rows' table reads pipelined one row ahead;
-                              // 3: both codes pipelined)
+                              // 3: both codes pipelined; 4: fec_rebuild.hip, PermTab rows copied from a
+                              // workgroup table and input addresses as per-block offsets)
     int dec_sorted = 1;       // multi-erasure codes (plan path, shards of 32+ chunks): sorted parallel plans
     int dec_ipl = 0;          // wave-form reconstruct items per lane: 1; 2 loaded together; 3: 2 one
                               // after the other (one plan stage); 0: 2 for k <= 4, else 1
@@ -198,6 +199,8 @@ struct Tuning {
     int dec_gate_pm = 10;     // multi-erasure blocks (per mille) above which the plan path is taken
     int dec_tier = 0;         // RS(16,24) / RS(20,30) rebuild in two tiers: waves of <= dec_tier rows
                               // (1, 2 or 4) in a small-register launch, the rest from a worklist (0: off)
+    int dec_win = 0;          // fec_rebuild.hip: loads in flight per lane (4, 6, 8; 0: by code, RS(16,24) 4,
+                              // RS(20,30) 6: 125 instead of 137 VGPRs, 4 instead of 3 waves/SIMD)
     int host_gather = 1;      // FEC_HOST_PINNED reconstruct: the parity planes each block reads are pulled by
                               // the device straight from the caller's pinned buffer (0: whole span by DMA)
 };
@@ -242,6 +245,10 @@ hipError_t launch_rs_reconstruct_wave(const ReconArgs& a, hipStream_t s);
 // a.err / a.list_grid.
 bool tier_recon_applies(uint32_t k, uint32_t maxe, uint32_t cps);
 hipError_t launch_rs_reconstruct_tiered(const ReconArgs& a, hipStream_t s);
+// Compile-time-k rebuild of RS(16,24) / RS(20,30) with table-copied PermTab rows and per-block input
+// offsets (fec_rebuild.hip), for the wave form's shapes with shards of 64+ chunks.
+bool rebuild_k_applies(uint32_t k, uint32_t maxe, uint32_t cps);
+hipError_t launch_rs_rebuild_k(const ReconArgs& a, hipStream_t s);
 hipError_t launch_rs_recover_fused(const ReconArgs& a, hipStream_t s);
 // Direct form (fec_recover.hip): applies when the single-erasure tables of (k, m) fit in LDS.
 bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t stride, bool single_slot);

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--tiers", action="store_true", help="A/B the two-tier rebuild (knob dec_tier) only")
     ap.add_argument("--multi", type=int, default=0,
                     help="e ~ U{1..multi} erasures uniform over all n shards (config_bench's RS(16,24) mix)")
+    ap.add_argument("--only", default="", help="comma-separated substrings: keep the variants naming one (and the default)")
     args = ap.parse_args()
     import torch
     fec = importlib.import_module("0xfec_amd")
@@ -51,7 +52,7 @@ def main():
     dp, pp, op = data.data_ptr(), par.data_ptr(), out.data_ptr()
     # every knob any variant sets, at its default: tune(D) must undo each variant completely
     D = dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=1, dec_ipl=0, dec_direct=1, dec_nt=3, dir_wpc=-1, dir_nt=-1,
-             dec_fixk=2, dec_sorted=1, dec_pseg=0, dec_tier=0, dec_direct_big=0, dec_gate=0, dec_gate_pm=10)
+             dec_fixk=4, dec_sorted=1, dec_pseg=0, dec_tier=0, dec_direct_big=0, dec_gate=0, dec_gate_pm=10, dec_win=0)
     variants = {"direct (default)": D,
                 "direct, PermTab rows by vector load": dict(D, dec_direct=2),
                 "direct noswz": dict(D, dec_swz=0),
@@ -65,7 +66,11 @@ def main():
         variants = {"default": D}
         variants["wave runtime k"] = dict(D, dec_fixk=0)
         variants["compile-time k, all k loads up front"] = dict(D, dec_fixk=1)
+        variants["rolling window (fixk 2, round-2 default)"] = dict(D, dec_fixk=2)
         variants["rolling window + row-pipelined tables (fixk 3)"] = dict(D, dec_fixk=3)
+        variants["table-copy rebuild (fixk 4)"] = dict(D, dec_fixk=4)
+        for w in (4, 6, 8):
+            variants["table-copy rebuild (fixk 4) window %d" % w] = dict(D, dec_fixk=4, dec_win=w)
         for w in (3, 4):
             variants["rolling window wpc%d" % w] = dict(D, dec_wpc=w)
         for w in (2, 3):
@@ -82,6 +87,9 @@ def main():
             for w in (0, 4, 3):
                 variants["direct_big wpc%d" % w] = dict(D, dec_direct_big=1, dir_wpc=w)
                 variants["gated wpc%d" % w] = dict(D, dec_direct_big=1, dec_gate=1, dir_wpc=w)
+    if args.only:
+        keys = [x for x in args.only.split(",") if x]
+        variants = {n: kv for n, kv in variants.items() if kv is D or any(x in n for x in keys)}
     base = codec.set_tuning(**D)
     use_status = [False]
 
