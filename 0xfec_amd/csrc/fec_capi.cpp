@@ -1111,7 +1111,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 30 ? &fk::g_tune.enc_bits : key == 31 ? &fk::g_tune.enc_bwpc
               : key == 32 ? &fk::g_tune.dec_tier : key == 33 ? &fk::g_tune.dec_direct_big
               : key == 34 ? &fk::g_tune.dec_gate : key == 35 ? &fk::g_tune.dec_gate_pm
-              : key == 36 ? &fk::g_tune.host_gather : key == 37 ? &fk::g_tune.dec_win : nullptr;
+              : key == 36 ? &fk::g_tune.host_gather : key == 37 ? &fk::g_tune.dec_win
+              : key == 38 ? &fk::g_tune.dec_s64 : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

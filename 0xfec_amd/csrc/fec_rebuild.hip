@@ -68,6 +68,24 @@ struct Slice {
     __host__ __device__ static size_t bytes(uint32_t stride) { return plans + (size_t)WB * stride; }
 };
 
+// split4 with the two shifted forms of a dword pair made by one 64-bit shift each: (hi:lo) >> 3
+// moves three bits of hi into the top of lo, which the 0x07070707 mask clears again (and >> 6
+// likewise under 0x03030303), so 4 dwords take 4 instead of 8 shifts.
+__device__ __forceinline__ void split4w(Idx (&ix)[4], const uint4& x) {
+    const uint64_t w0 = ((uint64_t)x.y << 32) | x.x, w1 = ((uint64_t)x.w << 32) | x.z;
+    // as asm: left to itself the compiler sees that only masked bits are used and splits each
+    // 64-bit shift back into two 32-bit ones
+    uint64_t a3, b3, a6, b6;
+    asm("v_lshrrev_b64 %0, 3, %1" : "=v"(a3) : "v"(w0));
+    asm("v_lshrrev_b64 %0, 3, %1" : "=v"(b3) : "v"(w1));
+    asm("v_lshrrev_b64 %0, 6, %1" : "=v"(a6) : "v"(w0));
+    asm("v_lshrrev_b64 %0, 6, %1" : "=v"(b6) : "v"(w1));
+    ix[0] = {x.x & 0x07070707u, (uint32_t)a3 & 0x07070707u, (uint32_t)a6 & 0x03030303u};
+    ix[1] = {x.y & 0x07070707u, (uint32_t)(a3 >> 32) & 0x07070707u, (uint32_t)(a6 >> 32) & 0x03030303u};
+    ix[2] = {x.z & 0x07070707u, (uint32_t)b3 & 0x07070707u, (uint32_t)b6 & 0x03030303u};
+    ix[3] = {x.w & 0x07070707u, (uint32_t)(b3 >> 32) & 0x07070707u, (uint32_t)(b6 >> 32) & 0x03030303u};
+}
+
 // acc ^= c_a x_a ^ c_b x_b (one 16-byte chunk), c by its split PermTab words.
 __device__ __forceinline__ void mac2s(uint32_t (&acc)[4], const Idx (&ia)[4], const Idx (&ib)[4], const uint4& la,
                                       uint32_t a2, const uint4& lb, uint32_t b2) {
@@ -116,7 +134,7 @@ __device__ __forceinline__ void pair_rows(uint32_t (&acc)[ROWS][4], const Idx (&
 
 // One item's ROWS rebuilt chunks: the K inputs at dbase + offs[j] through a rolling window of W
 // loads (each folded pair's registers take the loads of the pair W inputs ahead).
-template <int K, int ROWS, int W, bool NTL, bool NTS, bool RP>
+template <int K, int ROWS, int W, bool NTL, bool NTS, bool RP, bool S64>
 __device__ __forceinline__ void rebuild_rows(const ReconArgs& a, const uint8_t* out_idx, const uint4* T01,
                                              const uint32_t* T2, const uint64_t* offs, uint8_t* dbase,
                                              uint8_t* obase, uint32_t c, uint32_t nout) {
@@ -146,8 +164,13 @@ __device__ __forceinline__ void rebuild_rows(const ReconArgs& a, const uint8_t* 
         const uint4 xa = x[j], xb = x[j + 1];
         __builtin_amdgcn_sched_barrier(0);
         Idx ia[4], ib[4];
-        split4(ia, xa);
-        split4(ib, xb);
+        if constexpr (S64) {
+            split4w(ia, xa);
+            split4w(ib, xb);
+        } else {
+            split4(ia, xa);
+            split4(ib, xb);
+        }
         if (j + W < K) load2(j + W, x[j + W], x[j + W + 1]);
         pair_rows<K, ROWS, RP>(acc, ia, ib, t01, t2, j);
     }
@@ -161,7 +184,7 @@ __device__ __forceinline__ void rebuild_rows(const ReconArgs& a, const uint8_t* 
 
 // Flat grid, one wave per 64 consecutive items of the (sorted) plan order; R: the code's largest
 // rebuilt row count (min(k, m)).
-template <int K, int R, int W, int POL, bool RP>
+template <int K, int R, int W, int POL, bool RP, bool S64>
 __global__ __launch_bounds__(kThreads) void rs_rebuild_k_kernel(ReconArgs a) {
     constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     using S = Slice<K, R>;
@@ -241,7 +264,7 @@ __global__ __launch_bounds__(kThreads) void rs_rebuild_k_kernel(ReconArgs a) {
     const uint64_t* O = offs + g * K;
     const uint8_t* oi = P + lay.out_off;
     static_assert(R <= 10, "row bodies 1..10");
-#define FEC_RB_ROWS(N) rebuild_rows<K, N, W, NTL, NTS, RP>(a, oi, T01, T2, O, dbase, obase, c, nout)
+#define FEC_RB_ROWS(N) rebuild_rows<K, N, W, NTL, NTS, RP, S64>(a, oi, T01, T2, O, dbase, obase, c, nout)
     switch (rows) {   // wave-uniform
         case 1: FEC_RB_ROWS(1); break;
         case 2: if constexpr (R >= 2) FEC_RB_ROWS(2); break;
@@ -264,9 +287,16 @@ hipError_t rebuild_launch(const ReconArgs& a, int w, hipStream_t s) {
     const int grid = (int)((total + kThreads - 1) / kThreads);
     if (grid == 0) return hipSuccess;
     const size_t lds = occupancy_lds(g_tune.dec_wpc, kTabLds + 4 * Slice<K, R>::bytes(a.lay.stride));
-    if (w == 4) hipLaunchKernelGGL((rs_rebuild_k_kernel<K, R, 4, 3, RP>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (w == 6) hipLaunchKernelGGL((rs_rebuild_k_kernel<K, R, 6, 3, RP>), dim3(grid), dim3(kThreads), lds, s, a);
-    else hipLaunchKernelGGL((rs_rebuild_k_kernel<K, R, 8, 3, RP>), dim3(grid), dim3(kThreads), lds, s, a);
+#define FEC_RB_LAUNCH(WW, S) \
+    hipLaunchKernelGGL((rs_rebuild_k_kernel<K, R, WW, 3, RP, S>), dim3(grid), dim3(kThreads), lds, s, a)
+    const bool s64 = g_tune.dec_s64 != 0;
+    if (w == 4 && s64) FEC_RB_LAUNCH(4, true);
+    else if (w == 4) FEC_RB_LAUNCH(4, false);
+    else if (w == 6 && s64) FEC_RB_LAUNCH(6, true);
+    else if (w == 6) FEC_RB_LAUNCH(6, false);
+    else if (s64) FEC_RB_LAUNCH(8, true);
+    else FEC_RB_LAUNCH(8, false);
+#undef FEC_RB_LAUNCH
     return hipGetLastError();
 }
 
