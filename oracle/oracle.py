@@ -245,10 +245,8 @@ def rs_recover_symbol_payloads(b, k, m):
         return None, "not enough present symbols to repair the missing ones"
     if b.is_complete():
         return None, None
-    L = REPAIR_PAYLOAD_METADATA_LEN + b.biggest
     n = b.tot_src + b.tot_rep
-    shards = np.zeros((1, n, L), dtype=np.uint8)
-    mask = 0
+    given = [None] * n   # shards[] of reed_solomon.go:101-122: framed sources, repairs as received
     missing = []
     for i in range(b.tot_src):
         ssid = b.smallest + i
@@ -258,13 +256,23 @@ def rs_recover_symbol_payloads(b, k, m):
         s, err = _shard_from_payload(b, ssid)
         if err:
             return None, err
-        shards[0, i] = np.frombuffer(s, dtype=np.uint8)
-        mask |= 1 << i
+        given[i] = s
     for pid, p in b.repairs.items():
-        if len(p) != L:
-            return None, "shard sizes do not match"   # klauspost ErrShardSize
-        shards[0, k + pid] = np.frombuffer(p.data, dtype=np.uint8)
-        mask |= 1 << (k + pid)
+        given[k + pid] = p.data
+    # enc.ReconstructData's checks (klauspost v1.12.4 checkShards / reconstruct): the shard size
+    # is the first non-empty shard's, every other non-empty one must match, and an empty
+    # (zero-length) shard counts as missing
+    L = next((len(g) for g in given if g is not None and len(g)), 0)
+    if L == 0:
+        return None, "no shard data"                  # klauspost ErrShardNoData
+    if any(g is not None and len(g) not in (0, L) for g in given):
+        return None, "shard sizes do not match"       # klauspost ErrShardSize
+    shards = np.zeros((1, n, L), dtype=np.uint8)
+    mask = 0
+    for i, g in enumerate(given):
+        if g is not None and len(g):
+            shards[0, i] = np.frombuffer(bytes(g), dtype=np.uint8)
+            mask |= 1 << i
     st = rs_reconstruct(k, m, shards, np.array([mask], dtype=np.uint32))
     if st[0] != 0:
         return None, "too few shards given"             # klauspost ErrTooFewShards

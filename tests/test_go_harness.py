@@ -109,6 +109,52 @@ def _synthetic_cases(oracle):
     return cases
 
 
+def _empty_repair_cases(oracle):
+    """RS blocks where a REPAIR arrived with a zero-length payload: klauspost's ReconstructData
+    counts a zero-length shard as missing (no ErrShardSize), so the block recovers from the other
+    shards, or fails with ErrTooFewShards when too few are left."""
+    rng = np.random.default_rng(0xE0FEC)
+    cases = []
+    for k, m, nlost, empty, keep in ((8, 4, 2, (0,), (0, 1, 2, 3)), (8, 4, 2, (0,), (0, 1)),
+                                     (20, 10, 3, (2, 5), tuple(range(10)))):
+        bid = int(rng.integers(0, 1 << 20))
+        lens = rng.integers(1, 1435, k)
+        pay = [bytes(rng.integers(0, 256, int(n), dtype=np.uint8)) for n in lens]
+        smallest = bid * k
+        src = {str(smallest + i): {"cap": 1452, "hex": pay[i].hex()} for i in range(k)}
+        blk = {"id": bid, "smallestSSID": smallest, "largestSSID": smallest + k - 1,
+               "biggestSourceSymbolLenSoFar": int(lens.max()), "totNumSourceSymbols": k,
+               "totNumRepairSymbols": m, "ssidToSourcePayload": src, "pidToRepairPayload": {}}
+        frames, err = oracle.rs_repair_symbols(oracle.block_from_fixture(blk), k, m)
+        assert err is None
+        lost = sorted(rng.choice(k, size=nlost, replace=False).tolist())
+        rblk = dict(blk)
+        rblk["ssidToSourcePayload"] = {s: v for s, v in src.items() if int(s) - smallest not in lost}
+        rblk["pidToRepairPayload"] = {str(p): ({"cap": 0, "hex": ""} if p in empty else
+                                               {"cap": len(frames[p][2]), "hex": frames[p][2].hex()})
+                                      for p in keep}
+        rblk["biggestSourceSymbolLenSoFar"] = len(frames[0][2]) - 2
+        got, err = oracle.rs_recover_symbol_payloads(oracle.block_from_fixture(rblk), k, m)
+        exp = ("err", err) if err is not None else ("bytes", got.hex())
+        cases.append(("rs_recover", rblk, k, m, exp, "RS(%d,%d) empty repairs %s, kept %s, lost %s"
+                      % (k, m, empty, keep, lost)))
+    return cases, pay
+
+
+def test_empty_repair_is_a_missing_shard(oracle):
+    """The oracle restates klauspost's zero-length rule: recovery ignores the empty repair."""
+    cases, _ = _empty_repair_cases(oracle)
+    kinds = [c[4][0] for c in cases]
+    assert kinds == ["bytes", "err", "bytes"]
+    assert cases[1][4][1] == "too few shards given"
+    for c in (cases[0], cases[2]):   # the recovered bytes are the lost sources, concatenated
+        blk, k = c[1], c[2]
+        ob = oracle.block_from_fixture(dict(blk, pidToRepairPayload={
+            p: v for p, v in blk["pidToRepairPayload"].items() if v["hex"]}))
+        got, err = oracle.rs_recover_symbol_payloads(ob, k, c[3])
+        assert err is None and got.hex() == c[4][1]
+
+
 @pytest.fixture(scope="module")
 def harness(fec):
     from native import binary
@@ -200,7 +246,7 @@ def test_go_call_sequence_golden(harness, golden, oracle, mode, tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["direct", "batch", "batchref"])
 def test_go_call_sequence_synthetic(harness, oracle, mode, tmp_path):
-    cases = _synthetic_cases(oracle)
+    cases = _synthetic_cases(oracle) + _empty_repair_cases(oracle)[0]
     _check(_run(harness, cases, mode, tmp_path), cases, texts=(mode == "direct"))
 
 
