@@ -31,4 +31,4 @@ for c in "rs 8 4 65536 2048 1200 1" "rs 8 4 65536 2048 1200 8" "rs 20 10 32768 1
     timeout -k 10 90 "$R/0xfec_amd/_bin/go_batch_bench" $c
 done > "$O/go_batch_bench.log" 2>&1
 cat "$O/go_batch_bench.log"
-tools/pmc_configs.sh "$TAG/counters" "rs1624,rs23"
+tools/pmc_configs.sh "$TAG/counters" "rs1624,rs2030m,rs23"
