@@ -328,7 +328,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.rehearse_one_gpu:
         local = 0
-    if world > 1:
+    # under torchrun the process group is always formed, a single rank included: then
+    # `torchrun --nproc-per-node 1 bench.py` runs the RCCL init, barriers and reductions of the
+    # N-GPU path on a one-GPU box
+    distributed = world_env is not None
+    if distributed:
         if args.rehearse_one_gpu:
             dist.init_process_group("gloo")
         else:
@@ -361,7 +365,7 @@ def main():
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -373,7 +377,7 @@ def main():
         ev[i][2].record(stream)
     codec.sync()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     wall = time.perf_counter() - t0
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
@@ -390,7 +394,7 @@ def main():
     inplace_ms = e0.elapsed_time(e1) / reps
     rank_step_ms = [step_ms]
     ranks_seen = 1
-    if world > 1:
+    if distributed:
         rdev = "cpu" if args.rehearse_one_gpu else dev   # gloo reduces host tensors
         ranks_seen = dist.get_world_size()
         per = [torch.zeros(1, device=rdev, dtype=torch.float64) for _ in range(ranks_seen)]
@@ -482,7 +486,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(k, m, args.cpu_sample_blocks, args.seed)
         print(json.dumps(out), flush=True)
     codec.close()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 
