@@ -72,6 +72,8 @@ def main():
         for w in (4, 6, 8):
             variants["table-copy rebuild (fixk 4) window %d" % w] = dict(D, dec_fixk=4, dec_win=w)
             variants["table-copy rebuild (fixk 4) window %d, 64-bit split shifts" % w] = dict(D, dec_fixk=4, dec_win=w, dec_s64=1)
+        for w in (2, 3):
+            variants["table-copy rebuild (fixk 4) wpc%d" % w] = dict(D, dec_fixk=4, dec_wpc=w)
         for w in (3, 4):
             variants["rolling window wpc%d" % w] = dict(D, dec_wpc=w)
         for w in (2, 3):
