@@ -53,6 +53,21 @@ constexpr PermTabSplit make_split_tables() {
 
 __device__ const PermTabSplit kPermTabSplit = make_split_tables();
 
+// Known answers (c * {0..7}, c * {0, 8, .., 56}, c * {0, 64, 128, 192} over 0x11D): c = 1 is the
+// identity; c = 0x80 and 0xFF exercise the reduction.
+constexpr PermTabSplit kSplitCheck = make_split_tables();
+static_assert(kSplitCheck.t01[1][0] == 0x03020100u && kSplitCheck.t01[1][1] == 0x07060504u &&
+                  kSplitCheck.t01[1][2] == 0x18100800u && kSplitCheck.t01[1][3] == 0x38302820u &&
+                  kSplitCheck.t2[1] == 0xC0804000u,
+              "PermTab of 1");
+static_assert(kSplitCheck.t01[0x80][0] == 0x9D1D8000u && kSplitCheck.t01[0x80][1] == 0xA727BA3Au &&
+                  kSplitCheck.t01[0x80][2] == 0x9CE87400u && kSplitCheck.t01[0x80][3] == 0x5125B9CDu &&
+                  kSplitCheck.t2[0x80] == 0x94138700u,
+              "PermTab of 0x80");
+static_assert(kSplitCheck.t01[0xFF][0] == 0x1CE3FF00u && kSplitCheck.t01[0xFF][3] == 0x76DD3D96u &&
+                  kSplitCheck.t2[0xFF] == 0x53623100u && kSplitCheck.t2[0] == 0u,
+              "PermTab of 0xFF");
+
 constexpr uint32_t kTabLds = 256 * 16 + 256 * 4;   // the workgroup's copy of kPermTabSplit
 
 // A wave's LDS slice: PermTab words of R rows x K inputs for each of its WB blocks, the blocks'

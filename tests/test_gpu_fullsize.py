@@ -3,6 +3,7 @@
   #2 RS(2,3)   65 536 blocks, one erased data shard per block
   #3 RS(8,12)  2^20 blocks, one erased data shard per block (the bench workload)
   #4 RS(16,24) 2^19 blocks, U{1..8} losses uniform over all 24 shards
+  RS(20,30)    2^19 blocks, U{1..10} losses uniform over all 30 shards (the reference's own code)
 
 Each batch is generated on the device (include/fec_synth.h), encoded (fec_rs_encode_batch,
 reed_solomon.go:51), recovered out of place (fec_rs_recover_batch, the device form of
@@ -57,7 +58,8 @@ def _sample_check(torch, oracle, k, m, data, par, lost, out, pick):
             assert np.array_equal(o[j, r], dmg[j, i]), (int(pick[j]), r, i)
 
 
-@pytest.mark.parametrize("k,m,B", [(2, 1, 65536), (8, 4, 1 << 20)], ids=["config2_rs2_3", "config3_rs8_12"])
+@pytest.mark.parametrize("k,m,B", [(2, 1, 65536), (8, 4, 1 << 20), (20, 10, 1 << 19)],
+                         ids=["config2_rs2_3", "config3_rs8_12", "rs20_30_reference_code"])
 def test_single_erasure_config_full_batch(fec, oracle, torch, k, m, B):
     codec = fec.Codec(0).use_torch_stream()
     try:
@@ -92,17 +94,19 @@ def test_single_erasure_config_full_batch(fec, oracle, torch, k, m, B):
         codec.close()
 
 
-@pytest.mark.parametrize("tier", [0, 2], ids=["default", "tier2"])
-def test_config4_rs16_24_mixed_erasures_full_batch(fec, oracle, torch, tier):
-    """RS(16,24) x 2^19 with e ~ U{1..8} lost shards per block, uniform over all 24."""
-    k, m, B = 16, 8, 1 << 19
+@pytest.mark.parametrize("k,m,tier", [(16, 8, 0), (16, 8, 2), (20, 10, 0)],
+                         ids=["config4_rs16_24", "config4_rs16_24_tier2", "rs20_30_reference_code"])
+def test_mixed_erasures_full_batch(fec, oracle, torch, k, m, tier):
+    """2^19 blocks with e ~ U{1..m} lost shards per block, uniform over all n: RS(16,24) (config #4)
+    and RS(20,30), the reference's own sender/receiver code (manager.go:58-59,81-82)."""
+    B = 1 << 19
     n = k + m
     codec = fec.Codec(0).use_torch_stream()
     old = codec.set_tuning(dec_tier=tier)
     try:
         data, par = _batch(torch, codec, k, m, B)
         g = torch.Generator(device="cuda")
-        g.manual_seed(0x1624)
+        g.manual_seed(0x1624 if k == 16 else 0x2030)
         e = torch.randint(1, m + 1, (B,), device="cuda", generator=g)
         rank = torch.rand((B, n), device="cuda", generator=g).argsort(dim=1).argsort(dim=1)
         lost = rank < e[:, None]
