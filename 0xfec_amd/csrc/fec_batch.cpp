@@ -570,9 +570,9 @@ BatchDecoder::~BatchDecoder() {
     for (Set& s : sets_) {
         if (s.inFlight && s.done) (void)hipEventSynchronize((hipEvent_t)s.done);
         if (s.done) (void)hipEventDestroy((hipEvent_t)s.done);
-        for (void* p : {(void*)s.h_in, (void*)s.h_out, (void*)s.h_masks, (void*)s.h_status})
+        for (void* p : {(void*)s.h_in, (void*)s.h_out, (void*)s.h_masks, (void*)s.h_status, s.h_desc})
             if (p) (void)hipHostFree(p);
-        for (void* p : {(void*)s.d_in, (void*)s.d_out, (void*)s.d_masks, (void*)s.d_status})
+        for (void* p : {(void*)s.d_in, (void*)s.d_out, (void*)s.d_masks, (void*)s.d_status, s.d_desc})
             if (p) (void)hipFree(p);
     }
 }
@@ -591,8 +591,14 @@ Error BatchDecoder::init() {
             (h = hipHostMalloc(&s.h_status, maxBlocks_ * 4, hipHostMallocDefault)) != hipSuccess ||
             (h = hipMalloc(&s.d_in, in_bytes)) != hipSuccess || (h = hipMalloc(&s.d_out, out_bytes)) != hipSuccess ||
             (h = hipMalloc(&s.d_masks, maxBlocks_ * 4)) != hipSuccess ||
-            (h = hipMalloc(&s.d_status, maxBlocks_ * 4)) != hipSuccess)
+            (h = hipMalloc(&s.d_status, maxBlocks_ * 4)) != hipSuccess ||
+            (h = hipHostMalloc(&s.h_desc, maxBlocks_ * n * sizeof(fk::GatherDesc), hipHostMallocDefault)) != hipSuccess ||
+            (h = hipMalloc(&s.d_desc, maxBlocks_ * n * sizeof(fk::GatherDesc))) != hipSuccess)
             return hip_error(h, "staging allocation");
+        void* in_dev = nullptr;
+        if ((h = hipHostGetDevicePointer(&in_dev, s.h_in, 0)) != hipSuccess)
+            return hip_error(h, "hipHostGetDevicePointer");
+        s.in_dev = (uint64_t)(uintptr_t)in_dev;
         hipEvent_t ev;
         if ((h = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hip_error(h, "hipEventCreate");
         s.done = ev;
@@ -626,7 +632,8 @@ Error BatchDecoder::stage(Block& b, uint8_t* dst, size_t slot, Pending* p, bool*
 }
 
 template <class StageFn>
-Error BatchDecoder::submitWith(size_t want, RecoveredQueue* q, bool* staged, StageFn&& stage_fn) {
+Error BatchDecoder::submitWith(size_t want, RecoveredQueue* q, bool* staged, StageFn&& stage_fn,
+                               const ShardRef* refs, std::vector<std::shared_ptr<PacketPool>>* pools) {
     if (staged) *staged = false;
     if (!q) return Error::text("nil recovered queue");
     want = std::min(kDecSlotMax, std::max<size_t>(16, round16(want)));
@@ -655,6 +662,20 @@ Error BatchDecoder::submitWith(size_t want, RecoveredQueue* q, bool* staged, Sta
     Error e = stage_fn(s->h_in + idx * n * s->slot, s->slot, &p, &nothing);
     if (!e.ok() || nothing) return e;
     s->h_masks[idx] = p.plan.mask;
+    // every shard of the block gets a gather descriptor (its staged slot unless referenced), so a
+    // set is gathered as a whole once any block of it holds a reference
+    fk::GatherDesc* desc = static_cast<fk::GatherDesc*>(s->h_desc) + idx * n;
+    for (size_t i = 0; i < n; ++i) {
+        if (refs && refs[i].dev) {
+            desc[i] = fk::GatherDesc{refs[i].dev, refs[i].len, refs[i].frame};
+            s->gather = true;
+        } else {
+            desc[i] = fk::GatherDesc{s->in_dev + (uint64_t)((idx * n + i) * s->slot), (uint32_t)s->slot, fk::kNoFrame};
+        }
+    }
+    if (pools)
+        for (auto& pl : *pools)
+            if (std::find(s->pools.begin(), s->pools.end(), pl) == s->pools.end()) s->pools.push_back(pl);
     s->maxLen = std::max(s->maxLen, rs_ ? p.plan.len : s->slot);
     s->outSlots = std::max(s->outSlots, rs_ ? p.plan.missing.size() : (size_t)1);
     p.q = q;
@@ -704,6 +725,57 @@ Error BatchDecoder::SubmitPayloads(BlockID id, SourceSymbolID smallest, SourceSy
     });
 }
 
+Error BatchDecoder::SubmitPayloadRefs(BlockID id, SourceSymbolID smallest, SourceSymbolID largest, int biggest,
+                                      const uint8_t* const* src, const size_t* slen, const uint8_t* const* rep,
+                                      const size_t* rlen, RecoveredQueue* q, bool* staged) {
+    if (!rs_ || !src || !slen || !rep || !rlen || biggest < 0)
+        return SubmitPayloads(id, smallest, largest, biggest, src, slen, rep, rlen, q, staged);
+    if (staged) *staged = false;
+    // the shards the device can gather: a source within `biggest` (a longer one is cut at biggest
+    // + 2 on the host, addLengthToSourceSymbolPayload's reslice) or a repair, in a registered pool
+    const size_t n = (size_t)k_ + m_;
+    std::vector<ShardRef> refs(n, ShardRef{0, 0, 0});
+    std::vector<uint8_t> skip(n, 0);
+    std::vector<std::shared_ptr<PacketPool>> pools;
+    for (size_t i = 0; i < n; ++i) {
+        const bool isSrc = i < (size_t)k_;
+        const uint8_t* ptr = isSrc ? src[i] : rep[i - k_];
+        const size_t len = isSrc ? slen[i] : rlen[i - k_];
+        if (!ptr || len == 0 || (isSrc && len > (size_t)biggest)) continue;
+        uint64_t dev = 0;
+        for (const auto& pl : pools)
+            if ((dev = pl->DevAddr(ptr, len))) break;
+        if (!dev) {
+            std::shared_ptr<PacketPool> pl;
+            if ((dev = PacketPool::Lookup(ptr, len, &pl))) pools.push_back(std::move(pl));
+        }
+        if (!dev) continue;
+        refs[i] = ShardRef{dev, (uint32_t)len, isSrc ? (uint32_t)biggest : fk::kNoFrame};
+        skip[i] = 1;
+    }
+    size_t want = kRepairPayloadMetadataLen + (size_t)biggest;
+    for (int p = 0; p < m_; ++p)
+        if (rep[p]) want = std::max(want, rlen[p]);
+    return submitWith(
+        want, q, staged,
+        [&](uint8_t* dst, size_t slot, Pending* p, bool* nothing) {
+            *nothing = false;
+            p->id = id;
+            p->meta = Block{};
+            p->meta.id = id;
+            p->meta.totNumSourceSymbols = k_;
+            p->meta.totNumRepairSymbols = m_;
+            p->meta.smallestSSID = smallest;
+            p->meta.largestSSID = largest;
+            p->meta.biggestSourceSymbolLenSoFar = biggest;
+            Error e = rs_->stageRecoverPayloads(biggest, src, slen, rep, rlen, dst, slot, &p->plan,
+                                                reinterpret_cast<const bool*>(skip.data()));
+            if (e.ok()) *nothing = p->plan.nothing;
+            return e;
+        },
+        refs.data(), &pools);
+}
+
 Error BatchDecoder::Flush() { return flushImpl(nullptr); }
 
 Error BatchDecoder::flushImpl(size_t* delivered) {
@@ -720,8 +792,18 @@ Error BatchDecoder::flushImpl(size_t* delivered) {
     hipStream_t st = (hipStream_t)fec_ctx_stream(ctx);
     const size_t B = s.blocks.size(), n = (size_t)k_ + m_, S = s.slot;
     const size_t nin = rs_ ? n : (size_t)k_;   // XOR stages its k inputs only
-    hipError_t h = hipMemcpyAsync(s.d_in, s.h_in, B * n * S, hipMemcpyHostToDevice, st);
-    if (h != hipSuccess) return hip_error(h, "hipMemcpyAsync H2D");
+    hipError_t h;
+    if (s.gather) {   // referenced payloads: the device pulls every shard of the set itself
+        if ((h = hipMemcpyAsync(s.d_desc, s.h_desc, B * n * sizeof(fk::GatherDesc), hipMemcpyHostToDevice, st)) !=
+            hipSuccess)
+            return hip_error(h, "hipMemcpyAsync H2D");
+        if ((h = hipSetDevice(engine_->device())) != hipSuccess) return hip_error(h, "hipSetDevice");
+        if ((h = fk::launch_gather_desc(static_cast<const fk::GatherDesc*>(s.d_desc), (uint32_t)(B * n), s.d_in, S,
+                                        st)) != hipSuccess)
+            return hip_error(h, "gather launch");
+    } else if ((h = hipMemcpyAsync(s.d_in, s.h_in, B * n * S, hipMemcpyHostToDevice, st)) != hipSuccess) {
+        return hip_error(h, "hipMemcpyAsync H2D");
+    }
     int rc;
     if (rs_) {
         if ((h = hipMemcpyAsync(s.d_masks, s.h_masks, B * 4, hipMemcpyHostToDevice, st)) != hipSuccess)
@@ -779,6 +861,8 @@ Error BatchDecoder::deliver(Set& s, size_t* blocks) {
     s.blocks.clear();
     s.maxLen = s.outSlots = s.delivered = 0;
     s.inFlight = false;
+    s.gather = false;
+    s.pools.clear();
     return Error::nil();
 }
 

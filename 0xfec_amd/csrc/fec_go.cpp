@@ -211,6 +211,21 @@ int fec_go_decoder_submit(fec_go_decoder* d, uint64_t block_id, uint64_t smalles
     return rc;
 }
 
+int fec_go_decoder_submit_ref(fec_go_decoder* d, uint64_t block_id, uint64_t smallest_ssid, uint64_t largest_ssid,
+                              int biggest, const uint8_t* const* sources, const size_t* source_lens,
+                              const uint8_t* const* repairs, const size_t* repair_lens, int* staged) {
+    if (staged) *staged = 0;
+    if (!d || !sources || !source_lens || !repairs || !repair_lens) return FEC_ERR_INVALID_ARG;
+    for (int i = 0; i < d->k; ++i)
+        if (sources[i] && source_lens[i] > fec::kMaxPacketBufferSize)
+            return report(fec::Error::text("source payload longer than a packet buffer"));
+    bool st = false;
+    const int rc = report(d->dec->SubmitPayloadRefs(block_id, smallest_ssid, largest_ssid, biggest, sources,
+                                                     source_lens, repairs, repair_lens, &d->q, &st));
+    if (staged) *staged = st ? 1 : 0;
+    return rc;
+}
+
 void fec_go_decoder_drop(fec_go_decoder* d, uint64_t block_id) {
     if (d) d->blocks.erase(block_id);
 }

@@ -278,7 +278,7 @@ Error ReedSolomonScheme::stageRecoverInput(Block& b, uint8_t* dst, size_t stride
 
 Error ReedSolomonScheme::stageRecoverPayloads(int biggest, const uint8_t* const* src, const size_t* slen,
                                               const uint8_t* const* rep, const size_t* rlen, uint8_t* dst,
-                                              size_t stride, RecoverPlan* plan) {
+                                              size_t stride, RecoverPlan* plan, const bool* skip) {
     // stageRecoverInput over the payloads themselves: the block is k sources (SSID order) and m
     // repairs (ParityID order); every check of reed_solomon.go:92-124 and ReconstructData, in order
     plan->nothing = false;
@@ -327,6 +327,7 @@ Error ReedSolomonScheme::stageRecoverPayloads(int biggest, const uint8_t* const*
     for (int i = 0; i < nsh; ++i) {
         if (len_of(i) == 0) continue;
         mask |= 1u << i;
+        if (skip && skip[i]) continue;
         uint8_t* d = dst + (size_t)i * stride;
         if (i < k_) {   // payload[:shardLen] of a zeroed packet buffer, BE16 length at [biggest]
             const size_t c = std::min(slen[i], L);

@@ -209,7 +209,14 @@ func (r *BatchReceiver) Close() {
 // Submit replaces `m.scheme.recoverSymbolPayloads(bS.block)` (manager.go:182) for a
 // recoverable block: validation and error texts as the reference, reported now; staged is
 // false for a complete block (the reference's nil, nil). The payload arrives from Poll.
-func (r *BatchReceiver) Submit(b *block) (staged bool, err error) {
+func (r *BatchReceiver) Submit(b *block) (staged bool, err error) { return r.submit(b, false) }
+
+// SubmitRef is Submit by reference (RS): received payloads lying in the registered
+// PacketPool are read by the device when the batch is coded (fec_go_decoder_submit_ref), so
+// the caller keeps those buffers unchanged until Poll returns the block; others are copied now.
+func (r *BatchReceiver) SubmitRef(b *block) (staged bool, err error) { return r.submit(b, true) }
+
+func (r *BatchReceiver) submit(b *block, byRef bool) (staged bool, err error) {
 	// recoverSymbolPayloads' block-level checks, on the Go block itself (reed_solomon.go:93-100)
 	if !b.isRecoverable() {
 		return false, fmt.Errorf("not enough present symbols to repair the missing ones")
@@ -250,9 +257,16 @@ func (r *BatchReceiver) Submit(b *block) (staged bool, err error) {
 		put(r.k+pid, p)
 	}
 	var st C.int
-	rc := C.fec_go_decoder_submit(r.d, C.uint64_t(b.id), C.uint64_t(b.smallestSSID), C.uint64_t(b.largestSSID),
-		C.int(b.biggestSourceSymbolLenSoFar), (**C.uint8_t)(unsafe.Pointer(r.src)), r.lens,
-		(**C.uint8_t)(unsafe.Pointer(&ptrs[r.k])), &lens[r.k], &st)
+	var rc C.int
+	if byRef {
+		rc = C.fec_go_decoder_submit_ref(r.d, C.uint64_t(b.id), C.uint64_t(b.smallestSSID), C.uint64_t(b.largestSSID),
+			C.int(b.biggestSourceSymbolLenSoFar), (**C.uint8_t)(unsafe.Pointer(r.src)), r.lens,
+			(**C.uint8_t)(unsafe.Pointer(&ptrs[r.k])), &lens[r.k], &st)
+	} else {
+		rc = C.fec_go_decoder_submit(r.d, C.uint64_t(b.id), C.uint64_t(b.smallestSSID), C.uint64_t(b.largestSSID),
+			C.int(b.biggestSourceSymbolLenSoFar), (**C.uint8_t)(unsafe.Pointer(r.src)), r.lens,
+			(**C.uint8_t)(unsafe.Pointer(&ptrs[r.k])), &lens[r.k], &st)
+	}
 	return st != 0, goErr(rc)
 }
 

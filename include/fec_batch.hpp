@@ -281,6 +281,14 @@ public:
     Error SubmitPayloads(BlockID id, SourceSymbolID smallest, SourceSymbolID largest, int biggest,
                          const uint8_t* const* src, const size_t* slen, const uint8_t* const* rep, const size_t* rlen,
                          RecoveredQueue* q, bool* staged = nullptr);
+    // By-reference form (RS): a present payload lying in a registered PacketPool is validated but
+    // not copied; the device gathers it (sources framed with their BE16 length trailer at
+    // `biggest`, repairs verbatim) when the batch is coded. Others are staged as by
+    // SubmitPayloads; XOR decoders stage everything. The pool buffers must stay unchanged until
+    // the block comes back from Poll / Drain.
+    Error SubmitPayloadRefs(BlockID id, SourceSymbolID smallest, SourceSymbolID largest, int biggest,
+                            const uint8_t* const* src, const size_t* slen, const uint8_t* const* rep,
+                            const size_t* rlen, RecoveredQueue* q, bool* staged = nullptr);
     Error Flush();
     Error Poll(size_t* blocks = nullptr);
     Error Drain(size_t* blocks = nullptr);
@@ -309,14 +317,25 @@ private:
         std::vector<Pending> blocks;
         size_t slot = 0, maxLen = 0, outSlots = 0, delivered = 0;
         bool inFlight = false;
+        void* h_desc = nullptr;     // pinned [maxBlocks][n] gather descriptors (fk::GatherDesc)
+        void* d_desc = nullptr;
+        uint64_t in_dev = 0;        // h_in as the device sees it
+        bool gather = false;        // a block of the set is referenced: the device gathers the set
+        std::vector<std::shared_ptr<PacketPool>> pools;   // pools the set's references point into
     };
     BatchDecoder(DecoderFECScheme scheme, int k, int m, size_t maxBlocks, std::shared_ptr<Engine> e)
         : scheme_(scheme), k_(k), m_(m), maxBlocks_(maxBlocks), engine_(std::move(e)) {}
     Error init();
     Error stage(Block& b, uint8_t* dst, size_t slot, Pending* p, bool* nothing);
-    // Submit's body: `stage_fn(dst, slot, &pending, &nothing)` validates and stages one block
+    // Submit's body: `stage_fn(dst, slot, &pending, &nothing)` validates and stages one block;
+    // refs (nullable, n entries): shards left where they are (dev != 0) for the device to gather
+    struct ShardRef {
+        uint64_t dev;              // device-visible address, 0: the shard is staged
+        uint32_t len, frame;       // bytes, BE16 trailer position (or fk::kNoFrame)
+    };
     template <class StageFn>
-    Error submitWith(size_t want, RecoveredQueue* q, bool* staged, StageFn&& stage_fn);
+    Error submitWith(size_t want, RecoveredQueue* q, bool* staged, StageFn&& stage_fn,
+                     const ShardRef* refs = nullptr, std::vector<std::shared_ptr<PacketPool>>* pools = nullptr);
     Error flushImpl(size_t* delivered);
     Error waitSet(Set& s);
     Error deliver(Set& s, size_t* blocks);

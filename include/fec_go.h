@@ -28,6 +28,8 @@
  *   fec_go_decoder_submit       the same straight from the Go block's state and payload
  *                               pointers (runtime.Pinner, as fec_go_encoder_submit): no
  *                               add_* calls, nothing retained after the call
+ *   fec_go_decoder_submit_ref   the same by reference, for received payloads in a registered
+ *                               pool: the device gathers them, no host copy (RS)
  *   fec_go_decoder_poll         the payload recoverSymbolPayloads returns, per recovered block
  *
  * Errors: 0, FEC_ERR_SCHEME with the reference's text in fec_last_error() (fec_scheme.h), or a
@@ -108,6 +110,14 @@ int fec_go_decoder_commit(fec_go_decoder *d, uint64_t block_id, int *staged);
 int fec_go_decoder_submit(fec_go_decoder *d, uint64_t block_id, uint64_t smallest_ssid, uint64_t largest_ssid,
                           int biggest, const uint8_t *const *sources, const size_t *source_lens,
                           const uint8_t *const *repairs, const size_t *repair_lens, int *staged);
+/* fec_go_decoder_submit by reference (RS decoders): a present source (at most `biggest` bytes)
+ * or repair payload lying in a registered pool (fec_go_pool_new) is validated now but read by the
+ * device when the batch is coded, so the caller keeps it unchanged until poll returns block_id.
+ * Payloads elsewhere, and XOR decoders, are copied now. Same checks and errors as
+ * fec_go_decoder_submit. */
+int fec_go_decoder_submit_ref(fec_go_decoder *d, uint64_t block_id, uint64_t smallest_ssid, uint64_t largest_ssid,
+                              int biggest, const uint8_t *const *sources, const size_t *source_lens,
+                              const uint8_t *const *repairs, const size_t *repair_lens, int *staged);
 /* Forget a block without recovering it (complete, or given up). */
 void fec_go_decoder_drop(fec_go_decoder *d, uint64_t block_id);
 int fec_go_decoder_flush(fec_go_decoder *d);

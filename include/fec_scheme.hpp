@@ -144,8 +144,11 @@ public:
     // The same for a block given as its payloads (fec_go_decoder_submit: no Block built):
     // src[i] = the payload of SSID smallestSSID + i or nullptr, read with the capacity of a
     // packet buffer (kMaxPacketBufferSize); rep[p] = the payload of ParityID p or nullptr.
+    // skip (nullable, k + m entries): shard i is validated and counted but not written (the
+    // caller has the device gather it, BatchDecoder::SubmitPayloadRefs).
     Error stageRecoverPayloads(int biggest, const uint8_t* const* src, const size_t* slen, const uint8_t* const* rep,
-                               const size_t* rlen, uint8_t* dst, size_t stride, RecoverPlan* plan);
+                               const size_t* rlen, uint8_t* dst, size_t stride, RecoverPlan* plan,
+                               const bool* skip = nullptr);
     // The rest of recoverSymbolPayloads: rebuilt[r] = the rebuilt shard of plan.missing[r].
     Error finishRecover(const Block& b, const RecoverPlan& plan, const uint8_t* const* rebuilt, Slice* out);
 

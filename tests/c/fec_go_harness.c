@@ -368,9 +368,26 @@ static int batch_recover(Case *c, int scheme) {
         ptrs[c->k + p] = r ? (r->len ? r->p : empty) : NULL;
         lens[c->k + p] = r ? r->len : 0;
     }
+    if (g_ref && scheme == FEC_SCHEME_REED_SOLOMON) {
+        /* batchref: the received payloads sit in registered packet buffers (BatchReceiver.SubmitRef) */
+        if (!g_pool && !(g_pool = fec_go_pool_new(2 * MAX_SYM, &g_pool_base, &rc))) {
+            fec_go_decoder_free(d);
+            return go_err(rc);
+        }
+        for (int i = 0; i < c->k + mm; ++i)
+            if (ptrs[i] && lens[i] && lens[i] <= FEC_GO_POOL_SLOT) {
+                uint8_t *buf = g_pool_base + (size_t)i * FEC_GO_POOL_SLOT;
+                memcpy(buf, ptrs[i], lens[i]);
+                ptrs[i] = buf;
+            }
+    }
     int staged = 0;
-    rc = fec_go_decoder_submit(d, c->id, c->smallest, c->largest, c->biggest, ptrs, lens, ptrs + c->k, lens + c->k,
-                               &staged);
+    if (g_ref)
+        rc = fec_go_decoder_submit_ref(d, c->id, c->smallest, c->largest, c->biggest, ptrs, lens, ptrs + c->k,
+                                       lens + c->k, &staged);
+    else
+        rc = fec_go_decoder_submit(d, c->id, c->smallest, c->largest, c->biggest, ptrs, lens, ptrs + c->k, lens + c->k,
+                                   &staged);
     if (rc) {
         fec_go_decoder_free(d);
         return go_err(rc);

@@ -134,3 +134,121 @@ def test_submit_ref_errors_match_submit(fec):
     finally:
         lib.fec_go_encoder_free(enc)
         lib.fec_go_pool_free(pool)
+
+
+def _bind_dec(lib):
+    _bind(lib)
+    lib.fec_go_decoder_new.restype = _vp
+    lib.fec_go_decoder_new.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _sz, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_int)]
+    lib.fec_go_decoder_free.argtypes = [_vp]
+    lib.fec_go_decoder_free.restype = None
+    for fn in (lib.fec_go_decoder_submit, lib.fec_go_decoder_submit_ref):
+        fn.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(_vp),
+                       ctypes.POINTER(_sz), ctypes.POINTER(_vp), ctypes.POINTER(_sz), ctypes.POINTER(ctypes.c_int)]
+    lib.fec_go_decoder_poll.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                        ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p,
+                                        _sz, _sz, ctypes.POINTER(_sz)]
+    return lib
+
+
+@pytest.mark.parametrize("k,m", [(8, 4), (20, 10), (2, 1)])
+def test_decoder_submit_ref_matches_oracle(fec, oracle, k, m):
+    """fec_go_decoder_submit_ref: received sources and repairs in registered packet buffers are
+    gathered by the device (sources framed with their trailer at `biggest`, repairs verbatim).
+    Every polled payload must equal the oracle's recoverSymbolPayloads (reed_solomon.go:92-136)
+    for the same block, with referenced, copied (outside the pool) and empty (missing) shards
+    mixed, at unaligned offsets, over several batches of both staging sets."""
+    lib = _bind_dec(fec.lib)
+    rng = np.random.default_rng(0xDEC + 31 * k + m)
+    nblocks, maxb, n = 200, 32, k + m
+    nbuf = nblocks * n + 8
+    base = _vp()
+    err = ctypes.c_int(0)
+    pool = lib.fec_go_pool_new(nbuf, ctypes.byref(base), ctypes.byref(err))
+    assert pool, lib.fec_last_error()
+    dec = lib.fec_go_decoder_new(RS, k, m, maxb, 0, ctypes.byref(err))
+    assert dec, lib.fec_last_error()
+    outside = []
+    try:
+        pool_np = np.frombuffer((ctypes.c_uint8 * (nbuf * POOL_SLOT)).from_address(base.value), dtype=np.uint8)
+        ptrs = (_vp * n)()
+        lens = (_sz * n)()
+        staged = ctypes.c_int(0)
+        ids = (ctypes.c_uint64 * maxb)()
+        pl = (ctypes.c_uint32 * maxb)()
+        offs = (ctypes.c_uint64 * maxb)()
+        out = np.zeros(maxb * k * SLOT, dtype=np.uint8)
+        nb = _sz(0)
+        want, got, order = {}, {}, []
+
+        def poll(wait):
+            assert lib.fec_go_decoder_poll(dec, wait, ids, pl, offs, out.ctypes.data, out.size, maxb,
+                                           ctypes.byref(nb)) == 0, lib.fec_last_error()
+            for d in range(nb.value):
+                order.append(ids[d])
+                got[ids[d]] = bytes(out[offs[d]:offs[d] + pl[d]])
+
+        def place(slot, data, mode, i):
+            if mode == 3 and i % 2:   # outside any pool: copied by the library
+                arr = np.frombuffer(bytearray(data) + b"\0" * 16, dtype=np.uint8).copy()
+                outside.append(arr)
+                return arr.ctypes.data
+            off = 2 * int(rng.integers(1, 4)) if mode == 2 else 0
+            start = slot * POOL_SLOT + off
+            if len(data) + off > POOL_SLOT:
+                start -= off
+            pool_np[start:start + len(data)] = np.frombuffer(data, dtype=np.uint8)
+            return base.value + start
+
+        for b in range(nblocks):
+            mode = b % 5    # 0,1: all in the pool; 2: unaligned; 3: mixed with copied; 4: an empty repair
+            pls = [rng.integers(0, 256, int(rng.integers(1, 1201)), dtype=np.uint8).tobytes() for _ in range(k)]
+            reps = _oracle_repairs(oracle, RS, k, m, pls)
+            L = len(reps[0])
+            lost = set(rng.choice(k, size=int(rng.integers(1, m + 1)), replace=False).tolist())
+            keep = sorted(rng.choice(m, size=m, replace=False).tolist()[:max(len(lost), 1) + int(rng.integers(0, 2))])
+            empty = keep[0] if mode == 4 and len(keep) > len(lost) else None
+            src = {}
+            for i in range(k):
+                if i in lost:
+                    ptrs[i], lens[i] = None, 0
+                else:
+                    ptrs[i], lens[i] = place(b * n + i, pls[i], mode, i), len(pls[i])
+                    src[b * k + i] = oracle.Payload(pls[i], 1452)
+            rmap = {}
+            for p in range(m):
+                if p not in keep:
+                    ptrs[k + p], lens[k + p] = None, 0
+                elif p == empty:
+                    ptrs[k + p], lens[k + p] = base.value + (b * n + k + p) * POOL_SLOT, 0
+                    rmap[p] = oracle.Payload(b"", 0)
+                else:
+                    ptrs[k + p], lens[k + p] = place(b * n + k + p, reps[p], mode, p), L
+                    rmap[p] = oracle.Payload(reps[p], L)
+            ob = oracle.Block(id=b, tot_src=k, tot_rep=m, biggest=L - 2, smallest=b * k, largest=b * k + k - 1,
+                              sources=src, repairs=rmap)
+            exp, e = oracle.rs_recover_symbol_payloads(ob, k, m)
+            rsrc = ctypes.cast(ptrs, ctypes.POINTER(_vp))
+            rrep = ctypes.cast(ctypes.byref(ptrs, k * ctypes.sizeof(_vp)), ctypes.POINTER(_vp))
+            rlen = ctypes.cast(ctypes.byref(lens, k * ctypes.sizeof(_sz)), ctypes.POINTER(_sz))
+            rc = lib.fec_go_decoder_submit_ref(dec, b, b * k, b * k + k - 1, L - 2, rsrc, lens, rrep, rlen,
+                                               ctypes.byref(staged))
+            if e is not None:
+                assert rc != 0, (b, e)
+                continue
+            assert rc == 0, lib.fec_last_error()
+            assert staged.value == 1
+            want[b] = exp
+            if b % 29 == 28:
+                poll(0)
+        while len(got) < len(want):
+            before = len(got)
+            poll(1)
+            assert len(got) > before
+        assert order == sorted(want), "blocks come back in submission order"
+        for b, exp in want.items():
+            assert got[b] == exp, "block %d" % b
+    finally:
+        lib.fec_go_decoder_free(dec)
+        lib.fec_go_pool_free(pool)

@@ -12,6 +12,8 @@
  * ref: every source payload sits in a registered packet buffer (fec_go_pool_new, one buffer per
  * payload, written before the timed region as the packer would write the frame into it) and is
  * submitted with fec_go_encoder_submit_ref: the device gathers it, the host copies nothing in.
+ * On the receive side (RS) the received sources and repair sit in pool buffers too (as the wire
+ * parser would have written them) and go in with fec_go_decoder_submit_ref.
  */
 #define _GNU_SOURCE
 #include <pthread.h>
@@ -63,7 +65,7 @@ static void *run(void *arg) {
     fec_go_pool *pool = NULL;
     uint8_t *pbase = NULL;
     if (j->ref && !j->fail) {
-        pool = fec_go_pool_new((size_t)nb * k, &pbase, &rc);
+        pool = fec_go_pool_new((size_t)nb * (k + 1), &pbase, &rc);
         if (!pool) {
             fprintf(stderr, "pool: %d %s\n", rc, fec_last_error());
             j->fail = 1;
@@ -123,6 +125,11 @@ static void *run(void *arg) {
         }
     }
     j->te = now() - t0;
+    /* ref: each block's received repair 0 in a pool buffer (after the sources' nb * k buffers) */
+    const int dref = j->ref && !j->fail && j->scheme == FEC_SCHEME_REED_SOLOMON;
+    if (dref)
+        for (int b = 0; b < nb; ++b)
+            memcpy(pbase + ((size_t)nb * k + b) * FEC_GO_POOL_SLOT, j->reps + (size_t)b * m * FEC_GO_SLOT, rlen);
     /* ---- decode: source 0 of every block lost, repair 0 received */
     pthread_barrier_wait(j->bar);
     t0 = now();
@@ -131,16 +138,19 @@ static void *run(void *arg) {
         ptrs[0] = NULL;
         lens[0] = 0;
         for (int i = 1; i < k; ++i) {
-            ptrs[i] = j->pay + ((size_t)b * k + i) * len;
+            ptrs[i] = dref ? pbase + ((size_t)b * k + i) * FEC_GO_POOL_SLOT : j->pay + ((size_t)b * k + i) * len;
             lens[i] = len;
         }
         for (int p = 0; p < m; ++p) {
-            ptrs[k + p] = p == 0 ? j->reps + (size_t)b * m * FEC_GO_SLOT : NULL;
+            ptrs[k + p] = p != 0 ? NULL
+                          : dref ? pbase + ((size_t)nb * k + b) * FEC_GO_POOL_SLOT
+                                 : j->reps + (size_t)b * m * FEC_GO_SLOT;
             lens[k + p] = rlen;
         }
         int st = 0;
-        if (fec_go_decoder_submit(d, (uint64_t)b, (uint64_t)b * k, (uint64_t)b * k + k - 1, (int)len, ptrs, lens,
-                                  ptrs + k, lens + k, &st) ||
+        if ((dref ? fec_go_decoder_submit_ref : fec_go_decoder_submit)(d, (uint64_t)b, (uint64_t)b * k,
+                                                                       (uint64_t)b * k + k - 1, (int)len, ptrs, lens,
+                                                                       ptrs + k, lens + k, &st) ||
             !st) {
             fprintf(stderr, "dsubmit: %s\n", fec_last_error());
             j->fail = 1;
