@@ -3,6 +3,9 @@
 package fec
 
 import (
+	"sync"
+	"unsafe"
+
 	"github.com/quic-go/quic-go/internal/protocol"
 	"github.com/quic-go/quic-go/internal/wire"
 )
@@ -99,6 +102,14 @@ type batchManager struct {
 	// reference, held until their frames are polled, then returned to the pool
 	pool *PacketPool
 	held map[protocol.BlockID][][]byte
+	// receiver with the pool: received payloads are read into its buffers (wire.FECPayloadBuffer,
+	// go/patches/fec_source_symbol_frame.go.diff) and recoverable blocks go in by reference
+	// (BatchReceiver.SubmitRef). A staged block's buffers go back once its data has been polled
+	// (rxHeld); buffers no block keeps go back at the next PollRecovered (release), because the
+	// connection parses a SOURCE_SYMBOL payload after HandleSourceSymbolFrame returns it
+	// (connection.go:1653), copying what it keeps (stream_frame.go:56-76).
+	rxHeld  map[protocol.BlockID][][]byte
+	release [][]byte
 }
 
 var (
@@ -122,6 +133,10 @@ func newBatchManager(id protocol.DecoderFECScheme, k, m int, send bool) (*batchM
 		}
 	} else {
 		bm.rx, err = NewBatchReceiver(id, k, m, hipBatchBlocks)
+		if bm.pool = hipPacketPool(); bm.pool != nil {
+			bm.rxHeld = make(map[protocol.BlockID][][]byte)
+			hookWirePayloads(bm.pool)
+		}
 	}
 	if err != nil {
 		return nil, err
@@ -206,9 +221,74 @@ func (m *batchManager) SourcePayloadBuffer() []byte {
 	return m.pool.Get()
 }
 
+var wireHookOnce sync.Once
+
+// hookWirePayloads points the wire parser's payload allocation at the pool (process-wide, as the
+// pool is). The bytes past the payload are zeroed, as make's are: addLengthToSourceSymbolPayload
+// reslices a source payload into its capacity (reed_solomon.go:77-87).
+func hookWirePayloads(pp *PacketPool) {
+	wireHookOnce.Do(func() {
+		wire.FECPayloadBuffer = func(n int) []byte {
+			if n > protocol.MaxPacketBufferSize {
+				return nil
+			}
+			b := pp.Get()
+			if b == nil {
+				return nil // pool exhausted: the parser makes one on the heap
+			}
+			b = b[:cap(b)]
+			clear(b[n:])
+			return b[:0]
+		}
+	})
+}
+
+// sameBuf: a and b are slices of one buffer (block.go:63,80 ignore a duplicate SSID / ParityID,
+// whose payload the block then does not keep).
+func sameBuf(a, b []byte) bool {
+	return cap(a) > 0 && cap(b) > 0 && unsafe.SliceData(a) == unsafe.SliceData(b)
+}
+
+// blockPayloads: every payload a block keeps.
+func blockPayloads(b *block) [][]byte {
+	ps := make([][]byte, 0, len(b.ssidToSourcePayload)+len(b.pidToRepairPayload))
+	for _, p := range b.ssidToSourcePayload {
+		ps = append(ps, p)
+	}
+	for _, p := range b.pidToRepairPayload {
+		ps = append(ps, p)
+	}
+	return ps
+}
+
+// HandleSourceSymbolFrame is the reference's (manager.go:200-227); with the pool it also notes
+// which received buffers no block keeps any longer, to go back at the next PollRecovered.
+func (m *batchManager) HandleSourceSymbolFrame(f *wire.SourceSymbolFrame) ([]byte, error) {
+	if m.rxHeld == nil {
+		return m.manager.HandleSourceSymbolFrame(f)
+	}
+	blockID := m.sidToBlockID(f.SSID)
+	prev := m.blockStatuses[blockID].block // nil: a new block, or one already processed
+	payload, err := m.manager.HandleSourceSymbolFrame(f)
+	if cur := m.blockStatuses[blockID].block; cur != nil {
+		if kept, ok := cur.ssidToSourcePayload[f.SSID]; !ok || !sameBuf(kept, f.Payload) {
+			m.release = append(m.release, f.Payload)
+		}
+	} else if prev != nil { // completed by this symbol: the block is dropped (manager.go:221-224)
+		if kept, ok := prev.ssidToSourcePayload[f.SSID]; !ok || !sameBuf(kept, f.Payload) {
+			m.release = append(m.release, f.Payload)
+		}
+		m.release = append(m.release, blockPayloads(prev)...)
+	} else {
+		m.release = append(m.release, f.Payload)
+	}
+	return payload, err
+}
+
 // HandleRepairFrame is manager.go:160-198 with recoverSymbolPayloads (:182) replaced by a
-// Submit of the recoverable block; it returns no data (it comes from PollRecovered). A block
-// that is already complete is the reference's nil, nil: nothing is staged.
+// Submit of the recoverable block (SubmitRef with the pool); it returns no data (it comes from
+// PollRecovered). A block that is already complete is the reference's nil, nil: nothing is
+// staged.
 func (m *batchManager) HandleRepairFrame(f *wire.RepairFrame) ([]byte, error) {
 	if _, exists := m.blockStatuses[f.Metadata.BlockID]; !exists {
 		m.blockStatuses[f.Metadata.BlockID] = blockStatus{
@@ -217,19 +297,40 @@ func (m *batchManager) HandleRepairFrame(f *wire.RepairFrame) ([]byte, error) {
 		}
 	}
 	bS := m.blockStatuses[f.Metadata.BlockID]
+	pooled := m.rxHeld != nil
 	if bS.isProcessed {
+		if pooled {
+			m.release = append(m.release, f.Payload)
+		}
 		return nil, nil
 	}
 	if err := bS.block.addRepairSymbol(f); err != nil {
+		if pooled {
+			m.release = append(m.release, f.Payload)
+		}
 		return nil, err
 	}
+	if kept := bS.block.pidToRepairPayload[f.Metadata.ParityID]; pooled && !sameBuf(kept, f.Payload) {
+		m.release = append(m.release, f.Payload)
+	}
 	if bS.block.isRecoverable() {
-		staged, err := m.rx.Submit(bS.block)
+		var staged bool
+		var err error
+		if pooled {
+			staged, err = m.rx.SubmitRef(bS.block)
+		} else {
+			staged, err = m.rx.Submit(bS.block)
+		}
 		if err != nil {
 			return nil, err
 		}
 		if staged {
 			m.pending++
+			if pooled { // the device reads these when the batch is coded
+				m.rxHeld[f.Metadata.BlockID] = blockPayloads(bS.block)
+			}
+		} else if pooled {
+			m.release = append(m.release, blockPayloads(bS.block)...)
 		}
 		bS.block = nil
 		bS.isProcessed = true
@@ -242,13 +343,25 @@ func (m *batchManager) HandleRepairFrame(f *wire.RepairFrame) ([]byte, error) {
 // staged block). Also starts decoding the staged blocks when no batch is in flight.
 func (m *batchManager) PollRecovered(wait bool) ([][]byte, error) {
 	var out [][]byte
+	if m.rxHeld != nil { // the receive burst that used these buffers has been handled
+		for _, p := range m.release {
+			m.pool.Put(p)
+		}
+		m.release = m.release[:0]
+	}
 	for m.pending > 0 {
 		rec, err := m.rx.Poll(wait)
 		if err != nil {
 			return out, err
 		}
 		for _, r := range rec {
-			out = append(out, r.Payloads)
+			out = append(out, r.Payloads) // a copy (BatchReceiver.Poll): the pool buffers can go back
+			if m.rxHeld != nil {
+				for _, p := range m.rxHeld[r.BlockID] {
+					m.pool.Put(p)
+				}
+				delete(m.rxHeld, r.BlockID)
+			}
 		}
 		m.pending -= len(rec)
 		if !wait || len(rec) == 0 {

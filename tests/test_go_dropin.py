@@ -36,7 +36,9 @@ INCLUDE = os.path.join(ROOT, "include")
 HARNESS = os.path.join(ROOT, "tests", "c", "fec_go_harness.c")
 
 PATCH_TARGETS = {"manager.go.diff": "internal/fec/manager.go", "packet_packer.go.diff": "packet_packer.go",
-                 "connection.go.diff": "connection.go", "repair_queue.go.diff": "repair_queue.go"}
+                 "connection.go.diff": "connection.go", "repair_queue.go.diff": "repair_queue.go",
+                 "fec_source_symbol_frame.go.diff": "internal/wire/fec_source_symbol_frame.go",
+                 "fec_repair_frame.go.diff": "internal/wire/fec_repair_frame.go"}
 
 needs_ref = pytest.mark.skipif(not os.path.isdir(REF), reason="reference sources not present")
 
@@ -264,6 +266,11 @@ def test_protocol_and_wire_identifiers_exist_in_the_reference():
                 names |= set(re.findall(r"^\s*(?:type|func|const|var)\s+([A-Z]\w*)", src, re.M))
                 names |= set(re.findall(r"^\t([A-Z]\w*)\b", src, re.M))   # const / var block entries
         decl[pkg] = names
+    # and what the wire patches declare (the receive-side allocator hook)
+    for d in ("fec_source_symbol_frame.go.diff", "fec_repair_frame.go.diff"):
+        add = "\n".join(ln[1:] for ln in _read(os.path.join(PATCHES, d)).split("\n")
+                        if ln.startswith("+") and not ln.startswith("+++"))
+        decl["wire"] |= set(re.findall(r"^\s*(?:type|func|const|var)\s+([A-Z]\w*)", _strip_go(add), re.M))
     texts = [_strip_go(_read(p)) for p in _go_files()]
     texts += ["\n".join(ln[1:] for ln in _read(os.path.join(PATCHES, d)).split("\n") if ln.startswith("+"))
               for d in PATCH_TARGETS]
