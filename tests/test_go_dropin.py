@@ -6,7 +6,9 @@ What is committed (go/, INTEGRATION.md):
                          RepairPoller / RecoveredPoller interfaces (no tag)
   go/patches/*.diff      the hooks in the reference's own files: manager.go (scheme selection,
                          manager.go:50-94), packet_packer.go (:650-664, :1005-1011),
-                         connection.go (:218, :594-630, :1341, :1660-1666), repair_queue.go
+                         connection.go (:218, :594-630, :1341, :1660-1666), repair_queue.go,
+                         and the wire parsers' payload allocation (fec_source_symbol_frame.go:34,
+                         fec_repair_frame.go:36: the receive side of the registered pool)
 
 These tests tie the three descriptions of the boundary together, so none can drift unnoticed:
   * every diff applies to the reference's files (patch --dry-run, then for real);
