@@ -108,10 +108,11 @@ def test_stress_roundtrip(scheme, k, m, blocks, maxb, san):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["direct", "batch"])
+@pytest.mark.parametrize("mode", ["direct", "batch", "batchref"])
 def test_sanitized_harness_golden(golden, oracle, mode, tmp_path):
     import test_go_harness as h
-    cases = h._with_oracle_texts(h._golden_cases(golden), oracle) + h._synthetic_cases(oracle)
+    cases = (h._with_oracle_texts(h._golden_cases(golden), oracle) + h._synthetic_cases(oracle) +
+             h._empty_repair_cases(oracle)[0])
     h._check(h._run(binary("fec_go_harness_san"), cases, mode, tmp_path, env=san_env(gpu=True)), cases,
              texts=(mode == "direct"))
 

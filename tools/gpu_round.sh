@@ -28,7 +28,9 @@ grep -v amdgpu.ids "$O/config_bench.log"
 # host-resident Go-ABI throughput (one host thread, submit + poll), then counters for the
 # configs furthest from the roofline
 for c in "rs 8 4 65536 2048 1200 1" "rs 8 4 65536 2048 1200 8" "rs 20 10 32768 1024 1200 1" "rs 20 10 32768 1024 1200 8" "rs 2 1 131072 4096 1200 8" "xor 2 1 131072 4096 1200 8"; do
-    timeout -k 10 90 "$R/0xfec_amd/_bin/go_batch_bench" $c
+  for mode in copy ref; do   # ref: both sides by reference from the registered pool (RS)
+    timeout -k 10 90 "$R/0xfec_amd/_bin/go_batch_bench" $c $mode
+  done
 done > "$O/go_batch_bench.log" 2>&1
 cat "$O/go_batch_bench.log"
 tools/pmc_configs.sh "$TAG/counters" "rs1624,rs2030m,rs23"
