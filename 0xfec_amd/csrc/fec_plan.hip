@@ -24,26 +24,40 @@ constexpr uint32_t kPlanSortThreads = 256;
 constexpr uint32_t kGroupScratch = 160;   // per block: S[32] slots, O[32] erased, X[32] others, D|N[64]
 
 struct SortLds {
-    size_t prows, dall, scratch, pos, recs, total;
+    size_t prows, dall, scratch, pos, rank, recs, total;
 };
-__host__ __device__ inline SortLds sort_lds(uint32_t m, uint32_t k, uint32_t groups, uint32_t stride) {
+constexpr uint32_t kRankBins = 33;   // erasure counts 0..32
+// recs: the records of `win` segments of `groups` blocks, sorted together (sort window)
+__host__ __device__ inline SortLds sort_lds(uint32_t m, uint32_t k, uint32_t groups, uint32_t stride,
+                                            uint32_t win = 1) {
     SortLds l;
     l.prows = 768;
     l.dall = l.prows + (size_t)m * k;
     l.scratch = (l.dall + 32 + 15) & ~(size_t)15;
     l.pos = l.scratch + (size_t)groups * kGroupScratch;
-    l.recs = (l.pos + (size_t)groups * 4 + 15) & ~(size_t)15;
-    l.total = l.recs + (size_t)groups * stride;
+    // ranking scratch: per wave of records and bin, a count (then its prefix), and per bin a start
+    l.rank = l.pos + (size_t)groups * win * 4;
+    l.recs = (l.rank + ((size_t)(groups * win + 63) / 64 + 1) * kRankBins * 4 + 15) & ~(size_t)15;
+    l.total = l.recs + (size_t)groups * win * stride;
     return l;
 }
 
+// Segments sorted together (knob dec_psort = p): 1, or as many as make 128 * p blocks. A rebuild
+// wave spans two neighbouring records, and its row count is the larger of their two erasure
+// counts; sorted over 16 blocks (RS(16,24)) or 8 (RS(20,30)) neighbours still differ by about
+// one row.
+__host__ __device__ inline uint32_t sort_window(uint32_t groups, int psort) {
+    const uint32_t blocks = 128u * (uint32_t)(psort > 0 ? psort : 0);
+    return groups < blocks ? blocks / groups : 1u;
+}
+
 template <uint32_t LPB>
-__global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanArgs a, uint32_t segs) {
+__global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanArgs a, uint32_t segs, uint32_t win) {
     constexpr uint32_t G = kPlanSortThreads / LPB;   // blocks per workgroup segment
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     if (a.gate && *a.gate != a.gate_want) return;   // the classify kernel picked the direct path
     const PlanLayout lay = a.lay;
-    const SortLds L = sort_lds(a.m, a.k, G, lay.stride);
+    const SortLds L = sort_lds(a.m, a.k, G, lay.stride, win);
     uint8_t* s_exp = smem;
     uint8_t* s_log = smem + 512;
     uint8_t* s_prows = smem + L.prows;
@@ -64,7 +78,6 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
     uint8_t* X = S + 64;                                  // the other n - k shard indices
     uint8_t* Dt = S + 96;                                 // D_p (k bytes), then N_r (maxe bytes)
     uint8_t* Nt = Dt + k;
-    uint8_t* P = smem + L.recs + (size_t)gb * lay.stride;
     const uint32_t all = low_mask(n), kmask = low_mask(k);
     const uint32_t seg0 = blockIdx.x * segs;
     // the first segment's masks in flight while the tables stage
@@ -78,7 +91,9 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
         // the next segment's mask loads before this segment's work
         const uint32_t bn = b + G;
         mask_next = (sg + 1 < segs && bn < a.nblocks) ? a.masks[bn] : 0u;
-        __syncthreads();   // tables staged (first pass); the previous segment's records copied out
+        __syncthreads();   // tables staged (first pass); the previous window's records copied out
+        const uint32_t wl = sg % win;   // segment within the sort window
+        uint8_t* P = smem + L.recs + ((size_t)wl * G + gb) * lay.stride;
         const uint32_t mask = valid ? mask_in & all : all;   // past the batch: nothing to rebuild
         const uint32_t e = k - __popc(mask & kmask);
         int32_t st = a.max_out ? (int32_t)e : 0;
@@ -168,23 +183,54 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
             }
         }
         __syncthreads();
-        // storage order of the segment: erasure count descending, then block order (stable)
-        const uint32_t nseg = min(G, a.nblocks - base);
-        if (threadIdx.x < G) {
-            const uint32_t t = threadIdx.x;
-            const uint32_t kt = smem[L.recs + (size_t)t * lay.stride + lay.nout_off];
-            uint32_t pos = 0;
-            for (uint32_t j = 0; j < G; ++j) {
-                const uint32_t kj = smem[L.recs + (size_t)j * lay.stride + lay.nout_off];
-                pos += (kj > kt) || (kj == kt && j < t);
+        // at the end of a sort window (or of the work): storage order of the window's records,
+        // erasure count descending, then block order (stable)
+        const bool last = sg + 1 == segs || base + G >= a.nblocks;
+        if (wl + 1 < win && !last) continue;   // workgroup-uniform
+        const uint32_t nw = (wl + 1) * G;           // record slots of the window
+        const uint32_t base0 = base - wl * G;       // its first block
+        const uint32_t nvalid = min(nw, a.nblocks - base0);
+        // counting sort: position = records with a larger count + earlier records with the same
+        // count (past-the-batch groups: nothing to rebuild, last indices, so they rank last).
+        // Per wave of records and bin, a ballot gives the count and each record's rank in its wave.
+        const uint32_t U = a.maxe + 1, nwv = (nw + 63) / 64;
+        uint32_t* wc = reinterpret_cast<uint32_t*>(smem + L.rank);   // [nwv][U], then start[U]
+        uint32_t* start = wc + nwv * U;
+        const uint32_t lane = threadIdx.x & 63u;
+        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        for (uint32_t t = threadIdx.x; t < nwv * 64; t += kPlanSortThreads) {   // wave-uniform bound
+            const uint32_t v = t < nw ? smem[L.recs + (size_t)t * lay.stride + lay.nout_off] : kRankBins;
+            uint32_t rin = 0;
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint64_t bm = __ballot(v == u);
+                if (v == u) rin = (uint32_t)__popcll(bm & lt);
+                if (lane == 0) wc[(t >> 6) * U + u] = (uint32_t)__popcll(bm);
             }
-            s_pos[t] = pos;   // past-the-batch groups (nothing to rebuild, last indices) rank last
+            if (t < nw) s_pos[t] = rin;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            // bins in descending order; within a bin, waves in order: wc becomes each wave's offset
+            uint32_t acc = 0;
+            for (uint32_t u = U; u-- > 0;) {
+                start[u] = acc;
+                for (uint32_t w = 0; w < nwv; ++w) {
+                    const uint32_t c = wc[w * U + u];
+                    wc[w * U + u] = acc;
+                    acc += c;
+                }
+            }
+        }
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < nw; t += kPlanSortThreads) {
+            const uint32_t v = smem[L.recs + (size_t)t * lay.stride + lay.nout_off];
+            s_pos[t] += wc[(t >> 6) * U + v];
         }
         __syncthreads();
         const uint32_t per = lay.stride / 16;
         const uint4* src = reinterpret_cast<const uint4*>(smem + L.recs);
-        uint4* dst = reinterpret_cast<uint4*>(a.plans + (uint64_t)base * lay.stride);
-        for (uint32_t i = threadIdx.x; i < nseg * per; i += kPlanSortThreads) {
+        uint4* dst = reinterpret_cast<uint4*>(a.plans + (uint64_t)base0 * lay.stride);
+        for (uint32_t i = threadIdx.x; i < nvalid * per; i += kPlanSortThreads) {
             const uint32_t r = i / per, q = i - r * per;
             dst[(size_t)s_pos[r] * per + q] = src[i];
         }
@@ -201,9 +247,12 @@ hipError_t sorted_launch(const PlanArgs& a, hipStream_t s) {
     uint32_t segs = g_tune.dec_pseg > 0 ? (uint32_t)g_tune.dec_pseg : std::max<uint32_t>(1, nseg / 4096);
     if (a.gate) segs = 64;   // gated: a small grid, cheap to exit when the direct path was picked
     segs = std::min<uint32_t>(segs, 64);
+    // a window never spans two workgroups: segs a multiple of it
+    const uint32_t win = std::min<uint32_t>(sort_window(G, g_tune.dec_psort), 64);
+    if (win > 1) segs = (segs + win - 1) / win * win;
     const uint32_t grid = (nseg + segs - 1) / segs;
-    const size_t lds = sort_lds(a.m, a.k, G, a.lay.stride).total;
-    hipLaunchKernelGGL((rs_plan_sorted_kernel<LPB>), dim3(grid), dim3(kPlanSortThreads), lds, s, a, segs);
+    const size_t lds = sort_lds(a.m, a.k, G, a.lay.stride, win).total;
+    hipLaunchKernelGGL((rs_plan_sorted_kernel<LPB>), dim3(grid), dim3(kPlanSortThreads), lds, s, a, segs, win);
     return hipGetLastError();
 }
 

@@ -349,8 +349,10 @@ def test_rs_encode_kernel_variants_match_oracle(codec, oracle, torch, variant, k
 # 1 with the row-pipelined rolling rebuild for RS(16,24) too (dec_fixk 3; RS(20,30) has it by default);
 # 17 is 1 with the table-copy rebuild of fec_rebuild.hip (dec_fixk 4: PermTab rows copied from the
 # workgroup's 256-coefficient table, input addresses as per-block offsets), 18 and 19 the same with
-# rolling windows of 4 and 6 loads, 20 is 17 with the inputs split by 64-bit shifts
-@pytest.mark.parametrize("wave", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20])
+# rolling windows of 4 and 6 loads, 20 is 17 with the inputs split by 64-bit shifts, 21 is 17 with the
+# plan records sorted over 512-block windows (dec_psort 4; the rest over 128, the default), 22 is 17
+# with the records sorted per segment (dec_psort 0, the round-2 order)
+@pytest.mark.parametrize("wave", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22])
 @pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10)])
 # L = 1008 / 1017: shards of 63 / 64 chunks, the edge of the two-block wave slices (rolling window)
 @pytest.mark.parametrize("L", [513, 1008, 1017, 1202, 1436])
@@ -373,8 +375,9 @@ def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, 
                            dec_direct=1 if wave in (7, 13, 14, 15) else 0,
                            dec_direct_big=1 if wave in (13, 14, 15) else 0, dec_gate=1 if wave in (14, 15) else 0,
                            dec_gate_pm=1000 if wave == 15 else 10,
-                           dec_sorted=0 if wave == 8 else 1, dec_fixk={9: 1, 16: 3, 17: 4, 18: 4, 19: 4, 20: 4}.get(wave, 2),
+                           dec_sorted=0 if wave == 8 else 1, dec_fixk={9: 1, 16: 3, 17: 4, 18: 4, 19: 4, 20: 4, 21: 4, 22: 4}.get(wave, 2),
                            dec_win={18: 4, 19: 6}.get(wave, 0), dec_s64=1 if wave == 20 else 0,
+                           dec_psort={21: 4, 22: 0}.get(wave, 1),
                            dec_tier={10: 1, 11: 2, 12: 4}.get(wave, 0))
     try:
         out = torch.full((B, m, S), 0xEE, dtype=torch.uint8, device="cuda")
