@@ -91,8 +91,11 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
         // the next segment's mask loads before this segment's work
         const uint32_t bn = b + G;
         mask_next = (sg + 1 < segs && bn < a.nblocks) ? a.masks[bn] : 0u;
-        __syncthreads();   // tables staged (first pass); the previous window's records copied out
         const uint32_t wl = sg % win;   // segment within the sort window
+        // a window's first segment: tables staged (first pass), the previous window's records
+        // copied out; within a window a block group's scratch is its own lanes' (wave-local)
+        if (wl == 0) __syncthreads();
+        else wave_sync();
         uint8_t* P = smem + L.recs + ((size_t)wl * G + gb) * lay.stride;
         const uint32_t mask = valid ? mask_in & all : all;   // past the batch: nothing to rebuild
         const uint32_t e = k - __popc(mask & kmask);
@@ -182,11 +185,11 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
                 C[r * k + gl] = s_exp[v % 255u];
             }
         }
-        __syncthreads();
         // at the end of a sort window (or of the work): storage order of the window's records,
         // erasure count descending, then block order (stable)
         const bool last = sg + 1 == segs || base + G >= a.nblocks;
         if (wl + 1 < win && !last) continue;   // workgroup-uniform
+        __syncthreads();   // every record of the window written
         const uint32_t nw = (wl + 1) * G;           // record slots of the window
         const uint32_t base0 = base - wl * G;       // its first block
         const uint32_t nvalid = min(nw, a.nblocks - base0);
