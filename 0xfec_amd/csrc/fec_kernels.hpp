@@ -201,10 +201,10 @@ struct Tuning {
                               // (1, 2 or 4) in a small-register launch, the rest from a worklist (0: off)
     int dec_win = 0;          // fec_rebuild.hip: loads in flight per lane (4, 6, 8; 0: by code, RS(16,24) 4,
                               // RS(20,30) 6: 125 instead of 137 VGPRs, 4 instead of 3 waves/SIMD)
-    int dec_psort = 1;        // sorted plans: records sorted over windows of 128 * dec_psort blocks (0: one
-                              // segment of 256 / plan_lanes(k) blocks). 128: RS(16,24) -2.8 %, RS(20,30)
-                              // -6.9 % decode time (rebuild rows, and a cheaper ranking); 256 / 512 cost
-                              // the plan kernel residency (its LDS) more than the rebuild gains (r03y)
+    int dec_psort = 1;        // sorted plans: records sorted over windows of 64 * dec_psort blocks (0: one
+                              // segment of 256 / plan_lanes(k) blocks). 64 / 128 blocks: RS(20,30) -8 / -7 %
+                              // decode time, RS(16,24) -3 % (rebuild rows; a cheaper ranking); 256 / 512
+                              // cost the plan kernel residency (its LDS) more than the rebuild gains (r03y)
     int dec_s64 = 0;          // fec_rebuild.hip: input splits by 64-bit shifts (two dwords a shift)
     int host_gather = 1;      // FEC_HOST_PINNED reconstruct: the parity planes each block reads are pulled by
                               // the device straight from the caller's pinned buffer (0: whole span by DMA)

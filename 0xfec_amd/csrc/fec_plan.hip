@@ -42,12 +42,12 @@ __host__ __device__ inline SortLds sort_lds(uint32_t m, uint32_t k, uint32_t gro
     return l;
 }
 
-// Segments sorted together (knob dec_psort = p): 1, or as many as make 128 * p blocks. A rebuild
+// Segments sorted together (knob dec_psort = p): 1, or as many as make 64 * p blocks. A rebuild
 // wave spans two neighbouring records, and its row count is the larger of their two erasure
 // counts; sorted over 16 blocks (RS(16,24)) or 8 (RS(20,30)) neighbours still differ by about
 // one row.
 __host__ __device__ inline uint32_t sort_window(uint32_t groups, int psort) {
-    const uint32_t blocks = 128u * (uint32_t)(psort > 0 ? psort : 0);
+    const uint32_t blocks = 64u * (uint32_t)(psort > 0 ? psort : 0);
     return groups < blocks ? blocks / groups : 1u;
 }
 

@@ -350,7 +350,7 @@ def test_rs_encode_kernel_variants_match_oracle(codec, oracle, torch, variant, k
 # 17 is 1 with the table-copy rebuild of fec_rebuild.hip (dec_fixk 4: PermTab rows copied from the
 # workgroup's 256-coefficient table, input addresses as per-block offsets), 18 and 19 the same with
 # rolling windows of 4 and 6 loads, 20 is 17 with the inputs split by 64-bit shifts, 21 is 17 with the
-# plan records sorted over 512-block windows (dec_psort 4; the rest over 128, the default), 22 is 17
+# plan records sorted over 256-block windows (dec_psort 4; the rest over 64, the default), 22 is 17
 # with the records sorted per segment (dec_psort 0, the round-2 order)
 @pytest.mark.parametrize("wave", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22])
 @pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10)])

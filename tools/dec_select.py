@@ -75,7 +75,7 @@ def main():
         for w in (2, 3):
             variants["table-copy rebuild (fixk 4) wpc%d" % w] = dict(D, dec_fixk=4, dec_wpc=w)
         for ps in (0, 2, 4):
-            variants["table-copy rebuild (fixk 4), plans sorted over %d blocks" % (128 * ps)] = dict(D, dec_fixk=4, dec_psort=ps)
+            variants["table-copy rebuild (fixk 4), plans sorted over %d blocks" % (64 * ps)] = dict(D, dec_fixk=4, dec_psort=ps)
         for w in (3, 4):
             variants["rolling window wpc%d" % w] = dict(D, dec_wpc=w)
         for w in (2, 3):

@@ -6,7 +6,7 @@ O=$R/gpurun_out/r03y
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 for spec in "16 8 8" "20 10 10"; do
-  for ps in 0 1; do
+  for ps in -1 1; do
     set -- $spec
     timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/p_$1_$ps" -o run -- \
       python3 "$R/tools/plan_sort_probe.py" $1 $2 $3 $ps > "$O/p_$1_$ps.log" 2>&1
