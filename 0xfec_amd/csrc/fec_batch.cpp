@@ -421,9 +421,11 @@ Error BatchEncoder::retire(Set& s) {
     s.inFlight = false;
     bool raw_only = !s.blocks.empty();
     for (const Pending& p : s.blocks) raw_only = raw_only && !p.q;
-    if (raw_only) {   // hand the blocks out of h_out in place (PeekRaw); an older holder goes first
-        const int idx = (int)(&s - sets_);
-        if (holding_ >= 0 && holding_ != idx) spill(sets_[holding_]);
+    const int idx = (int)(&s - sets_);
+    // an older holding set's blocks go out before any of this set's: raw_ only ever holds blocks
+    // older than a holding set's (PeekRaw serves raw_ first)
+    if (holding_ >= 0 && holding_ != idx) spill(sets_[holding_]);
+    if (raw_only) {   // hand the blocks out of h_out in place (PeekRaw)
         holding_ = idx;
         s.rawNext = 0;
         return Error::nil();
@@ -464,17 +466,22 @@ bool BatchEncoder::pump(size_t* blocks) {
             ++it;
             continue;
         }
-        std::lock_guard<std::mutex> lk(it->tok->mu);   // the queue cannot be freed meanwhile
-        // a freed or closed queue drops its frames, as the reference's closed connection would
-        if (it->tok->alive && !it->q->Closed()) {
-            if (it->q->Len() + it->payloads.size() > it->q->MaxLen()) {
-                held.push_back(it->q);
-                ++it;
-                continue;
+        // Our own reference to the token: when the queue is gone, the backlog entry may hold the
+        // last one, and erasing the entry must not free the mutex this scope still holds.
+        const std::shared_ptr<QueueToken> tok = it->tok;
+        {
+            std::lock_guard<std::mutex> lk(tok->mu);   // the queue cannot be freed meanwhile
+            // a freed or closed queue drops its frames, as the reference's closed connection would
+            if (tok->alive && !it->q->Closed()) {
+                if (it->q->Len() + it->payloads.size() > it->q->MaxLen()) {
+                    held.push_back(it->q);
+                    ++it;
+                    continue;
+                }
+                for (size_t j = 0; j < it->payloads.size(); ++j)
+                    (void)it->q->Add(RepairFrame{it->id, (ParityID)j, it->payloads[j]});
+                if (blocks) ++*blocks;
             }
-            for (size_t j = 0; j < it->payloads.size(); ++j)
-                (void)it->q->Add(RepairFrame{it->id, (ParityID)j, it->payloads[j]});
-            if (blocks) ++*blocks;
         }
         it = backlog_.erase(it);
     }

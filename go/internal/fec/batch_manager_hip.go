@@ -118,6 +118,7 @@ var (
 	_ RepairPoller     = &batchManager{}
 	_ RecoveredPoller  = &batchManager{}
 	_ PayloadAllocator = &batchManager{}
+	_ Closer           = &batchManager{}
 )
 
 func newBatchManager(id protocol.DecoderFECScheme, k, m int, send bool) (*batchManager, error) {
@@ -371,4 +372,49 @@ func (m *batchManager) PollRecovered(wait bool) ([][]byte, error) {
 	return out, nil
 }
 
-func (m *batchManager) RecoveryPending() bool { return m.pending > 0 }
+// RecoveryPending: staged blocks whose data has not been handed out, or received pool buffers
+// waiting to go back (PollRecovered returns them even when nothing is staged, so a lossless
+// stream does not drain the pool).
+func (m *batchManager) RecoveryPending() bool { return m.pending > 0 || len(m.release) > 0 }
+
+// Close is the connection's teardown (go/patches/connection.go.diff, after the run loop ends):
+// the library encoder / decoder is freed first, which waits for a batch still in flight (the
+// device may be reading pool buffers by reference), then every pool buffer this manager still
+// holds goes back: blocks submitted but not polled (held, rxHeld), buffers awaiting release, and
+// the payloads of blocks that never completed. Buffers from the heap are ignored by Put.
+func (m *batchManager) Close() {
+	if m.tx != nil {
+		m.tx.Close()
+	}
+	if m.rx != nil {
+		m.rx.Close()
+	}
+	if m.pool == nil {
+		return
+	}
+	for id, ps := range m.held {
+		for _, p := range ps {
+			m.pool.Put(p)
+		}
+		delete(m.held, id)
+	}
+	for id, ps := range m.rxHeld {
+		for _, p := range ps {
+			m.pool.Put(p)
+		}
+		delete(m.rxHeld, id)
+	}
+	for _, p := range m.release {
+		m.pool.Put(p)
+	}
+	m.release = nil
+	for id, bS := range m.blockStatuses {
+		if bS.block != nil {
+			for _, p := range blockPayloads(bS.block) {
+				m.pool.Put(p)
+			}
+		}
+		delete(m.blockStatuses, id)
+	}
+	m.pending = 0
+}

@@ -34,3 +34,11 @@ type RecoveredPoller interface {
 type PayloadAllocator interface {
 	SourcePayloadBuffer() []byte
 }
+
+// Closer is a Sender or Receiver that holds device state and buffers of the process-wide packet
+// pool (the GPU batch managers). The connection calls Close once its run loop has ended
+// (go/patches/connection.go.diff); the reference managers hold only Go memory and do not
+// implement it.
+type Closer interface {
+	Close()
+}

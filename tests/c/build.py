@@ -4,7 +4,8 @@
   fec_go_stress         many-block round trips through include/fec_go.h
   fec_go_threads        encoders / decoders created on one thread, driven concurrently from
                         others (Go's goroutine-to-thread migration), checked against the oracle
-  *_san                 the same two linked against lib0xfec_hip_san.so: the library's host
+  fec_batch_lifetime    a connection's queue freed while the batch codec still owes it blocks
+  *_san                 the same programs linked against lib0xfec_hip_san.so: the library's host
                         C++ (C-ABI, scheme/batch layers, wire codecs, Go ABI) compiled with
                         AddressSanitizer + UBSan on the host side only (-Xarch_host), kernels
                         unchanged (device code is never instrumented)
@@ -86,7 +87,7 @@ def build():
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
     extra = {"fec_go_threads": (["-pthread"], ["-L", oracle_dir, "-loracle", "-Wl,-rpath," + oracle_dir],
                                 [os.path.join(oracle_dir, "liboracle.so")])}
-    for prog in ("fec_go_harness", "fec_go_stress", "fec_go_threads"):
+    for prog in ("fec_go_harness", "fec_go_stress", "fec_go_threads", "fec_batch_lifetime"):
         src = os.path.join(here, prog + ".c")
         cflags, libs, deps = extra.get(prog, ([], [], []))
         exe = os.path.join(BIN, prog)

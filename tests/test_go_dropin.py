@@ -335,13 +335,17 @@ def test_patch_identifiers_are_declared():
     for ident in ("newHIPSender", "newHIPReceiver"):
         assert ident in mgr and ident in fec_decl
     quic = _strip_go(added["packet_packer.go.diff"] + "\n" + added["connection.go.diff"])
+    ref_fec = os.path.join(REF, "internal", "fec")
+    for f in os.listdir(ref_fec):   # the reference package's own declarations (fec.Sender, ...)
+        if f.endswith(".go") and not f.endswith("_test.go"):
+            fec_decl |= _decls(_strip_go(_read(os.path.join(ref_fec, f))))
     for ident in set(re.findall(r"\bfec\.([A-Z]\w*)", quic)):
-        assert ident in fec_decl, "fec.%s used by a hook but not declared in go/internal/fec" % ident
+        assert ident in fec_decl, "fec.%s used by a hook but not declared in internal/fec" % ident
     for meth in set(re.findall(r"poller\.(\w+)\(", quic)):
         assert meth in fec_decl, "poller.%s is not a method of the poller interfaces (fec_poll.go)" % meth
     assert "Room" in _decls(_strip_go(added["repair_queue.go.diff"]))
     assert re.search(r"repairQueue\.Room\(\)", quic)
-    for ident in ("pollRepairFrames", "handleRecoveredFEC"):
+    for ident in ("pollRepairFrames", "handleRecoveredFEC", "closeFEC"):
         assert re.search(r"func \(\w \*\w+\) %s\(" % ident, quic)
 
 

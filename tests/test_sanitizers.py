@@ -164,3 +164,23 @@ def test_go_abi_concurrent_connections(san):
                        env=san_env(gpu=True) if san else None)
     assert p.returncode == 0, p.stderr[-4000:]
     assert p.stdout.startswith("ok connections=4 blocks=960")
+
+
+def test_batch_lifetime_fails_loudly_without_device(fec):
+    if fec.device_count() > 0:
+        pytest.skip("a GPU is present")
+    p = subprocess.run([binary("fec_batch_lifetime_san")], capture_output=True, text=True, timeout=60,
+                       env=san_env(gpu=False))
+    assert p.returncode == 1 and "no HIP device" in p.stderr, p.stderr[-2000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("san", [False, True], ids=["plain", "asan_ubsan"])
+def test_queue_freed_while_blocks_owed(san):
+    """A RepairQueue freed while its frames sit in the encoder's backlog or its batch is in flight,
+    and a RecoveredQueue freed while its blocks are in flight: poll and drain drop those blocks
+    and touch nothing freed (the backlog entry held the last token reference)."""
+    exe = binary("fec_batch_lifetime_san" if san else "fec_batch_lifetime")
+    p = subprocess.run([exe], capture_output=True, text=True, timeout=110, env=san_env(gpu=True) if san else None)
+    assert p.returncode == 0, p.stderr[-4000:]
+    assert p.stdout.startswith("ok backlog inflight mixed decoder")
