@@ -76,6 +76,9 @@ lib.fec_xor_reconstruct_batch.argtypes = [_vp, _i, _sz, _sz, _vp, _sz, _vp, _sz,
 _u64 = ctypes.c_uint64
 lib.fec_synth_data.argtypes = [_vp, _u64, _u64, _sz, _i, _sz, _vp, _sz, _sz]
 lib.fec_synth_single_erasures.argtypes = [_vp, _u64, _u64, _sz, _i, _i, _vp, _vp]
+lib.fec_probe_encode_traffic.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz]
+lib.fec_probe_recover_traffic.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _vp, _vp, _sz]
+lib.fec_probe_link.argtypes = [_vp, _sz, _i, ctypes.POINTER(ctypes.c_double)]
 
 
 class FecError(RuntimeError):
@@ -293,6 +296,22 @@ class Codec:
     def synth_single_erasures(self, seed, first_block, nblocks, k, m, masks, erased=None):
         return _check(lib.fec_synth_single_erasures(self._h, seed, first_block, nblocks, k, m, masks, erased),
                       "fec_synth_single_erasures")
+
+    # ---- traffic twins of the headline kernels (include/fec_probe.h; measurement only)
+    def probe_encode_traffic_raw(self, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss):
+        return _check(lib.fec_probe_encode_traffic(self._h, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss),
+                      "fec_probe_encode_traffic")
+
+    def probe_recover_traffic_raw(self, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss, masks, out, out_bs):
+        return _check(lib.fec_probe_recover_traffic(self._h, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss,
+                                                    masks, out, out_bs), "fec_probe_recover_traffic")
+
+    def probe_link(self, nbytes=512 << 20, reps=3):
+        """{h2d, d2h, duplex_each} GB/s of pinned hipMemcpyAsync on this ctx's device."""
+        out = (ctypes.c_double * 3)()
+        _check(lib.fec_probe_link(self._h, nbytes, reps, out), "fec_probe_link")
+        return {"bytes": nbytes, "h2d_GBps": round(out[0], 2), "d2h_GBps": round(out[1], 2),
+                "duplex_each_GBps": round(out[2], 2)}
 
     def xor_encode(self, k, shards, shard_len=None):
         B, n, S = _shape3(shards)

@@ -91,10 +91,9 @@ struct Work {
     }
 };
 
-// One staging set of the host-resident path (pinned host + device buffers, a stream, an event):
-// with two, chunk c+1 is staged and copied up while chunk c is coded and copied down.
+// One staging set of the host-resident path: pinned host and device buffers for one chunk of
+// blocks, and the events that carry that chunk through the pipeline's streams (HostPipe).
 struct HostSet {
-    Work w;                      // scratch of the kernels on this set's stream
     uint8_t* h_in = nullptr;
     uint8_t* h_out = nullptr;
     uint8_t* d_in = nullptr;
@@ -103,10 +102,26 @@ struct HostSet {
     uint32_t* d_masks = nullptr;
     int32_t* h_status = nullptr;
     int32_t* d_status = nullptr;
-    uint8_t* d_raw = nullptr;   // FEC_HOST_PINNED: the caller's span, copied linearly (fec_pack.hip)
-    size_t in_cap = 0, out_cap = 0, blk_cap = 0, raw_cap = 0;
-    hipStream_t s = nullptr;
-    hipEvent_t done = nullptr;
+    uint8_t* d_raw_in = nullptr;    // FEC_HOST_PINNED: the caller's span, copied linearly (fec_pack.hip)
+    uint8_t* d_raw_out = nullptr;   // FEC_HOST_PINNED: the packed image of the outputs, copied down linearly
+    size_t in_cap = 0, out_cap = 0, blk_cap = 0, raw_in_cap = 0, raw_out_cap = 0;
+    hipEvent_t up_done = nullptr;     // its H2D copies have landed
+    hipEvent_t k_done = nullptr;      // its kernels are done (the device inputs are free)
+    hipEvent_t down_done = nullptr;   // its D2H copies have landed (the set is free)
+};
+
+// The host-resident pipeline. Chunk c of a call uses set c % kHostSets and moves through three
+// streams in order: H2D copies on `up`, kernels on `comp`, D2H copies on `down`, ordered by the
+// set's events alone. PCIe's two directions and the kernels of different chunks therefore overlap,
+// and the up direction (the larger one on every path) never waits for the host: the host blocks only
+// to reuse a set, on its chunk kHostSets back, and at the end of a call. Measured on one MI355X
+// (tools/pcie_duplex_probe.hip, profiles/r04/pcie_duplex_probe_r04a.log): H2D 57.5 GB/s, D2H 57.0,
+// both at once 48.9 each way; this shape with 64 MiB chunks moved 53.7 GB/s up and 26.8 down.
+constexpr int kHostSets = 3;
+struct HostPipe {
+    hipStream_t up = nullptr, comp = nullptr, down = nullptr;
+    Work w;   // scratch of the kernels on comp
+    HostSet set[kHostSets];
 };
 
 struct fec_ctx {
@@ -125,7 +140,7 @@ struct fec_ctx {
     size_t masks_cap = 0;
     int grid_cache[3][6] = {};
     int ncu = 256;           // compute units of the device
-    HostSet hs[2];           // host-resident path: two staging sets, each with its own stream
+    HostPipe pipe;           // host-resident path (FEC_HOST / FEC_HOST_PINNED)
     hipEvent_t handoff = nullptr;   // orders a newly set stream after the previous one
 };
 
@@ -599,13 +614,13 @@ static int check_device_layout(const void* p, size_t bs, size_t ss, size_t len) 
 // ---------------------------------------------------------------- host-resident path
 // FEC_HOST (pageable host memory): each chunk of blocks is staged by the calling thread into a
 // pinned buffer, copied up with one hipMemcpyAsync, coded, copied down with one, and its results
-// copied out once the set comes round again. FEC_HOST_PINNED (the caller's buffers are pinned or
-// registered): no staging copies at all; each shard column is moved with one 2D hipMemcpyAsync
-// straight between the caller's layout and the device staging. Only what the code needs crosses
-// PCIe: encode sends the k data shards and returns the m parity shards; reconstruct sends the data
-// shards and the parity planes up to the highest parity any block of the chunk reads, and
-// returns only the rebuilt shards. Two staging sets alternate on two streams, so the staging
-// copies and PCIe transfers of one chunk overlap the kernels of the other.
+// copied out once its set comes round again. FEC_HOST_PINNED (the caller's buffers are pinned or
+// registered): no staging copies; the caller's span of a chunk goes up in one linear DMA and is
+// repacked into 16-byte slots on the device (or one 2D DMA per shard column when the span is
+// sparse), and packed outputs come down the same way. Only what the code needs crosses PCIe:
+// encode sends the k data shards and returns the m parity shards; reconstruct sends the data
+// shards and the parity planes its blocks read, and returns only the rebuilt shards. Chunks run
+// through HostPipe's three streams (up / kernels / down), kHostSets at a time.
 
 static size_t host_chunk_blocks(size_t bytes_per_block) {
     if (fk::g_tune.host_chunk > 0) return (size_t)fk::g_tune.host_chunk;   // tests: many small chunks
@@ -627,13 +642,13 @@ static void parallel_for(size_t n, F fn) {
     for (auto& t : th) t.join();
 }
 
-static int host_raw_grow(HostSet& s, size_t bytes) {
-    if (bytes <= s.raw_cap) return FEC_OK;
-    if (s.d_raw) HIP_TRY(hipFree(s.d_raw));
-    s.d_raw = nullptr;
-    s.raw_cap = 0;
-    HIP_TRY(hipMalloc(&s.d_raw, bytes));
-    s.raw_cap = bytes;
+static int grow_dev(uint8_t** p, size_t* cap, size_t bytes) {
+    if (bytes <= *cap) return FEC_OK;
+    if (*p) HIP_TRY(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    HIP_TRY(hipMalloc(p, bytes));
+    *cap = bytes;
     return FEC_OK;
 }
 
@@ -647,89 +662,162 @@ static bool dense_span(size_t nb, size_t cols, size_t bs, size_t ss, size_t len)
     return span_bytes(nb, cols, bs, ss, len) * 4 <= nb * cols * len * 5;
 }
 
-// Caller's columns [0, cols) of nb blocks into the device stage [nb][st_bs/st_ss]: one linear DMA
-// of the span of all span_cols >= cols columns and a device repack when that span is dense (a
-// few unneeded columns ride along: one linear DMA beats narrow 2D rows), else one 2D DMA per
-// column.
-static int pinned_up(HostSet& s, uint8_t* stage, size_t st_bs, size_t st_ss, const uint8_t* src, size_t bs, size_t ss,
-                     size_t nb, size_t cols, size_t len, uint8_t* raw, size_t span_cols) {
-    if (dense_span(nb, span_cols, bs, ss, len)) {
-        HIP_TRY(hipMemcpyAsync(raw, src, span_bytes(nb, span_cols, bs, ss, len), hipMemcpyHostToDevice, s.s));
-        HIP_TRY(fk::launch_span_to_stage(stage, st_bs, st_ss, raw, bs, ss, (uint32_t)nb, (uint32_t)cols, (uint32_t)len,
-                                         s.s));
+// Caller's columns [0, cols) of nb blocks toward the device stage [nb][st_bs/st_ss], on stream
+// `up`: when the span of all span_cols >= cols columns is dense, one linear DMA of it into `raw`
+// (a few unneeded columns ride along: one linear DMA beats narrow 2D rows) and *repack = true (the
+// kernel stream then runs pinned_repack); else one 2D DMA per column straight into the stage.
+static int pinned_up(hipStream_t up, uint8_t* stage, size_t st_bs, size_t st_ss, const uint8_t* src, size_t bs,
+                     size_t ss, size_t nb, size_t cols, size_t len, uint8_t* raw, size_t span_cols, bool* repack) {
+    *repack = dense_span(nb, span_cols, bs, ss, len);
+    if (*repack) {
+        HIP_TRY(hipMemcpyAsync(raw, src, span_bytes(nb, span_cols, bs, ss, len), hipMemcpyHostToDevice, up));
         return FEC_OK;
     }
     for (size_t j = 0; j < cols; ++j)
-        HIP_TRY(hipMemcpy2DAsync(stage + j * st_ss, st_bs, src + j * ss, bs, len, nb, hipMemcpyHostToDevice, s.s));
+        HIP_TRY(hipMemcpy2DAsync(stage + j * st_ss, st_bs, src + j * ss, bs, len, nb, hipMemcpyHostToDevice, up));
     return FEC_OK;
 }
 
-// Device stage [nb][st_bs/st_ss] columns back to the caller: for a packed caller layout (no
-// bytes between shards) a device repack and one linear DMA; else one 2D DMA per column, which
-// writes exactly len bytes per shard.
-static int pinned_down(HostSet& s, uint8_t* dst, size_t bs, size_t ss, const uint8_t* stage, size_t st_bs,
-                       size_t st_ss, size_t nb, size_t cols, size_t len, uint8_t* raw) {
-    if (ss == len && bs == cols * len) {
-        HIP_TRY(fk::launch_stage_to_packed(raw, stage, st_bs, st_ss, (uint32_t)nb, (uint32_t)cols, (uint32_t)len, s.s));
-        HIP_TRY(hipMemcpyAsync(dst, raw, nb * cols * len, hipMemcpyDeviceToHost, s.s));
+// The caller layout's outputs are packed (no bytes between shards): the kernel stream packs the
+// device stage into one image that goes down in one linear DMA.
+static bool packed_out(size_t bs, size_t ss, size_t cols, size_t len) { return ss == len && bs == cols * len; }
+
+// Device stage [nb][st_bs/st_ss] columns back to the caller, on stream `down`: the packed image
+// (packed_out) in one linear DMA, else one 2D DMA per column, which writes exactly len bytes per
+// shard.
+static int pinned_down(hipStream_t down, uint8_t* dst, size_t bs, size_t ss, const uint8_t* stage, size_t st_bs,
+                       size_t st_ss, size_t nb, size_t cols, size_t len, const uint8_t* raw) {
+    if (packed_out(bs, ss, cols, len)) {
+        HIP_TRY(hipMemcpyAsync(dst, raw, nb * cols * len, hipMemcpyDeviceToHost, down));
         return FEC_OK;
     }
     for (size_t j = 0; j < cols; ++j)
-        HIP_TRY(hipMemcpy2DAsync(dst + j * ss, bs, stage + j * st_ss, st_bs, len, nb, hipMemcpyDeviceToHost, s.s));
+        HIP_TRY(hipMemcpy2DAsync(dst + j * ss, bs, stage + j * st_ss, st_bs, len, nb, hipMemcpyDeviceToHost, down));
     return FEC_OK;
 }
 
-static int host_set_grow(fec_ctx* ctx, HostSet& s, size_t in_bytes, size_t out_bytes, size_t blocks) {
-    if (!s.s) {
-        HIP_TRY(hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
-    }
-    if (in_bytes > s.in_cap) {
-        if (s.h_in) HIP_TRY(hipHostFree(s.h_in));
-        if (s.d_in) HIP_TRY(hipFree(s.d_in));
-        s.h_in = s.d_in = nullptr;
-        s.in_cap = 0;
-        HIP_TRY(hipHostMalloc(&s.h_in, in_bytes, hipHostMallocDefault));
-        HIP_TRY(hipMalloc(&s.d_in, in_bytes));
-        s.in_cap = in_bytes;
-    }
-    if (out_bytes > s.out_cap) {
-        if (s.h_out) HIP_TRY(hipHostFree(s.h_out));
-        if (s.d_out) HIP_TRY(hipFree(s.d_out));
-        s.h_out = s.d_out = nullptr;
-        s.out_cap = 0;
-        HIP_TRY(hipHostMalloc(&s.h_out, out_bytes, hipHostMallocDefault));
-        HIP_TRY(hipMalloc(&s.d_out, out_bytes));
-        s.out_cap = out_bytes;
-    }
-    if (blocks > s.blk_cap) {
-        for (void* q : {(void*)s.h_masks, (void*)s.h_status})
-            if (q) HIP_TRY(hipHostFree(q));
-        for (void* q : {(void*)s.d_masks, (void*)s.d_status})
-            if (q) HIP_TRY(hipFree(q));
-        s.h_masks = s.d_masks = nullptr;
-        s.h_status = s.d_status = nullptr;
-        s.blk_cap = 0;
-        HIP_TRY(hipHostMalloc(&s.h_masks, blocks * 4, hipHostMallocDefault));
-        HIP_TRY(hipHostMalloc(&s.h_status, blocks * 4, hipHostMallocDefault));
-        HIP_TRY(hipMalloc(&s.d_masks, blocks * 4));
-        HIP_TRY(hipMalloc(&s.d_status, blocks * 4));
-        s.blk_cap = blocks;
-    }
-    (void)ctx;
+static int host_pipe_init(HostPipe& p) {
+    if (p.up) return FEC_OK;
+    for (hipStream_t* q : {&p.up, &p.comp, &p.down}) HIP_TRY(hipStreamCreateWithFlags(q, hipStreamNonBlocking));
+    for (HostSet& s : p.set)
+        for (hipEvent_t* e : {&s.up_done, &s.k_done, &s.down_done})
+            HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
     return FEC_OK;
 }
 
-// Run `fn` with the ctx's kernels enqueued on the host-path set's stream, with that set's scratch.
+// Buffers of every set for chunks of in / out staged bytes and `blocks` blocks (a call grows them
+// before its first chunk, when no chunk of the pipe is in flight).
+static int host_pipe_grow(HostPipe& p, size_t in_bytes, size_t out_bytes, size_t blocks) {
+    int rc;
+    if ((rc = host_pipe_init(p))) return rc;
+    for (HostSet& s : p.set) {
+        if (in_bytes > s.in_cap) {
+            if (s.h_in) HIP_TRY(hipHostFree(s.h_in));
+            if (s.d_in) HIP_TRY(hipFree(s.d_in));
+            s.h_in = s.d_in = nullptr;
+            s.in_cap = 0;
+            HIP_TRY(hipHostMalloc(&s.h_in, in_bytes, hipHostMallocDefault));
+            HIP_TRY(hipMalloc(&s.d_in, in_bytes));
+            s.in_cap = in_bytes;
+        }
+        if (out_bytes > s.out_cap) {
+            if (s.h_out) HIP_TRY(hipHostFree(s.h_out));
+            if (s.d_out) HIP_TRY(hipFree(s.d_out));
+            s.h_out = s.d_out = nullptr;
+            s.out_cap = 0;
+            HIP_TRY(hipHostMalloc(&s.h_out, out_bytes, hipHostMallocDefault));
+            HIP_TRY(hipMalloc(&s.d_out, out_bytes));
+            s.out_cap = out_bytes;
+        }
+        if (blocks > s.blk_cap) {
+            for (void* q : {(void*)s.h_masks, (void*)s.h_status})
+                if (q) HIP_TRY(hipHostFree(q));
+            for (void* q : {(void*)s.d_masks, (void*)s.d_status})
+                if (q) HIP_TRY(hipFree(q));
+            s.h_masks = s.d_masks = nullptr;
+            s.h_status = s.d_status = nullptr;
+            s.blk_cap = 0;
+            HIP_TRY(hipHostMalloc(&s.h_masks, blocks * 4, hipHostMallocDefault));
+            HIP_TRY(hipHostMalloc(&s.h_status, blocks * 4, hipHostMallocDefault));
+            HIP_TRY(hipMalloc(&s.d_masks, blocks * 4));
+            HIP_TRY(hipMalloc(&s.d_status, blocks * 4));
+            s.blk_cap = blocks;
+        }
+    }
+    return FEC_OK;
+}
+
+// Run `fn` with the ctx's kernels enqueued on the pipe's kernel stream, with its scratch.
 template <class F>
-static int on_stream(fec_ctx* ctx, HostSet& hs, F fn) {
+static int on_pipe(fec_ctx* ctx, F fn) {
     hipStream_t keep = ctx->stream;
     Work* keep_w = ctx->work;
-    ctx->stream = hs.s;
-    ctx->work = &hs.w;
+    ctx->stream = ctx->pipe.comp;
+    ctx->work = &ctx->pipe.w;
     const int rc = fn();
     ctx->stream = keep;
     ctx->work = keep_w;
+    return rc;
+}
+
+// One chunk of a host-path call: blocks [b0, b0 + nb) and what its stages decided.
+struct HostChunk {
+    size_t b0 = 0, nb = 0;
+    bool live = false;
+    bool repack = false;      // pinned: the data span came up raw, the kernel stream repacks it
+    size_t planes = 0;        // reconstruct: parity planes [0, planes) reach the device
+    uint32_t gather = 0;      // reconstruct, pinned: planes the device pulls itself (bit r)
+    size_t slots = 1;         // reconstruct: output slots per block
+};
+
+// Chunks of `chunk` blocks through the pipe. up(s, ch): host staging, then the H2D copies on
+// p.up; kern(s, ch): kernels on p.comp; down(s, ch): D2H copies on p.down; finish(s, ch) on the
+// host once the chunk's copies have landed. On any failure every stream is drained before the
+// error returns, so no set is left in flight.
+template <class Up, class Kern, class Down, class Finish>
+static int host_pipeline(fec_ctx* ctx, size_t nblocks, size_t chunk, Up up, Kern kern, Down down, Finish finish) {
+    HostPipe& p = ctx->pipe;
+    HostChunk pend[kHostSets];
+    auto run = [&]() -> int {
+        int rc;
+        size_t c = 0;
+        for (size_t b0 = 0; b0 < nblocks; b0 += chunk, ++c) {
+            const int i = (int)(c % kHostSets);
+            HostSet& s = p.set[i];
+            if (pend[i].live) {   // the set's chunk kHostSets back: all of its buffers are free after this
+                HIP_TRY(hipEventSynchronize(s.down_done));
+                pend[i].live = false;
+                if ((rc = finish(s, pend[i]))) return rc;
+            }
+            HostChunk ch;
+            ch.b0 = b0;
+            ch.nb = std::min(chunk, nblocks - b0);
+            if ((rc = up(s, ch))) return rc;
+            HIP_TRY(hipEventRecord(s.up_done, p.up));
+            HIP_TRY(hipStreamWaitEvent(p.comp, s.up_done, 0));
+            if ((rc = kern(s, ch))) return rc;
+            HIP_TRY(hipEventRecord(s.k_done, p.comp));
+            HIP_TRY(hipStreamWaitEvent(p.down, s.k_done, 0));
+            if ((rc = down(s, ch))) return rc;
+            HIP_TRY(hipEventRecord(s.down_done, p.down));
+            ch.live = true;
+            pend[i] = ch;
+        }
+        for (size_t t = 0; t < (size_t)kHostSets; ++t) {   // oldest chunk first
+            const int i = (int)((c + t) % kHostSets);
+            if (!pend[i].live) continue;
+            HIP_TRY(hipEventSynchronize(p.set[i].down_done));
+            pend[i].live = false;
+            if ((rc = finish(p.set[i], pend[i]))) return rc;
+        }
+        return FEC_OK;
+    };
+    const int rc = run();
+    if (rc) {
+        for (hipStream_t q : {p.up, p.comp, p.down})
+            if (q) (void)hipStreamSynchronize(q);
+        (void)hipGetLastError();
+    }
     return rc;
 }
 
@@ -738,68 +826,69 @@ static int host_encode(fec_ctx* ctx, Code* code, int k, int m, size_t len, size_
                        size_t dbs, uint8_t* parity, size_t pbs, size_t ss, bool pinned) {
     const size_t ssd = round16(len);
     const size_t chunk = std::min(nblocks, host_chunk_blocks((size_t)k * ssd));
-    struct Pending {
-        size_t b0 = 0, nb = 0;
-        bool live = false;
-    } pend[2];
+    HostPipe& p = ctx->pipe;
     int rc;
-    auto finish = [&](int i) -> int {
-        HostSet& s = ctx->hs[i];
-        HIP_TRY(hipEventSynchronize(s.done));
-        if (!pinned)
-            parallel_for(pend[i].nb, [&](size_t lo, size_t hi) {
-                for (size_t b = lo; b < hi; ++b)
-                    for (int r = 0; r < m; ++r)
-                        memcpy(parity + (pend[i].b0 + b) * pbs + r * ss, s.h_out + (b * m + r) * ssd, len);
-            });
-        pend[i].live = false;
+    if ((rc = host_pipe_grow(p, chunk * k * ssd, chunk * m * ssd, 1))) return rc;
+    const bool pack = pinned && packed_out(pbs, ss, (size_t)m, len);
+    if (pinned)
+        for (HostSet& s : p.set) {
+            if ((rc = grow_dev(&s.d_raw_in, &s.raw_in_cap, span_bytes(chunk, k, dbs, ss, len) + 16))) return rc;
+            if (pack && (rc = grow_dev(&s.d_raw_out, &s.raw_out_cap, chunk * m * len + 16))) return rc;
+        }
+    auto up = [&](HostSet& s, HostChunk& ch) -> int {
+        if (pinned)
+            return pinned_up(p.up, s.d_in, (size_t)k * ssd, ssd, data + ch.b0 * dbs, dbs, ss, ch.nb, k, len, s.d_raw_in,
+                             k, &ch.repack);
+        parallel_for(ch.nb, [&](size_t lo, size_t hi) {
+            for (size_t b = lo; b < hi; ++b)
+                for (int j = 0; j < k; ++j) memcpy(s.h_in + (b * k + j) * ssd, data + (ch.b0 + b) * dbs + j * ss, len);
+        });
+        HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, ch.nb * k * ssd, hipMemcpyHostToDevice, p.up));
         return FEC_OK;
     };
-    size_t c = 0;
-    for (size_t b0 = 0; b0 < nblocks; b0 += chunk, ++c) {
-        const int i = (int)(c & 1);
-        const size_t nb = std::min(chunk, nblocks - b0);
-        if (pend[i].live && (rc = finish(i))) return rc;
-        HostSet& s = ctx->hs[i];
-        if ((rc = host_set_grow(ctx, s, chunk * k * ssd, chunk * m * ssd, 1))) return rc;
-        if (pinned) {
-            if ((rc = host_raw_grow(s, chunk * std::max(dbs, pbs) + 16))) return rc;
-            if ((rc = pinned_up(s, s.d_in, (size_t)k * ssd, ssd, data + b0 * dbs, dbs, ss, nb, k, len, s.d_raw, k)))
-                return rc;
-        } else {
-            parallel_for(nb, [&](size_t lo, size_t hi) {
-                for (size_t b = lo; b < hi; ++b)
-                    for (int j = 0; j < k; ++j)
-                        memcpy(s.h_in + (b * k + j) * ssd, data + (b0 + b) * dbs + j * ss, len);
-            });
-            HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, nb * k * ssd, hipMemcpyHostToDevice, s.s));
-        }
-        rc = on_stream(ctx, s, [&] {
-            return code ? rs_encode_device(ctx, code, len, nb, s.d_in, (size_t)k * ssd, s.d_out, (size_t)m * ssd, ssd)
-                        : xor_encode_device(ctx, k, len, nb, s.d_in, (size_t)k * ssd, s.d_out, ssd, ssd);
+    auto kern = [&](HostSet& s, HostChunk& ch) -> int {
+        if (ch.repack)
+            HIP_TRY(fk::launch_span_to_stage(s.d_in, (size_t)k * ssd, ssd, s.d_raw_in, dbs, ss, (uint32_t)ch.nb,
+                                             (uint32_t)k, (uint32_t)len, p.comp));
+        const int r = on_pipe(ctx, [&] {
+            return code ? rs_encode_device(ctx, code, len, ch.nb, s.d_in, (size_t)k * ssd, s.d_out, (size_t)m * ssd, ssd)
+                        : xor_encode_device(ctx, k, len, ch.nb, s.d_in, (size_t)k * ssd, s.d_out, ssd, ssd);
         });
-        if (rc) return rc;
-        if (pinned) {
-            if ((rc = pinned_down(s, parity + b0 * pbs, pbs, ss, s.d_out, (size_t)m * ssd, ssd, nb, m, len, s.d_raw)))
-                return rc;
-        } else {
-            HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, nb * m * ssd, hipMemcpyDeviceToHost, s.s));
-        }
-        HIP_TRY(hipEventRecord(s.done, s.s));
-        pend[i] = {b0, nb, true};
-    }
-    for (size_t t = 0; t < 2; ++t) {   // older chunk first
-        const int i = (int)((c + t) & 1);
-        if (pend[i].live && (rc = finish(i))) return rc;
-    }
-    return FEC_OK;
+        if (r) return r;
+        if (pack)
+            HIP_TRY(fk::launch_stage_to_packed(s.d_raw_out, s.d_out, (size_t)m * ssd, ssd, (uint32_t)ch.nb,
+                                               (uint32_t)m, (uint32_t)len, p.comp));
+        return FEC_OK;
+    };
+    auto down = [&](HostSet& s, HostChunk& ch) -> int {
+        if (pinned)
+            return pinned_down(p.down, parity + ch.b0 * pbs, pbs, ss, s.d_out, (size_t)m * ssd, ssd, ch.nb, m, len,
+                               s.d_raw_out);
+        HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, ch.nb * m * ssd, hipMemcpyDeviceToHost, p.down));
+        return FEC_OK;
+    };
+    auto finish = [&](HostSet& s, HostChunk& ch) -> int {
+        if (!pinned)
+            parallel_for(ch.nb, [&](size_t lo, size_t hi) {
+                for (size_t b = lo; b < hi; ++b)
+                    for (int r = 0; r < m; ++r)
+                        memcpy(parity + (ch.b0 + b) * pbs + r * ss, s.h_out + (b * m + r) * ssd, len);
+            });
+        return FEC_OK;
+    };
+    return host_pipeline(ctx, nblocks, chunk, up, kern, down, finish);
 }
 
 // RS reconstruct, in place in the caller's data slots: per chunk, the data shards and the parity
-// planes [0, P) (P = 1 + the highest parity index any block of the chunk reads among its first k
-// present shards) go up; the recover kernel rebuilds each block's erased data shards into
-// [block][slot] outputs (slots = the chunk's largest erasure count); only those come down and are
-// scattered into the erased slots.
+// planes its blocks read go up (P = 1 + the highest parity index any block of the chunk reads
+// among its first k present shards); the recover kernel rebuilds each block's erased data shards
+// into [block][slot] outputs (slots = the chunk's largest erasure count); only those come down
+// and are scattered into the erased slots. Pinned callers: a parity plane that at least 3/4 of
+// the chunk's blocks read goes up by one 2D DMA (tools/zerocopy_probe.hip: 52 GB/s for a 1202-B
+// row of every 4808 B); a sparser one is pulled by the device, plane by plane and block by block,
+// straight from the caller's buffer (gather_planes_kernel), which moves only what is read but runs
+// slower beside a D2H copy (pcie_duplex_probe: a kernel reading host memory and a D2H DMA at once
+// make 29.9 GB/s each way).
 static int host_reconstruct_rs(fec_ctx* ctx, Code* code, int k, int m, size_t len, size_t nblocks, uint8_t* data,
                                size_t dbs, const uint8_t* parity, size_t pbs, size_t ss, const uint32_t* masks,
                                int32_t* block_status, bool pinned) {
@@ -808,41 +897,17 @@ static int host_reconstruct_rs(fec_ctx* ctx, Code* code, int k, int m, size_t le
     const uint32_t all = fk::low_mask((uint32_t)n), kmask = fk::low_mask((uint32_t)k);
     const size_t maxe = (size_t)std::max(1, std::min(k, m));
     const size_t chunk = std::min(nblocks, host_chunk_blocks(n * ssd));
-    struct Pending {
-        size_t b0 = 0, nb = 0, slots = 0;
-        bool live = false;
-    } pend[2];
-    bool failed = false;
+    HostPipe& p = ctx->pipe;
     int rc;
-    auto finish = [&](int i) -> int {
-        HostSet& s = ctx->hs[i];
-        HIP_TRY(hipEventSynchronize(s.done));
-        for (size_t b = 0; b < pend[i].nb; ++b) {
-            const int32_t st = s.h_status[b];
-            if (block_status) block_status[pend[i].b0 + b] = st < 0 ? st : 0;
-            if (st < 0) failed = true;
-        }
-        parallel_for(pend[i].nb, [&](size_t lo, size_t hi) {
-            for (size_t b = lo; b < hi; ++b) {
-                const int32_t st = s.h_status[b];
-                const uint32_t mask = s.h_masks[b];
-                for (int j = 0, r = 0; j < k && r < st; ++j)
-                    if (!((mask >> j) & 1u))
-                        memcpy(data + (pend[i].b0 + b) * dbs + j * ss, s.h_out + (b * pend[i].slots + r++) * ssd, len);
-            }
-        });
-        pend[i].live = false;
-        return FEC_OK;
-    };
-    size_t c = 0;
-    for (size_t b0 = 0; b0 < nblocks; b0 += chunk, ++c) {
-        const int i = (int)(c & 1);
-        const size_t nb = std::min(chunk, nblocks - b0);
-        if (pend[i].live && (rc = finish(i))) return rc;
-        HostSet& s = ctx->hs[i];
-        if ((rc = host_set_grow(ctx, s, chunk * n * ssd, chunk * maxe * ssd, chunk))) return rc;
+    if ((rc = host_pipe_grow(p, chunk * n * ssd, chunk * maxe * ssd, chunk))) return rc;
+    if (pinned)
+        for (HostSet& s : p.set)
+            if ((rc = grow_dev(&s.d_raw_in, &s.raw_in_cap, span_bytes(chunk, k, dbs, ss, len) + 16))) return rc;
+    bool failed = false;
+    auto up = [&](HostSet& s, HostChunk& ch) -> int {
+        const size_t nb = ch.nb, b0 = ch.b0;
         // per block: the parity planes its first k present shards reach, its erasure count
-        size_t P = 0, slots = 1;
+        uint32_t needers[32] = {};
         for (size_t b = 0; b < nb; ++b) {
             const uint32_t mask = masks[b0 + b] & all;
             s.h_masks[b] = mask;
@@ -852,60 +917,91 @@ static int host_reconstruct_rs(fec_ctx* ctx, Code* code, int k, int m, size_t le
             for (int r = 0; r < m && need; ++r)
                 if ((mask >> (k + r)) & 1u) {
                     --need;
-                    P = std::max(P, (size_t)r + 1);
+                    ++needers[r];
+                    ch.planes = std::max(ch.planes, (size_t)r + 1);
                 }
-            slots = std::max(slots, (size_t)e);
+            ch.slots = std::max(ch.slots, (size_t)e);
         }
         uint8_t* d_par = s.d_in + nb * k * ssd;   // parity planes [P][nb][ssd]
-        HIP_TRY(hipMemcpyAsync(s.d_masks, s.h_masks, nb * 4, hipMemcpyHostToDevice, s.s));
+        HIP_TRY(hipMemcpyAsync(s.d_masks, s.h_masks, nb * 4, hipMemcpyHostToDevice, p.up));
         if (pinned) {
-            const size_t draw = span_bytes(nb, k, dbs, ss, len);
-            if ((rc = host_raw_grow(s, draw + span_bytes(nb, m, pbs, ss, len) + 16))) return rc;
-            if ((rc = pinned_up(s, s.d_in, (size_t)k * ssd, ssd, data + b0 * dbs, dbs, ss, nb, k, len, s.d_raw, k)))
+            if ((rc = pinned_up(p.up, s.d_in, (size_t)k * ssd, ssd, data + b0 * dbs, dbs, ss, nb, k, len, s.d_raw_in, k,
+                                &ch.repack)))
                 return rc;
-            // parity: the device reads exactly the planes each block's mask needs straight out of
-            // the caller's pinned buffer (fec_pack.hip gather_planes_kernel), instead of the whole
-            // [nb][m] span riding one linear DMA; a buffer the runtime cannot map takes the DMA
+            // the device reads sparse planes straight out of the caller's pinned buffer (needs a
+            // device mapping of it; otherwise every plane goes by DMA)
             const uint8_t* dpar = nullptr;
-            const bool mapped = P && fk::g_tune.host_gather &&
+            const bool mapped = ch.planes && fk::g_tune.host_gather &&
                                 hipHostGetDevicePointer((void**)&dpar, (void*)(parity + b0 * pbs), 0) == hipSuccess &&
                                 dpar;
-            if (P && !mapped) (void)hipGetLastError();
-            if (mapped)
-                HIP_TRY(fk::launch_gather_planes(dpar, pbs, ss, (uint32_t)len, s.d_masks, (uint32_t)nb, (uint32_t)P,
-                                                 (uint32_t)k, d_par, ssd, s.s));
-            else if (P && (rc = pinned_up(s, d_par, ssd, nb * ssd, parity + b0 * pbs, pbs, ss, nb, P, len,
-                                          s.d_raw + ((draw + 15) & ~size_t(15)), m)))
-                return rc;
-        } else {
-            parallel_for(nb, [&](size_t lo, size_t hi) {
-                for (size_t b = lo; b < hi; ++b) {
-                    const uint32_t mask = s.h_masks[b];
-                    if ((mask & kmask) == kmask) continue;   // nothing to rebuild: nothing read
-                    for (int j = 0; j < k; ++j)
-                        if ((mask >> j) & 1u)
-                            memcpy(s.h_in + (b * k + j) * ssd, data + (b0 + b) * dbs + j * ss, len);
-                    for (size_t r = 0; r < P; ++r)
-                        if ((mask >> (k + r)) & 1u)
-                            memcpy(s.h_in + nb * k * ssd + (r * nb + b) * ssd, parity + (b0 + b) * pbs + r * ss, len);
+            if (ch.planes && !mapped) (void)hipGetLastError();
+            for (size_t r = 0; r < ch.planes; ++r) {
+                const bool sparse = fk::g_tune.host_gather == 2 || needers[r] * 4 < nb * 3;
+                if (mapped && sparse) {
+                    ch.gather |= 1u << r;
+                    continue;
                 }
-            });
-            HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, (nb * k + P * nb) * ssd, hipMemcpyHostToDevice, s.s));
+                HIP_TRY(hipMemcpy2DAsync(d_par + r * nb * ssd, ssd, parity + b0 * pbs + r * ss, pbs, len, nb,
+                                         hipMemcpyHostToDevice, p.up));
+            }
+            return FEC_OK;
         }
-        rc = on_stream(ctx, s, [&] {
-            return rs_reconstruct_device(ctx, code, len, nb, s.d_in, (size_t)k * ssd, d_par, ssd, ssd, s.d_masks,
-                                         s.d_status, ctx->d_err + 1, s.d_out, slots * ssd, (uint32_t)slots, nb * ssd);
+        const size_t P = ch.planes;
+        parallel_for(nb, [&](size_t lo, size_t hi) {
+            for (size_t b = lo; b < hi; ++b) {
+                const uint32_t mask = s.h_masks[b];
+                if ((mask & kmask) == kmask) continue;   // nothing to rebuild: nothing read
+                for (int j = 0; j < k; ++j)
+                    if ((mask >> j) & 1u) memcpy(s.h_in + (b * k + j) * ssd, data + (b0 + b) * dbs + j * ss, len);
+                for (size_t r = 0; r < P; ++r)
+                    if ((mask >> (k + r)) & 1u)
+                        memcpy(s.h_in + nb * k * ssd + (r * nb + b) * ssd, parity + (b0 + b) * pbs + r * ss, len);
+            }
         });
-        if (rc) return rc;
-        HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, nb * slots * ssd, hipMemcpyDeviceToHost, s.s));
-        HIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, nb * 4, hipMemcpyDeviceToHost, s.s));
-        HIP_TRY(hipEventRecord(s.done, s.s));
-        pend[i] = {b0, nb, slots, true};
-    }
-    for (size_t t = 0; t < 2; ++t) {
-        const int i = (int)((c + t) & 1);
-        if (pend[i].live && (rc = finish(i))) return rc;
-    }
+        HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, (nb * k + P * nb) * ssd, hipMemcpyHostToDevice, p.up));
+        return FEC_OK;
+    };
+    auto kern = [&](HostSet& s, HostChunk& ch) -> int {
+        const size_t nb = ch.nb;
+        uint8_t* d_par = s.d_in + nb * k * ssd;
+        if (ch.repack)
+            HIP_TRY(fk::launch_span_to_stage(s.d_in, (size_t)k * ssd, ssd, s.d_raw_in, dbs, ss, (uint32_t)nb,
+                                             (uint32_t)k, (uint32_t)len, p.comp));
+        if (ch.gather) {
+            const uint8_t* dpar = nullptr;
+            HIP_TRY(hipHostGetDevicePointer((void**)&dpar, (void*)(parity + ch.b0 * pbs), 0));
+            HIP_TRY(fk::launch_gather_planes(dpar, pbs, ss, (uint32_t)len, s.d_masks, (uint32_t)nb, (uint32_t)ch.planes,
+                                             ch.gather, (uint32_t)k, d_par, ssd, p.comp));
+        }
+        return on_pipe(ctx, [&] {
+            return rs_reconstruct_device(ctx, code, len, nb, s.d_in, (size_t)k * ssd, d_par, ssd, ssd, s.d_masks,
+                                         s.d_status, ctx->d_err + 1, s.d_out, ch.slots * ssd, (uint32_t)ch.slots,
+                                         nb * ssd);
+        });
+    };
+    auto down = [&](HostSet& s, HostChunk& ch) -> int {
+        HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, ch.nb * ch.slots * ssd, hipMemcpyDeviceToHost, p.down));
+        HIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, ch.nb * 4, hipMemcpyDeviceToHost, p.down));
+        return FEC_OK;
+    };
+    auto finish = [&](HostSet& s, HostChunk& ch) -> int {
+        for (size_t b = 0; b < ch.nb; ++b) {
+            const int32_t st = s.h_status[b];
+            if (block_status) block_status[ch.b0 + b] = st < 0 ? st : 0;
+            if (st < 0) failed = true;
+        }
+        parallel_for(ch.nb, [&](size_t lo, size_t hi) {
+            for (size_t b = lo; b < hi; ++b) {
+                const int32_t st = s.h_status[b];
+                const uint32_t mask = s.h_masks[b];
+                for (int j = 0, r = 0; j < k && r < st; ++j)
+                    if (!((mask >> j) & 1u))
+                        memcpy(data + (ch.b0 + b) * dbs + j * ss, s.h_out + (b * ch.slots + r++) * ssd, len);
+            }
+        });
+        return FEC_OK;
+    };
+    if ((rc = host_pipeline(ctx, nblocks, chunk, up, kern, down, finish))) return rc;
     // the sticky device word of the host path is not used: statuses say it all
     return failed ? FEC_ERR_TOO_FEW_SHARDS : FEC_OK;
 }
@@ -1049,16 +1145,21 @@ void fec_ctx_destroy(fec_ctx* ctx) {
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
     if (ctx->d_masks) (void)hipFree(ctx->d_masks);
     if (ctx->d_status) (void)hipFree(ctx->d_status);
-    for (HostSet& s : ctx->hs) {
-        if (s.s) (void)hipStreamSynchronize(s.s);
+    HostPipe& p = ctx->pipe;
+    for (hipStream_t q : {p.up, p.comp, p.down})
+        if (q) (void)hipStreamSynchronize(q);
+    for (HostSet& s : p.set) {
         for (void* q : {(void*)s.h_in, (void*)s.h_out, (void*)s.h_masks, (void*)s.h_status})
             if (q) (void)hipHostFree(q);
-        for (void* q : {(void*)s.d_in, (void*)s.d_out, (void*)s.d_masks, (void*)s.d_status, (void*)s.d_raw})
+        for (void* q : {(void*)s.d_in, (void*)s.d_out, (void*)s.d_masks, (void*)s.d_status, (void*)s.d_raw_in,
+                        (void*)s.d_raw_out})
             if (q) (void)hipFree(q);
-        s.w.release();
-        if (s.done) (void)hipEventDestroy(s.done);
-        if (s.s) (void)hipStreamDestroy(s.s);
+        for (hipEvent_t e : {s.up_done, s.k_done, s.down_done})
+            if (e) (void)hipEventDestroy(e);
     }
+    p.w.release();
+    for (hipStream_t q : {p.up, p.comp, p.down})
+        if (q) (void)hipStreamDestroy(q);
     if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
     if (ctx->own) (void)hipStreamDestroy(ctx->own);
     (void)hipGetLastError();

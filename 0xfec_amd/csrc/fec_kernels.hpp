@@ -206,8 +206,9 @@ struct Tuning {
                               // decode time, RS(16,24) -3 % (rebuild rows; a cheaper ranking); 256 / 512
                               // cost the plan kernel residency (its LDS) more than the rebuild gains (r03y)
     int dec_s64 = 0;          // fec_rebuild.hip: input splits by 64-bit shifts (two dwords a shift)
-    int host_gather = 1;      // FEC_HOST_PINNED reconstruct: the parity planes each block reads are pulled by
-                              // the device straight from the caller's pinned buffer (0: whole span by DMA)
+    int host_gather = 1;      // FEC_HOST_PINNED reconstruct: parity planes that few blocks read are pulled by
+                              // the device straight from the caller's pinned buffer, the rest by 2D DMA (0:
+                              // every plane by DMA; 2: every plane by the device)
 };
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):
@@ -287,10 +288,12 @@ struct GatherDesc {
     uint32_t frame;
 };
 hipError_t launch_gather_desc(const GatherDesc* desc, uint32_t n, uint8_t* dst, uint64_t slot, hipStream_t s);
-// The parity planes [0, planes) of nb blocks (block b, plane r at base + b*bs + r*ss) that each
-// block's present mask makes it read, to dst + (r*nb + b)*slot; the others are skipped.
+// The parity planes r < planes with bit r of plane_bits set, of nb blocks (block b, plane r at
+// base + b*bs + r*ss), that each block's present mask makes it read, to dst + (r*nb + b)*slot; the
+// others are skipped.
 hipError_t launch_gather_planes(const uint8_t* base, uint64_t bs, uint64_t ss, uint32_t len, const uint32_t* masks,
-                                uint32_t nb, uint32_t planes, uint32_t k, uint8_t* dst, uint64_t slot, hipStream_t s);
+                                uint32_t nb, uint32_t planes, uint32_t plane_bits, uint32_t k, uint8_t* dst,
+                                uint64_t slot, hipStream_t s);
 
 // Blocks per decode tile for shard chunk count `cps`, bounded by LDS.
 uint32_t pick_tile_blocks(uint32_t cps, uint32_t k, uint32_t maxe, const PlanLayout& lay);

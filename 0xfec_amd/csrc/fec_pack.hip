@@ -133,11 +133,12 @@ __global__ __launch_bounds__(256) void gather_desc_kernel(const GatherDesc* __re
 // present parities for e erased data shards); other (r, b) are not read or written.
 __global__ __launch_bounds__(256) void gather_planes_kernel(const uint8_t* __restrict__ base, uint64_t bs, uint64_t ss,
                                                            uint32_t len, const uint32_t* __restrict__ masks,
-                                                           uint32_t nb, uint32_t planes, uint32_t k,
-                                                           uint8_t* __restrict__ dst, uint64_t slot) {
+                                                           uint32_t nb, uint32_t planes, uint32_t plane_bits,
+                                                           uint32_t k, uint8_t* __restrict__ dst, uint64_t slot) {
     const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
     if (i >= nb * planes) return;
     const uint32_t r = i / nb, b = i - r * nb;
+    if (!((plane_bits >> r) & 1u)) return;   // a plane the host path moves by DMA
     const uint32_t mask = masks[b];
     const uint32_t e = k - (uint32_t)__popc(mask & low_mask(k));
     const uint32_t par = k < 32 ? mask >> k : 0u;
@@ -157,11 +158,12 @@ hipError_t launch_gather_desc(const GatherDesc* desc, uint32_t n, uint8_t* dst, 
 }
 
 hipError_t launch_gather_planes(const uint8_t* base, uint64_t bs, uint64_t ss, uint32_t len, const uint32_t* masks,
-                                uint32_t nb, uint32_t planes, uint32_t k, uint8_t* dst, uint64_t slot, hipStream_t s) {
+                                uint32_t nb, uint32_t planes, uint32_t plane_bits, uint32_t k, uint8_t* dst,
+                                uint64_t slot, hipStream_t s) {
     const uint64_t n = (uint64_t)nb * planes;
-    if (n == 0) return hipSuccess;
+    if (n == 0 || plane_bits == 0) return hipSuccess;
     hipLaunchKernelGGL(gather_planes_kernel, dim3((uint32_t)((n + 3) / 4)), dim3(256), 0, s, base, bs, ss, len, masks,
-                       nb, planes, k, dst, slot);
+                       nb, planes, plane_bits, k, dst, slot);
     return hipGetLastError();
 }
 

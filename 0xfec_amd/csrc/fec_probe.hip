@@ -1,0 +1,256 @@
+// fec_probe.hip — traffic twins of the headline kernels (measurement only; include/fec_probe.h).
+//
+// A twin moves exactly the bytes its kernel moves, with the same launch geometry (flat grid, one
+// 16-byte chunk per lane, XCD-contiguous workgroup order, the same residency cap through dynamic
+// LDS, non-temporal loads and stores, zero-padded tail chunks) and no field arithmetic: the XOR of
+// its inputs stands in for the products. Timed on the same box and buffers right after the
+// kernel, its rate is that box's ceiling for the kernel's access shape, so a bench line can say
+// how much of a kernel's distance to the 8 TB/s spec is the box and how much is the kernel.
+//   encode twin   rs_encode_fixed_kernel<K, M, ..> (fec_encode.hip): K shard loads, M stores
+//   recover twin  rs_recover_direct_kernel<K, ..> (fec_recover.hip) on single-erasure blocks:
+//                 the k-1 other data shards and the first present parity, one store to `out`
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+
+#include "../../include/fec_hip.h"
+#include "../../include/fec_probe.h"
+#include "fec_device.hpp"
+
+namespace fk {
+namespace {
+
+template <int K, int M>
+__global__ __launch_bounds__(kThreads) void probe_encode_kernel(EncodeArgs a) {
+    extern __shared__ uint8_t smem[];   // residency only, as the encode's staged tables
+    const uint32_t it = xcd_order(a.swz) * kThreads + threadIdx.x;
+    if (it >= a.total) return;
+    const uint32_t b = fdiv(it, a.div_cps);
+    const uint32_t c = it - b * a.cps;
+    const uint8_t* src = a.in + (uint64_t)b * a.in_bs + (uint64_t)c * kChunk;
+    uint4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] = ld16<true>(src + (uint64_t)j * a.ss);
+    uint4 acc[M];
+#pragma unroll
+    for (int r = 0; r < M; ++r) acc[r] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        acc[j % M].x ^= x[j].x;
+        acc[j % M].y ^= x[j].y;
+        acc[j % M].z ^= x[j].z;
+        acc[j % M].w ^= x[j].w;
+    }
+    uint8_t* dst = a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk;
+    const uint32_t nb = min(a.len - c * kChunk, (uint32_t)kChunk);
+#pragma unroll
+    for (int r = 0; r < M; ++r) st16<true>(dst + (uint64_t)r * a.ss, keep_bytes(acc[r], nb));
+    if (a.pad_zero == 0x5A5A5A5Au) smem[0] = 1;   // never: keeps the LDS allocation
+}
+
+struct RecoverProbeArgs {
+    const uint8_t* data;
+    const uint8_t* parity;
+    uint8_t* out;
+    const uint32_t* masks;
+    uint64_t dbs, pbs, ss, out_bs;
+    uint32_t len, cps, total, nblocks, swz;
+    FastDiv div_cps;
+};
+
+template <int K>
+__global__ __launch_bounds__(kThreads) void probe_recover_kernel(RecoverProbeArgs a, uint32_t m) {
+    extern __shared__ uint8_t smem[];   // residency only, as the decode's wave slices
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t i0 = xcd_order(a.swz) * kThreads + (wave << 6);
+    if (i0 >= a.total) return;
+    // the wave's <= 3 block masks in one load, as the direct kernel
+    const uint32_t bfirst = fdiv(i0, a.div_cps);
+    const uint32_t nbw = fdiv(min(i0 + 63u, a.total - 1u), a.div_cps) - bfirst + 1;
+    const uint32_t mine = lane < nbw ? a.masks[bfirst + lane] : 0u;
+    const uint32_t item = i0 + lane;
+    if (item >= a.total) return;
+    const uint32_t blk = fdiv(item, a.div_cps);
+    const uint32_t g = blk - bfirst;
+    const uint32_t c = item - blk * a.cps;
+    const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 0);
+    const uint32_t m1 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 1);
+    const uint32_t m2 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 2);
+    const uint32_t mask = (g == 0 ? m0 : g == 1 ? m1 : m2) & low_mask(K + m);
+    const uint32_t E0 = __ffs(~mask & low_mask(K)) - 1;
+    const uint32_t R0 = __ffs(mask >> K) - 1;
+    if (__popc(mask & low_mask(K)) != K - 1 || R0 >= m) return;   // not a single-erasure block: nothing read
+    const uint8_t* d0 = a.data + (uint64_t)blk * a.dbs + (uint64_t)c * kChunk;
+    uint4 x[K];
+#pragma unroll
+    for (int j = 0; j < K - 1; ++j) x[j] = ld16<true>(d0 + (uint64_t)(j + (j >= (int)E0)) * a.ss);
+    x[K - 1] = ld16<true>(a.parity + (uint64_t)blk * a.pbs + (uint64_t)R0 * a.ss + (uint64_t)c * kChunk);
+    uint4 acc = x[0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) {
+        acc.x ^= x[j].x;
+        acc.y ^= x[j].y;
+        acc.z ^= x[j].z;
+        acc.w ^= x[j].w;
+    }
+    const uint32_t nb = min(a.len - c * kChunk, (uint32_t)kChunk);
+    st16<true>(a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk, keep_bytes(acc, nb));
+    if (a.swz == 0x5A5A5A5Au) smem[0] = 1;   // never: keeps the LDS allocation
+}
+
+int stream_of(fec_ctx* ctx, hipStream_t* s) {
+    if (!ctx) return FEC_ERR_INVALID_ARG;
+    *s = (hipStream_t)fec_ctx_stream(ctx);
+    int dev = 0;
+    if (hipStreamGetDevice(*s, &dev) != hipSuccess || hipSetDevice(dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return FEC_ERR_HIP;
+    }
+    return FEC_OK;
+}
+
+bool layout_ok(const void* p, size_t bs, size_t ss, size_t len) {
+    return p && !((uintptr_t)p & 15) && !(bs & 15) && !(ss & 15) && ss >= len;
+}
+
+}  // namespace
+}  // namespace fk
+
+extern "C" int fec_probe_encode_traffic(fec_ctx* ctx, int k, int m, size_t shard_len, size_t nblocks,
+                                        const void* data, size_t dbs, void* parity, size_t pbs, size_t ss) {
+    using namespace fk;
+    hipStream_t s;
+    int rc = stream_of(ctx, &s);
+    if (rc) return rc;
+    if (!((k == 2 && m == 1) || (k == 8 && m == 4) || (k == 16 && m == 8))) return FEC_ERR_INVALID_ARG;
+    if (!layout_ok(data, dbs, ss, shard_len) || !layout_ok(parity, pbs, ss, shard_len) || shard_len == 0)
+        return FEC_ERR_ALIGNMENT;
+    const uint32_t cps = (uint32_t)((shard_len + kChunk - 1) / kChunk);
+    if ((uint64_t)nblocks * cps >= (uint64_t(1) << 31)) return FEC_ERR_INVALID_ARG;
+    if (nblocks == 0) return FEC_OK;
+    EncodeArgs a{};
+    a.in = (const uint8_t*)data;
+    a.out = (uint8_t*)parity;
+    a.in_bs = dbs;
+    a.out_bs = pbs;
+    a.ss = ss;
+    a.k = (uint32_t)k;
+    a.m = (uint32_t)m;
+    a.len = (uint32_t)shard_len;
+    a.cps = cps;
+    a.total = (uint32_t)(nblocks * cps);
+    a.div_cps = make_fastdiv(cps);
+    a.swz = (uint32_t)g_tune.xcd_swz;
+    const int grid = (int)((a.total + kThreads - 1) / kThreads);
+    // the fixed encode's residency: g_tune.enc_wpc workgroups per CU, RS(2,3) uncapped
+    const size_t lds = occupancy_lds(k == 2 ? 0 : g_tune.enc_wpc, (size_t)m * k * 32);
+    if (k == 2) hipLaunchKernelGGL((probe_encode_kernel<2, 1>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (k == 8) hipLaunchKernelGGL((probe_encode_kernel<8, 4>), dim3(grid), dim3(kThreads), lds, s, a);
+    else hipLaunchKernelGGL((probe_encode_kernel<16, 8>), dim3(grid), dim3(kThreads), lds, s, a);
+    return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
+}
+
+extern "C" int fec_probe_recover_traffic(fec_ctx* ctx, int k, int m, size_t shard_len, size_t nblocks,
+                                         const void* data, size_t dbs, const void* parity, size_t pbs, size_t ss,
+                                         const uint32_t* masks, void* out, size_t out_bs) {
+    using namespace fk;
+    hipStream_t s;
+    int rc = stream_of(ctx, &s);
+    if (rc) return rc;
+    if (!((k == 2 && m == 1) || (k == 8 && m == 4) || (k == 16 && m == 8) || (k == 20 && m == 10)))
+        return FEC_ERR_INVALID_ARG;
+    if (!masks || !layout_ok(data, dbs, ss, shard_len) || !layout_ok(parity, pbs, ss, shard_len) ||
+        !layout_ok(out, out_bs, 16, 0) || shard_len == 0 || out_bs < ((shard_len + 15) & ~size_t(15)))
+        return FEC_ERR_ALIGNMENT;
+    const uint32_t cps = (uint32_t)((shard_len + kChunk - 1) / kChunk);
+    if ((uint64_t)nblocks * cps >= (uint64_t(1) << 31) || cps < 32) return FEC_ERR_INVALID_ARG;
+    if (nblocks == 0) return FEC_OK;
+    RecoverProbeArgs a{};
+    a.data = (const uint8_t*)data;
+    a.parity = (const uint8_t*)parity;
+    a.out = (uint8_t*)out;
+    a.masks = masks;
+    a.dbs = dbs;
+    a.pbs = pbs;
+    a.ss = ss;
+    a.out_bs = out_bs;
+    a.len = (uint32_t)shard_len;
+    a.cps = cps;
+    a.total = (uint32_t)(nblocks * cps);
+    a.nblocks = (uint32_t)nblocks;
+    a.swz = (uint32_t)g_tune.dec_swz;
+    a.div_cps = make_fastdiv(cps);
+    const int grid = (int)((a.total + kThreads - 1) / kThreads);
+    // the direct decode's residency (fec_recover.hip direct_launch): 4 workgroups per CU at k = 8,
+    // 3 at k >= 16, small codes uncapped; LDS as its four wave slices of 3 blocks' PermTab rows
+    const int wpc = g_tune.dir_wpc >= 0 ? g_tune.dir_wpc : (k >= 16 ? 3 : k >= 8 ? 4 : 0);
+    const size_t lds = occupancy_lds(wpc, (size_t)4 * 3 * k * 32);
+    const uint32_t um = (uint32_t)m;
+    if (k == 2) hipLaunchKernelGGL((probe_recover_kernel<2>), dim3(grid), dim3(kThreads), lds, s, a, um);
+    else if (k == 8) hipLaunchKernelGGL((probe_recover_kernel<8>), dim3(grid), dim3(kThreads), lds, s, a, um);
+    else if (k == 16) hipLaunchKernelGGL((probe_recover_kernel<16>), dim3(grid), dim3(kThreads), lds, s, a, um);
+    else hipLaunchKernelGGL((probe_recover_kernel<20>), dim3(grid), dim3(kThreads), lds, s, a, um);
+    return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
+}
+
+// The host link as the host path drives it (fec_capi.cpp HostPipe): hipMemcpyAsync between pinned
+// host and device buffers of `bytes`, H2D alone, D2H alone, and both at once on two non-blocking
+// streams; the best of `reps` by host wall clock around a device synchronisation. GB/s into
+// out[0..2]. Buffers are allocated and freed here.
+extern "C" int fec_probe_link(fec_ctx* ctx, size_t bytes, int reps, double* out) {
+    using namespace fk;
+    hipStream_t s0;
+    int rc = stream_of(ctx, &s0);
+    if (rc) return rc;
+    if (!out || bytes == 0 || reps <= 0) return FEC_ERR_INVALID_ARG;
+    uint8_t *h_up = nullptr, *h_dn = nullptr, *d_up = nullptr, *d_dn = nullptr;
+    hipStream_t su = nullptr, sd = nullptr;
+    rc = FEC_ERR_HIP;
+    auto best = [&](auto fn) -> double {
+        fn();
+        if (hipDeviceSynchronize() != hipSuccess) return -1.0;
+        double b = 1e30;
+        for (int r = 0; r < reps; ++r) {
+            const auto t0 = std::chrono::steady_clock::now();
+            fn();
+            if (hipDeviceSynchronize() != hipSuccess) return -1.0;
+            b = std::min(b, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+        }
+        return b;
+    };
+    if (hipHostMalloc(&h_up, bytes, hipHostMallocDefault) == hipSuccess &&
+        hipHostMalloc(&h_dn, bytes, hipHostMallocDefault) == hipSuccess && hipMalloc(&d_up, bytes) == hipSuccess &&
+        hipMalloc(&d_dn, bytes) == hipSuccess && hipStreamCreateWithFlags(&su, hipStreamNonBlocking) == hipSuccess &&
+        hipStreamCreateWithFlags(&sd, hipStreamNonBlocking) == hipSuccess) {
+        memset(h_up, 1, bytes);
+        memset(h_dn, 2, bytes);
+        (void)hipMemset(d_dn, 3, bytes);
+        (void)hipMemset(d_up, 4, bytes);
+        (void)hipDeviceSynchronize();
+        // both directions first, on the fresh streams: the runtime keeps a stream on the SDMA engine
+        // it first got, and two copies issued back to back on fresh streams get different engines
+        // (pcie_duplex_probe: 48.6 GB/s each way); streams that each ran a copy alone first can end
+        // up sharing one engine (28.7 each way, serialised)
+        const double tb = best([&] {
+            (void)hipMemcpyAsync(d_up, h_up, bytes, hipMemcpyHostToDevice, su);
+            (void)hipMemcpyAsync(h_dn, d_dn, bytes, hipMemcpyDeviceToHost, sd);
+        });
+        const double tu = best([&] { (void)hipMemcpyAsync(d_up, h_up, bytes, hipMemcpyHostToDevice, su); });
+        const double td = best([&] { (void)hipMemcpyAsync(h_dn, d_dn, bytes, hipMemcpyDeviceToHost, sd); });
+        if (tu > 0 && td > 0 && tb > 0) {
+            out[0] = (double)bytes / tu / 1e9;
+            out[1] = (double)bytes / td / 1e9;
+            out[2] = (double)bytes / tb / 1e9;
+            rc = FEC_OK;
+        }
+    }
+    for (hipStream_t q : {su, sd})
+        if (q) (void)hipStreamDestroy(q);
+    for (void* q : {(void*)h_up, (void*)h_dn})
+        if (q) (void)hipHostFree(q);
+    for (void* q : {(void*)d_up, (void*)d_dn})
+        if (q) (void)hipFree(q);
+    (void)hipGetLastError();
+    return rc;
+}

@@ -239,12 +239,22 @@ def host_resident(torch, fec, codec, k, m, blocks, seed, reps=3):
     masks = (((1 << n) - 1) & ~(1 << erased)).astype(np.uint32)
     # PCIe bytes of a step: encode k up + m down; reconstruct the k data shards up (one linear DMA
     # of the span), the one parity plane each block reads (pageable: staged by the host; pinned:
-    # pulled by the device straight from the caller's buffer, fec_pack.hip gather_planes_kernel),
-    # the rebuilt shard down
+    # one 2D DMA of the plane, which every block reads here), the rebuilt shard down
+    up_bytes, down_bytes = blocks * (k + k + 1) * L, blocks * (m + 1) * L
+    # the link as the host path drives it (include/fec_probe.h fec_probe_link: pinned hipMemcpyAsync,
+    # H2D, D2H, both at once on two streams; tools/pcie_duplex_probe.hip measures more shapes)
+    link = codec.probe_link()
+    # the link's bound for the step: while both directions run, each at the duplex rate; the rest
+    # of the up direction (the larger one) alone at the H2D rate
+    both = min(up_bytes, down_bytes)
+    bound_s = both / (link["duplex_each_GBps"] * 1e9) + (up_bytes - both) / (link["h2d_GBps"] * 1e9) \
+        + (down_bytes - both) / (link["d2h_GBps"] * 1e9)
     out = {"blocks": blocks, "layout": "packed host [B][k][1202] + [B][m][1202]",
-           "pcie_bytes_per_step": blocks * (k + m + k + 1 + 1) * L,
-           "pcie_bytes_note": "k+m+k+1+1 shards per block in both forms (pinned: parity planes gathered by the "
-                              "device, only the plane each block reads; round 2 moved the whole parity span, k+m+k+m+1)"}
+           "pcie_bytes_per_step": up_bytes + down_bytes, "pcie_up_bytes": up_bytes, "pcie_down_bytes": down_bytes,
+           "pcie_bytes_note": "up k+k+1 shards per block (encode data; reconstruct data span + the parity plane each "
+                              "block reads), down m+1 (parity; the rebuilt shard), in both forms",
+           "link_probe": link, "link_bound_ms": round(bound_s * 1e3, 2),
+           "link_bound_GiBps": round(blocks * k * PAYLOAD / 2**30 / bound_s, 2)}
     for form in ("pinned", "pageable"):
         if form == "pinned":
             data = torch.from_numpy(src.copy()).pin_memory()
@@ -274,7 +284,48 @@ def host_resident(torch, fec, codec, k, m, blocks, seed, reps=3):
         best = min(t)
         out[form] = {"value": round(blocks * k * PAYLOAD / 2**30 / best, 2), "unit": "GiB/s",
                      "ms_per_step": round(best * 1e3, 2), "pcie_GBps": round(out["pcie_bytes_per_step"] / best / 1e9, 2),
+                     "up_GBps": round(up_bytes / best / 1e9, 2), "down_GBps": round(down_bytes / best / 1e9, 2),
+                     "frac_of_probe": round(bound_s / best, 4),
                      "check": ok and bool(np.array_equal(pnp[:64], oracle_parity(k, m, src[:64])))}
+    return out
+
+
+def box_probe(torch, codec, b, step, stream, enc_bytes, dec_bytes, rounds=5, burst=4):
+    """Times the traffic twin of the encode and of the direct decode (fec_probe.hip: the same bytes,
+    launch shape, residency and cache policy, no field arithmetic) in bursts interleaved with bursts
+    of the kernels themselves. Returns per kernel the twin's TB/s (the box's ceiling for that
+    access shape), the kernel's TB/s in the same interleaved bursts, and their ratio."""
+    def enc_twin():
+        codec.probe_encode_traffic_raw(b.k, b.m, SHARD_LEN, b.B, b.data.data_ptr(), b.k * SHARD_STRIDE,
+                                       b.parity.data_ptr(), b.m * SHARD_STRIDE, SHARD_STRIDE)
+
+    def dec_twin():
+        codec.probe_recover_traffic_raw(b.k, b.m, SHARD_LEN, b.B, b.data.data_ptr(), b.k * SHARD_STRIDE,
+                                        b.parity.data_ptr(), b.m * SHARD_STRIDE, SHARD_STRIDE, b.masks.data_ptr(),
+                                        b.recovered.data_ptr(), SHARD_STRIDE)
+
+    def timed_burst(fn):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(burst):
+            fn()
+        e1.record(stream)
+        return e0, e1
+
+    out = {}
+    for name, twin, kern, nbytes in (("encode", enc_twin, step.encode, enc_bytes),
+                                     ("decode", dec_twin, step.decode, dec_bytes)):
+        twin()
+        kern()
+        ev = []
+        for _ in range(rounds):   # twin first: the kernel then rewrites what the twin wrote
+            ev.append((timed_burst(twin), timed_burst(kern)))
+        codec.sync()
+        tw = sum(a[0].elapsed_time(a[1]) for a, _ in ev) / (rounds * burst)
+        kt = sum(c[0].elapsed_time(c[1]) for _, c in ev) / (rounds * burst)
+        out[name] = {"probe_ms": round(tw, 4), "probe_TBps": round(nbytes / tw / 1e9, 3),
+                     "kernel_ms_interleaved": round(kt, 4), "kernel_TBps_interleaved": round(nbytes / kt / 1e9, 3),
+                     "kernel_frac_of_probe_interleaved": round(tw / kt, 4)}
     return out
 
 
@@ -424,14 +475,20 @@ def main():
     L = SHARD_LEN
     enc_bytes = B * (k + m) * L                  # read k shards, write m shards
     dec_bytes = B * (k + 1) * L                  # read first k present, write 1 erased data shard
+    # this box's ceiling for each kernel's access shape, after the checks (the twins overwrite the
+    # parity and recovered buffers): traffic twins (include/fec_probe.h), interleaved with the
+    # kernels themselves so both see the same box state
+    probe = box_probe(torch, codec, batch, step, stream, enc_bytes, dec_bytes)
     value = shard.aggregate_gibps([B] * world, k, PAYLOAD, step_ms / 1000.0)
     enc_bw = enc_bytes / (enc_ms / 1000.0)
     dec_bw = dec_bytes / (dec_ms / 1000.0)
     enc_kernel = encode_kernel_name(k, m)
     if enc_ms >= dec_ms:
+        dom_name = "encode"
         dominant, dom_bw, dom_bytes = enc_kernel + ">", enc_bw, enc_bytes
         traffic, traffic_src = committed_traffic(enc_kernel, "fec_encode.hip")
     else:
+        dom_name = "decode"
         dominant, dom_bw, dom_bytes = "rs_recover_direct_kernel<%d" % k, dec_bw, dec_bytes
         traffic, traffic_src = committed_traffic("rs_recover_direct_kernel", "fec_recover.hip")
 
@@ -461,16 +518,26 @@ def main():
                          "unit": "GB/s", "frac": round(dom_bw / HBM_PEAK, 4),
                          "traffic": None if traffic is None else round(traffic / 1e9, 3),
                          "traffic_unit": "GB per launch", "traffic_profile": traffic_src,
-                         "kernel": dominant, "algorithmic_bytes_per_launch": dom_bytes},
+                         "kernel": dominant, "algorithmic_bytes_per_launch": dom_bytes,
+                         # this box's ceiling for the kernel's access shape (its traffic twin) and
+                         # the timed-region rate over it
+                         "probe_TBps": probe[dom_name]["probe_TBps"],
+                         "frac_of_probe": round(dom_bw / 1e12 / probe[dom_name]["probe_TBps"], 4),
+                         "probe_kernel": "fec_probe.hip probe_%s_kernel (include/fec_probe.h)" % (
+                             "encode" if dom_name == "encode" else "recover")},
             "kernels": {
                 # read_frac: the HBM-read roofline of SURVEY.md 8(d) (reads alone: k shards per block)
                 "encode": {"ms": round(enc_ms, 4), "GB/s": round(enc_bw / 1e9, 1), "bytes": enc_bytes,
                            "frac": round(enc_bw / HBM_PEAK, 4),
-                           "read_frac": round(B * k * L / (enc_ms / 1000.0) / HBM_PEAK, 4)},
+                           "read_frac": round(B * k * L / (enc_ms / 1000.0) / HBM_PEAK, 4),
+                           "frac_of_probe": round(enc_bw / 1e12 / probe["encode"]["probe_TBps"], 4),
+                           "probe": probe["encode"]},
                 "decode": {"ms": round(dec_ms, 4), "GB/s": round(dec_bw / 1e9, 1), "bytes": dec_bytes,
                            "frac": round(dec_bw / HBM_PEAK, 4),
                            "read_frac": round(B * k * L / (dec_ms / 1000.0) / HBM_PEAK, 4),
-                           "api": "fec_rs_recover_batch (direct single-erasure kernel, no plan launch)"},
+                           "api": "fec_rs_recover_batch (direct single-erasure kernel, no plan launch)",
+                           "frac_of_probe": round(dec_bw / 1e12 / probe["decode"]["probe_TBps"], 4),
+                           "probe": probe["decode"]},
                 "decode_inplace": {"ms": round(inplace_ms, 4),
                                    "GB/s": round(dec_bytes / (inplace_ms / 1e3) / 1e9, 1),
                                    "api": "fec_rs_reconstruct_batch (direct kernel, in place), not in the step"},

@@ -140,7 +140,7 @@ static int decoder(void) {
         const uint8_t *rp;
         size_t rl;
         uint64_t bid, pid;
-        if (!fec_frames_get(fr, 0, &bid, &pid, &rp, &rl)) return fail("frames_get", 0);
+        if ((err = fec_frames_get(fr, 0, &bid, &pid, &rp, &rl))) return fail("frames_get", err);
         if ((err = fec_block_add_repair_symbol(rx, bid, pid, rp, rl))) return fail("rx repair", err);
         int staged = 0;
         if ((err = fec_batch_decoder_submit(d, rx, q, &staged)) || !staged) return fail("decoder submit", err);

@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""Chunk size and parity-plane policy of the host-resident pipeline (fec_capi.cpp HostPipe),
+measured with bench.py's own host_resident() step (RS(8,12) encode + single-erasure reconstruct,
+packed pinned and pageable host buffers).
+
+    python tools/host_chunk_sweep.py [--blocks 131072]
+
+One JSON line per setting: knob host_chunk (blocks per chunk; 0 = the library's default, 128 MiB
+of staged shards) and host_gather (1: sparse parity planes pulled by the device, dense ones by
+2D DMA; 2: every plane pulled by the device; 0: every plane by DMA)."""
+import argparse
+import importlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--blocks", type=int, default=1 << 17)
+    ap.add_argument("--chunks", default="0,2048,4096,8192,16384,32768")
+    args = ap.parse_args()
+    import torch
+    bench = importlib.import_module("bench")
+    fec = importlib.import_module("0xfec_amd")
+    codec = fec.Codec(0)
+    codec.prepare(8, 4)
+    for chunk in [int(c) for c in args.chunks.split(",")]:
+        for gather in (1, 2) if chunk == 0 else (1,):
+            old = codec.set_tuning(host_chunk=chunk, host_gather=gather)
+            r = bench.host_resident(torch, fec, codec, 8, 4, args.blocks, 0x0FEC)
+            codec.set_tuning(**old)
+            print(json.dumps({"host_chunk": chunk, "host_gather": gather, "link_bound_GiBps": r["link_bound_GiBps"],
+                              "pinned": r["pinned"], "pageable": r["pageable"]}), flush=True)
+    codec.close()
+
+
+if __name__ == "__main__":
+    main()
