@@ -1214,7 +1214,7 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 34 ? &fk::g_tune.dec_gate : key == 35 ? &fk::g_tune.dec_gate_pm
               : key == 36 ? &fk::g_tune.host_gather : key == 37 ? &fk::g_tune.dec_win
               : key == 38 ? &fk::g_tune.dec_s64
-              : key == 39 ? &fk::g_tune.dec_psort : nullptr;
+              : key == 39 ? &fk::g_tune.dec_psort : key == 40 ? &fk::g_tune.dec_pv : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

@@ -26,12 +26,17 @@ constexpr uint32_t kGroupScratch = 160;   // per block: S[32] slots, O[32] erase
 struct SortLds {
     size_t prows, dall, scratch, pos, rank, recs, total;
 };
+// Plan form 2 (knob dec_pv = 2) stages its tables differently: exp over [0, 768) (exp[i mod 255], so
+// a sum of three logs needs no reduction), log over [768, 1024), then log of 0..31 in 4 copies
+// (log 0 taken as 0): lane l reads copy l & 3, so the 32 lanes of a half-wave that look up
+// log(i ^ j) for shard indices i, j < 32 never meet on a bank (32 banks of 4 bytes per half-wave).
+constexpr uint32_t kV2Exp = 0, kV2Log = 768, kV2Log32 = 1024, kV2Tables = 1152;
 constexpr uint32_t kRankBins = 33;   // erasure counts 0..32
 // recs: the records of `win` segments of `groups` blocks, sorted together (sort window)
 __host__ __device__ inline SortLds sort_lds(uint32_t m, uint32_t k, uint32_t groups, uint32_t stride,
-                                            uint32_t win = 1) {
+                                            uint32_t win = 1, bool v2 = false) {
     SortLds l;
-    l.prows = 768;
+    l.prows = v2 ? kV2Tables : 768;
     l.dall = l.prows + (size_t)m * k;
     l.scratch = (l.dall + 32 + 15) & ~(size_t)15;
     l.pos = l.scratch + (size_t)groups * kGroupScratch;
@@ -51,22 +56,32 @@ __host__ __device__ inline uint32_t sort_window(uint32_t groups, int psort) {
     return groups < blocks ? blocks / groups : 1u;
 }
 
-template <uint32_t LPB>
+template <uint32_t LPB, bool V2>
 __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanArgs a, uint32_t segs, uint32_t win) {
     constexpr uint32_t G = kPlanSortThreads / LPB;   // blocks per workgroup segment
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     if (a.gate && *a.gate != a.gate_want) return;   // the classify kernel picked the direct path
     const PlanLayout lay = a.lay;
-    const SortLds L = sort_lds(a.m, a.k, G, lay.stride, win);
-    uint8_t* s_exp = smem;
-    uint8_t* s_log = smem + 512;
+    const SortLds L = sort_lds(a.m, a.k, G, lay.stride, win, V2);
+    uint8_t* s_exp = smem + (V2 ? kV2Exp : 0);
+    uint8_t* s_log = smem + (V2 ? kV2Log : 512);
+    // form 2: this lane's copy of log(0..31)
+    const uint8_t* s_l32 = smem + kV2Log32 + (threadIdx.x & 3u) * 32u;
     uint8_t* s_prows = smem + L.prows;
     uint32_t* s_pos = reinterpret_cast<uint32_t*>(smem + L.pos);
     const uint32_t k = a.k, m = a.m, n = k + m;
     const uint32_t gb = threadIdx.x / LPB, gl = threadIdx.x % LPB;   // block group, lane in group
-    // exp | log (768 bytes, contiguous in gf::kTables) as dwords, then the parity rows and dall:
-    // staged once per workgroup, which then plans `segs` consecutive segments of G blocks
-    {
+    // exp | log (768 bytes, contiguous in gf::kTables) as dwords (form 2: the layout above), then
+    // the parity rows and dall: staged once per workgroup, which then plans `segs` consecutive
+    // segments of G blocks
+    if constexpr (V2) {
+        for (uint32_t i = threadIdx.x; i < kV2Tables; i += kPlanSortThreads) {
+            const uint32_t j = i - kV2Log32;
+            smem[i] = i < kV2Log ? gf::kTables.exp[i % 255u]
+                    : i < kV2Log32 ? gf::kTables.log[i - kV2Log]
+                    : (j & 31u) ? gf::kTables.log[j & 31u] : (uint8_t)0;
+        }
+    } else {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(&gf::kTables);
         if (threadIdx.x < 192) reinterpret_cast<uint32_t*>(smem)[threadIdx.x] = src[threadIdx.x];
     }
@@ -143,6 +158,21 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
                     const uint32_t sj = S[gl];
                     C[gl] = (uint8_t)(sj < k ? (row[sj] ? s_exp[s_log[inv] + s_log[row[sj]]] : 0u) : inv);
                 }
+            } else if constexpr (V2) {
+                // form 2: D_p and N_r are the same sum for the shard t = s_p or i_r, over the set Y =
+                // the others X (complement form) or the inputs S; log32(0) = 0 drops the t = y term
+                // that the sums below skip by a compare. Lane q of the group takes t = S[q] (q < k)
+                // or O[q - k]: RS(20,30) both sets in one pass over 30 lanes; Nt = Dt + k.
+                const bool comp = n - k < k;
+                const uint32_t ny = comp ? n - k : k;
+                const uint8_t* Y = comp ? X : S;
+                for (uint32_t q = gl; q < k + e; q += LPB) {
+                    const uint32_t t = q < k ? S[q] : O[q - k];
+                    uint32_t s = 0;
+                    for (uint32_t u = 0; u < ny; ++u) s += s_l32[t ^ Y[u]];
+                    if (comp) s = s_dall[t] + 255u * 32u - s;
+                    Dt[q] = (uint8_t)(s % 255u);
+                }
             } else {
                 // Lagrange over the shard indices (rs_plan_kernel): D_p = sum_{q != p} log(s_p ^ s_q),
                 // N_r = sum_q log(i_r ^ s_q), coef[r][p] = exp(N_r - log(i_r ^ s_p) - D_p). With
@@ -181,8 +211,9 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
         if (nout >= 2 && gl < k) {
             const uint32_t sp = S[gl], dp = Dt[gl];
             for (uint32_t r = 0; r < nout; ++r) {
-                const uint32_t v = Nt[r] + 2u * 255u - s_log[O[r] ^ sp] - dp;
-                C[r * k + gl] = s_exp[v % 255u];
+                // < 765: form 2's exp needs no reduction
+                const uint32_t v = Nt[r] + 2u * 255u - (V2 ? s_l32[O[r] ^ sp] : s_log[O[r] ^ sp]) - dp;
+                C[r * k + gl] = s_exp[V2 ? v : v % 255u];
             }
         }
         // at the end of a sort window (or of the work): storage order of the window's records,
@@ -242,6 +273,7 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
 
 template <uint32_t LPB>
 hipError_t sorted_launch(const PlanArgs& a, hipStream_t s) {
+    const bool v2 = g_tune.dec_pv == 2;
     constexpr uint32_t G = kPlanSortThreads / LPB;
     const uint32_t nseg = (a.nblocks + G - 1) / G;
     if (nseg == 0) return hipSuccess;
@@ -254,8 +286,11 @@ hipError_t sorted_launch(const PlanArgs& a, hipStream_t s) {
     const uint32_t win = std::min<uint32_t>(sort_window(G, g_tune.dec_psort), 64);
     if (win > 1) segs = (segs + win - 1) / win * win;
     const uint32_t grid = (nseg + segs - 1) / segs;
-    const size_t lds = sort_lds(a.m, a.k, G, a.lay.stride, win).total;
-    hipLaunchKernelGGL((rs_plan_sorted_kernel<LPB>), dim3(grid), dim3(kPlanSortThreads), lds, s, a, segs, win);
+    const size_t lds = sort_lds(a.m, a.k, G, a.lay.stride, win, v2).total;
+    if (v2)
+        hipLaunchKernelGGL((rs_plan_sorted_kernel<LPB, true>), dim3(grid), dim3(kPlanSortThreads), lds, s, a, segs, win);
+    else
+        hipLaunchKernelGGL((rs_plan_sorted_kernel<LPB, false>), dim3(grid), dim3(kPlanSortThreads), lds, s, a, segs, win);
     return hipGetLastError();
 }
 

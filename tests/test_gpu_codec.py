@@ -351,8 +351,10 @@ def test_rs_encode_kernel_variants_match_oracle(codec, oracle, torch, variant, k
 # workgroup's 256-coefficient table, input addresses as per-block offsets), 18 and 19 the same with
 # rolling windows of 4 and 6 loads, 20 is 17 with the inputs split by 64-bit shifts, 21 is 17 with the
 # plan records sorted over 256-block windows (dec_psort 4; the rest over 64, the default), 22 is 17
-# with the records sorted per segment (dec_psort 0, the round-2 order)
-@pytest.mark.parametrize("wave", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22])
+# with the records sorted per segment (dec_psort 0, the round-2 order); 23 and 24 are 17 and 22 with
+# the plan kernel's form 2 (dec_pv 2: conflict-free log(i ^ j) table copies, merged D / N sums)
+@pytest.mark.parametrize("wave", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22,
+                                  23, 24])
 @pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10)])
 # L = 1008 / 1017: shards of 63 / 64 chunks, the edge of the two-block wave slices (rolling window)
 @pytest.mark.parametrize("L", [513, 1008, 1017, 1202, 1436])
@@ -375,9 +377,9 @@ def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, 
                            dec_direct=1 if wave in (7, 13, 14, 15) else 0,
                            dec_direct_big=1 if wave in (13, 14, 15) else 0, dec_gate=1 if wave in (14, 15) else 0,
                            dec_gate_pm=1000 if wave == 15 else 10,
-                           dec_sorted=0 if wave == 8 else 1, dec_fixk={9: 1, 16: 3, 17: 4, 18: 4, 19: 4, 20: 4, 21: 4, 22: 4}.get(wave, 2),
+                           dec_sorted=0 if wave == 8 else 1, dec_fixk={9: 1, 16: 3, 17: 4, 18: 4, 19: 4, 20: 4, 21: 4, 22: 4, 23: 4, 24: 4}.get(wave, 2),
                            dec_win={18: 4, 19: 6}.get(wave, 0), dec_s64=1 if wave == 20 else 0,
-                           dec_psort={21: 4, 22: 0}.get(wave, 1),
+                           dec_psort={21: 4, 22: 0, 24: 0}.get(wave, 1), dec_pv=2 if wave in (23, 24) else 1,
                            dec_tier={10: 1, 11: 2, 12: 4}.get(wave, 0))
     try:
         out = torch.full((B, m, S), 0xEE, dtype=torch.uint8, device="cuda")
@@ -389,6 +391,35 @@ def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, 
             miss = [i for i in range(k) if not (masks[b] >> i) & 1]
             for r, i in enumerate(miss):
                 assert np.array_equal(got[b, r, :L], sh[b, i, :L]), (b, r, i)
+        codec.rs_reconstruct_split(k, m, data, par, dm, shard_len=L)
+        codec.sync()
+        assert np.array_equal(data.cpu().numpy()[:, :, :L], sh[:, :k, :L])
+    finally:
+        codec.set_tuning(**old)
+
+
+# The sorted plan kernel's two forms on codes of both sum forms: n - k < k sums over the
+# complement (RS(16,24), RS(20,30), RS(9,10)), n - k >= k over the inputs (RS(4,12), RS(8,16),
+# RS(10,32), RS(1,4)), with 1..min(k, m) data erasures and parity losses mixed in.
+@pytest.mark.parametrize("pv", [1, 2])
+@pytest.mark.parametrize("k,m", [(16, 8), (20, 10), (9, 1), (4, 8), (8, 8), (10, 22), (1, 3)])
+def test_rs_plan_forms_match_oracle(codec, oracle, torch, pv, k, m):
+    rng = np.random.default_rng(1000 * k + m + pv)
+    n, B, L = k + m, 517, 1202
+    S = (L + 15) // 16 * 16
+    sh = _rand_shards(rng, B, n, S, L)
+    oracle.rs_encode(k, m, sh)
+    masks = _random_masks(rng, B, k, m)
+    data_np = np.ascontiguousarray(sh[:, :k]).copy()
+    for b in range(B):
+        for i in range(k):
+            if not (masks[b] >> i) & 1:
+                data_np[b, i] = 0x5A
+    par = torch.from_numpy(np.ascontiguousarray(sh[:, k:])).cuda()
+    dm = torch.from_numpy(masks.view(np.int32)).cuda()
+    old = codec.set_tuning(dec_pv=pv, dec_direct=0)
+    try:
+        data = torch.from_numpy(data_np).cuda()
         codec.rs_reconstruct_split(k, m, data, par, dm, shard_len=L)
         codec.sync()
         assert np.array_equal(data.cpu().numpy()[:, :, :L], sh[:, :k, :L])

@@ -196,9 +196,155 @@ static void *run(void *arg) {
     return NULL;
 }
 
+static int cmp_dbl(const void *a, const void *b) {
+    const double x = *(const double *)a, y = *(const double *)b;
+    return x < y ? -1 : x > y;
+}
+
+static double pct(const double *s, int n, double p) {
+    int i = (int)(p * (n - 1) + 0.5);
+    return s[i < 0 ? 0 : i >= n ? n - 1 : i];
+}
+
+/* Receive-side stall of one run-loop burst (connection.go.diff handleRecoveredFEC): N recoverable
+ * blocks (source 0 lost, repair 0 received) are submitted, then
+ *   block:  fec_go_decoder_poll(wait=1) until all N are back: the time the run loop is held;
+ *   poll:   one fec_go_decoder_poll(wait=0) right after the submits (it launches the staged set),
+ *           the time the run loop is held; then non-blocking polls until all N are back: the
+ *           completion latency the recovered frames see.
+ * Timed per burst over `reps` bursts; prints p50 / p99 / max in microseconds. */
+static int burst(int k, int m, int N, int reps, size_t len, int ref) {
+    const int pool_blocks = N * 4 > 256 ? N * 4 : 256;   /* distinct blocks, reused round robin */
+    const size_t maxb = (size_t)(N > 64 ? N : 64);
+    uint8_t *pay = malloc((size_t)pool_blocks * k * len), *reps_buf = calloc((size_t)pool_blocks * m, FEC_GO_SLOT);
+    uint64_t x = 0xB0057;
+    for (size_t i = 0; i < (size_t)pool_blocks * k * len; ++i) {
+        x = x * 6364136223846793005ull + 1442695040888963407ull;
+        pay[i] = (uint8_t)(x >> 56);
+    }
+    const uint8_t **ptrs = malloc((size_t)(k + m) * sizeof *ptrs);
+    size_t *lens = malloc((size_t)(k + m) * sizeof *lens);
+    uint64_t *ids = malloc(maxb * 8), *offs = malloc(maxb * 8);
+    uint32_t *rl = malloc(maxb * 4);
+    uint8_t *rp = malloc(maxb * (size_t)m * FEC_GO_SLOT), *out = malloc(maxb * len);
+    int rc = 0;
+    fec_go_encoder *e = fec_go_encoder_new(FEC_SCHEME_REED_SOLOMON, k, m, maxb, 0, &rc);
+    fec_go_decoder *d = fec_go_decoder_new(FEC_SCHEME_REED_SOLOMON, k, m, maxb, 0, &rc);
+    if (!e || !d) {
+        fprintf(stderr, "new: %d %s\n", rc, fec_last_error());
+        return 1;
+    }
+    /* repairs of every pool block (outside the timing) */
+    uint32_t rlen = 0;
+    for (int b = 0, polled = 0; b < pool_blocks; ++b) {
+        for (int i = 0; i < k; ++i) {
+            ptrs[i] = pay + ((size_t)b * k + i) * len;
+            lens[i] = len;
+        }
+        if (fec_go_encoder_submit(e, (uint64_t)b, ptrs, lens, k)) return 1;
+        while (polled <= b) {
+            size_t got = 0;
+            if (fec_go_encoder_poll(e, 1, ids, rl, rp, maxb, &got)) return 1;
+            for (size_t q = 0; q < got; ++q, ++polled) {
+                memcpy(reps_buf + (size_t)ids[q] * m * FEC_GO_SLOT, rp + q * m * FEC_GO_SLOT, (size_t)m * FEC_GO_SLOT);
+                rlen = rl[q];
+            }
+        }
+    }
+    fec_go_pool *pool = NULL;
+    uint8_t *pbase = NULL;
+    if (ref) {   /* received payloads as the wire parser leaves them: in registered pool buffers */
+        pool = fec_go_pool_new((size_t)pool_blocks * (k + 1), &pbase, &rc);
+        if (!pool) return 1;
+        for (int b = 0; b < pool_blocks; ++b) {
+            for (int i = 0; i < k; ++i)
+                memcpy(pbase + ((size_t)b * (k + 1) + i) * FEC_GO_POOL_SLOT, pay + ((size_t)b * k + i) * len, len);
+            memcpy(pbase + ((size_t)b * (k + 1) + k) * FEC_GO_POOL_SLOT, reps_buf + (size_t)b * m * FEC_GO_SLOT, rlen);
+        }
+    }
+    double *held = malloc((size_t)reps * sizeof(double)), *lat = malloc((size_t)reps * sizeof(double));
+    uint64_t next_id = 0;
+    for (int policy = 0; policy < 2; ++policy) {
+        for (int r = -8; r < reps; ++r) {   /* 8 untimed bursts first */
+            const double t0 = now();
+            for (int j = 0; j < N; ++j) {
+                const int b = (int)(next_id % (uint64_t)pool_blocks);
+                const uint8_t *base = ref ? pbase + (size_t)b * (k + 1) * FEC_GO_POOL_SLOT : NULL;
+                ptrs[0] = NULL;
+                lens[0] = 0;
+                for (int i = 1; i < k; ++i) {
+                    ptrs[i] = ref ? base + (size_t)i * FEC_GO_POOL_SLOT : pay + ((size_t)b * k + i) * len;
+                    lens[i] = len;
+                }
+                for (int p = 0; p < m; ++p) {
+                    ptrs[k + p] = p ? NULL : ref ? base + (size_t)k * FEC_GO_POOL_SLOT : reps_buf + (size_t)b * m * FEC_GO_SLOT;
+                    lens[k + p] = p ? 0 : rlen;
+                }
+                int st = 0;
+                if ((ref ? fec_go_decoder_submit_ref : fec_go_decoder_submit)(d, next_id, next_id * k, next_id * k + k - 1,
+                                                                              (int)len, ptrs, lens, ptrs + k, lens + k, &st) ||
+                    !st) {
+                    fprintf(stderr, "dsubmit: %s\n", fec_last_error());
+                    return 1;
+                }
+                ++next_id;
+            }
+            size_t done = 0, got = 0;
+            double t_held = 0;
+            if (policy == 0) {
+                while (done < (size_t)N) {
+                    if (fec_go_decoder_poll(d, 1, ids, rl, offs, out, maxb * len, maxb, &got)) return 1;
+                    done += got;
+                }
+                t_held = now() - t0;
+            } else {
+                if (fec_go_decoder_poll(d, 0, ids, rl, offs, out, maxb * len, maxb, &got)) return 1;
+                done += got;
+                t_held = now() - t0;
+                while (done < (size_t)N) {
+                    if (fec_go_decoder_poll(d, 0, ids, rl, offs, out, maxb * len, maxb, &got)) return 1;
+                    done += got;
+                }
+            }
+            const double t_done = now() - t0;
+            /* the last recovered payload must be its block's lost source 0 */
+            const int b = (int)((next_id - 1) % (uint64_t)pool_blocks);
+            if (got && memcmp(out + offs[got - 1], pay + (size_t)b * k * len, len)) {
+                fprintf(stderr, "mismatch at burst %d\n", r);
+                return 1;
+            }
+            if (r >= 0) held[r] = t_held * 1e6, lat[r] = t_done * 1e6;
+        }
+        qsort(held, (size_t)reps, sizeof(double), cmp_dbl);
+        qsort(lat, (size_t)reps, sizeof(double), cmp_dbl);
+        printf("{\"mode\": \"burst\", \"scheme\": \"RS(%d,%d)\", \"submit\": \"%s\", \"policy\": \"%s\", \"burst_blocks\": %d, "
+               "\"bursts\": %d, \"run_loop_held_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f}, "
+               "\"recovered_after_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f}, \"held_us_per_block_p50\": %.2f}\n",
+               k, k + m, ref ? "ref" : "copy", policy ? "poll (wait=0), re-poll" : "block (wait=1)", N, reps,
+               pct(held, reps, 0.5), pct(held, reps, 0.99), held[reps - 1], pct(lat, reps, 0.5), pct(lat, reps, 0.99),
+               lat[reps - 1], pct(held, reps, 0.5) / N);
+        fflush(stdout);
+    }
+    fec_go_encoder_free(e);
+    fec_go_decoder_free(d);
+    if (pool) fec_go_pool_free(pool);
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc >= 2 && !strcmp(argv[1], "burst")) {
+        if (argc < 6) {
+            fprintf(stderr, "usage: %s burst k m N reps [len] [copy|ref]\n", argv[0]);
+            return 2;
+        }
+        const int rc = burst(atoi(argv[2]), atoi(argv[3]), atoi(argv[4]), atoi(argv[5]),
+                             argc > 6 ? (size_t)atoi(argv[6]) : 1200, argc > 7 && !strcmp(argv[7], "ref"));
+        fflush(stdout);
+        _exit(rc);
+    }
     if (argc < 6) {
-        fprintf(stderr, "usage: %s rs|xor k m blocks max_blocks [len] [threads]\n", argv[0]);
+        fprintf(stderr, "usage: %s rs|xor k m blocks max_blocks [len] [threads] [copy|ref]\n"
+                        "       %s burst k m N reps [len] [copy|ref]\n", argv[0], argv[0]);
         return 2;
     }
     const int xr = !strcmp(argv[1], "xor");

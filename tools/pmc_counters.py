@@ -8,6 +8,8 @@ dispatch), plus derived figures:
   wait_frac             SQ_WAIT_ANY / SQ_WAVE_CYCLES (parked on s_waitcnt / barrier)
   valu_simd_util        SQ_ACTIVE_INST_VALU * 4 / (1024 SIMDs * GRBM_GUI_ACTIVE / 8)
                         (quad-cycles -> cycles; GRBM_GUI_ACTIVE is summed over the 8 XCDs)
+  lds_conflict_frac     SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (LDS cycles lost to bank conflicts)
+  lds_busy_frac         SQ_LDS_IDX_ACTIVE / (256 CUs * GRBM_GUI_ACTIVE / 8)
   clock_ghz             GRBM_GUI_ACTIVE / 8 / kernel duration (when a kernel-trace is present)
   read_bytes / write_bytes  2 * FETCH_SIZE KiB (gfx950 correction) / WRITE_SIZE KiB
 
@@ -61,6 +63,12 @@ def main():
         g = c.get("GRBM_GUI_ACTIVE")
         if g and "SQ_ACTIVE_INST_VALU" in c:
             d["valu_simd_util"] = c["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * g / 8)
+        if c.get("SQ_LDS_IDX_ACTIVE"):
+            # share of the LDS's indexed-access cycles lost to bank conflicts
+            d["lds_conflict_frac"] = c.get("SQ_LDS_BANK_CONFLICT", 0.0) / c["SQ_LDS_IDX_ACTIVE"]
+        if g and "SQ_LDS_IDX_ACTIVE" in c:
+            # LDS busy share of the kernel's cycles, per CU (256 CUs; GRBM_GUI_ACTIVE summed over 8 XCDs)
+            d["lds_busy_frac"] = c["SQ_LDS_IDX_ACTIVE"] / (256 * g / 8)
         if "FETCH_SIZE" in c:
             d["read_bytes"] = 2 * c["FETCH_SIZE"] * 1024
         if "WRITE_SIZE" in c:
