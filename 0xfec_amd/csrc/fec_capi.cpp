@@ -142,6 +142,12 @@ struct fec_ctx {
     int ncu = 256;           // compute units of the device
     HostPipe pipe;           // host-resident path (FEC_HOST / FEC_HOST_PINNED)
     hipEvent_t handoff = nullptr;   // orders a newly set stream after the previous one
+    // multi-erasure decode with the plan kernels of later sub-batches beside the rebuild of earlier
+    // ones (knob dec_povl): the plans run on `side` (high priority), each sub-batch's rebuild waits
+    // for its plan's event; side_in orders the side stream after the calling stream
+    hipStream_t side = nullptr;
+    hipEvent_t side_in = nullptr;
+    hipEvent_t side_ev[8] = {};
 };
 
 #define HIP_TRY(expr)                      \
@@ -396,6 +402,16 @@ static int rs_encode_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks
     return FEC_OK;
 }
 
+static int ensure_side(fec_ctx* ctx) {
+    if (ctx->side) return FEC_OK;
+    int least = 0, greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIP_TRY(hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, greatest));
+    HIP_TRY(hipEventCreateWithFlags(&ctx->side_in, hipEventDisableTiming));
+    for (hipEvent_t& e : ctx->side_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return FEC_OK;
+}
+
 static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks, uint8_t* data,
                                  size_t dbs, const uint8_t* parity, size_t pbs, size_t ss, const uint32_t* masks,
                                  int32_t* status, int* err, uint8_t* out = nullptr, size_t out_bs = 0,
@@ -440,8 +456,71 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         const int rc = grow_hard(ctx, (per_launch * cps + 63) / 64);
         if (rc) return rc;
     }
+    // plans of sub-batch j + 1 beside the rebuild of sub-batch j (knob dec_povl = sub-batches per
+    // launch, each a multiple of 64 blocks, the plan sort window)
+    const int povl = std::min(fk::g_tune.dec_povl, 8);
+    const bool overlap = povl > 1 && sorted && wave && !fused && !tiered && !direct && !gated &&
+                         fk::rebuild_k_applies(k, maxe, cps) && nblocks >= (size_t)povl * 1024;
+    if (overlap) {
+        const int rc = ensure_side(ctx);
+        if (rc) return rc;
+    }
     for (size_t b0 = 0; b0 < nblocks; b0 += per_launch) {
         const size_t nb = std::min(per_launch, nblocks - b0);
+        if (overlap) {
+            HIP_TRY(hipEventRecord(ctx->side_in, ctx->stream));
+            HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->side_in, 0));
+            const size_t sub = (nb + povl - 1) / povl + 63 & ~(size_t)63;
+            int j = 0;
+            for (size_t s0 = 0; s0 < nb; s0 += sub, ++j) {   // every plan first, on the side stream
+                const size_t snb = std::min(sub, nb - s0);
+                fk::PlanArgs p{};
+                p.masks = masks + b0 + s0;
+                p.plans = ctx->work->d_plans + s0 * lay.stride;
+                p.status = status ? status + b0 + s0 : nullptr;
+                p.err = err;
+                p.prows = code->d_prows;
+                p.k = k;
+                p.m = m;
+                p.nblocks = (uint32_t)snb;
+                p.maxe = maxe;
+                p.lay = lay;
+                p.max_out = out ? out_slots : 0;
+                p.dall = code->d_dall;
+                HIP_TRY(fk::launch_rs_plan_sorted(p, ctx->side));
+                HIP_TRY(hipEventRecord(ctx->side_ev[j], ctx->side));
+            }
+            j = 0;
+            for (size_t s0 = 0; s0 < nb; s0 += sub, ++j) {   // each rebuild after its plan
+                const size_t snb = std::min(sub, nb - s0);
+                HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->side_ev[j], 0));
+                fk::ReconArgs a{};
+                a.data = data + (b0 + s0) * dbs;
+                a.parity = parity + (b0 + s0) * pbs;
+                a.dbs = dbs;
+                a.pbs = pbs;
+                a.ss = ss;
+                a.pss = pss;
+                a.plans = ctx->work->d_plans + s0 * lay.stride;
+                a.k = k;
+                a.len = (uint32_t)len;
+                a.cps = cps;
+                a.nblocks = (uint32_t)snb;
+                a.maxe = maxe;
+                a.lay = lay;
+                a.g = G;
+                a.ntiles = (uint32_t)((snb + G - 1) / G);
+                a.div_cps = fk::make_fastdiv(cps);
+                a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
+                a.rot = fk::g_tune.rotate ? fk::line_rotation(ss, cps) : 0;
+                a.swz = (uint32_t)fk::g_tune.dec_swz;
+                a.sorted = 1u;
+                a.out = out ? out + (b0 + s0) * out_bs : nullptr;
+                a.out_bs = out_bs;
+                HIP_TRY(fk::launch_rs_rebuild_k(a, ctx->stream));
+            }
+            continue;
+        }
         fk::PlanArgs p{};
         p.masks = masks + b0;
         p.plans = ctx->work->d_plans;
@@ -1161,6 +1240,13 @@ void fec_ctx_destroy(fec_ctx* ctx) {
     for (hipStream_t q : {p.up, p.comp, p.down})
         if (q) (void)hipStreamDestroy(q);
     if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
+    if (ctx->side) {
+        (void)hipStreamSynchronize(ctx->side);
+        (void)hipStreamDestroy(ctx->side);
+    }
+    for (hipEvent_t e : ctx->side_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->side_in) (void)hipEventDestroy(ctx->side_in);
     if (ctx->own) (void)hipStreamDestroy(ctx->own);
     (void)hipGetLastError();
     delete ctx;
@@ -1214,7 +1300,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 34 ? &fk::g_tune.dec_gate : key == 35 ? &fk::g_tune.dec_gate_pm
               : key == 36 ? &fk::g_tune.host_gather : key == 37 ? &fk::g_tune.dec_win
               : key == 38 ? &fk::g_tune.dec_s64
-              : key == 39 ? &fk::g_tune.dec_psort : key == 40 ? &fk::g_tune.dec_pv : nullptr;
+              : key == 39 ? &fk::g_tune.dec_psort : key == 40 ? &fk::g_tune.dec_pv
+              : key == 41 ? &fk::g_tune.dec_povl : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

@@ -206,6 +206,9 @@ struct Tuning {
                               // decode time, RS(16,24) -3 % (rebuild rows; a cheaper ranking); 256 / 512
                               // cost the plan kernel residency (its LDS) more than the rebuild gains (r03y)
     int dec_s64 = 0;          // fec_rebuild.hip: input splits by 64-bit shifts (two dwords a shift)
+    int dec_povl = 0;         // multi-erasure decode (sorted plans + fec_rebuild.hip): sub-batches per launch
+                              // whose plan kernels run on a high-priority side stream beside the rebuild of
+                              // the sub-batches before them (0 / 1: one plan launch, then one rebuild)
     int dec_pv = 1;           // sorted plan kernel form: 1, or 2 (log(i ^ j) of shard indices from a 4-copy
                               // table no half-wave meets on a bank; D_p and N_r in one merged pass; exp
                               // over [0, 768) so the coefficient sums need no reduction)

@@ -210,7 +210,33 @@ def cpu_baseline(k, m, blocks, seed, budget_s=12.0):
     best = max(trial, key=trial.get) if trial else orc.ISA_SCALAR
     value, reps = rate(best, 200, budget_s)
     scalar, sreps = rate(orc.ISA_SCALAR, 3, 0.0)
+
+    def one_core(kk, mm, nb=4096):
+        """One thread's per-block time (us) for encode and single-erasure ReconstructData, the
+        fastest ISA, amortised over nb blocks: what one connection's run loop would spend coding
+        a block itself (the yardstick of the receive-side burst stall)."""
+        nn = kk + mm
+        s1 = np.zeros((nb, nn, SHARD_LEN), dtype=np.uint8)
+        s1[:, :kk] = rng.integers(0, 256, (nb, kk, SHARD_LEN), dtype=np.uint8)
+        m1 = np.full(nb, ((1 << nn) - 1) & ~1, dtype=np.uint32)
+        out = None
+        for isa in isas or [orc.ISA_SCALAR]:
+            orc.rs_encode_simd(kk, mm, s1, isa, threads=1)
+            te, td = [], []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                orc.rs_encode_simd(kk, mm, s1, isa, threads=1)
+                t1 = time.perf_counter()
+                orc.rs_reconstruct_simd(kk, mm, s1, m1, isa, threads=1)
+                te.append(t1 - t0)
+                td.append(time.perf_counter() - t1)
+            cand = (min(te) / nb * 1e6, min(td) / nb * 1e6, orc.isa_name(isa))
+            if out is None or cand[0] + cand[1] < out[0] + out[1]:
+                out = cand
+        return {"encode_us": round(out[0], 3), "reconstruct_1_erasure_us": round(out[1], 3), "isa": out[2]}
+
     return {"value": round(value, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "single_core": {"RS(%d,%d)" % (kk, kk + mm): one_core(kk, mm) for kk, mm in ((k, m), (20, 10))},
             "isa": orc.isa_name(best),
             "sample": "%d reps x %d blocks RS(%d,%d) 1202-B shards, encode + 1-erasure ReconstructData, "
                       "oracle/fec_simd.c (klauspost kernel method restated, bit-exact vs the scalar oracle), "

@@ -377,6 +377,10 @@ func (m *batchManager) PollRecovered(wait bool) ([][]byte, error) {
 // stream does not drain the pool).
 func (m *batchManager) RecoveryPending() bool { return m.pending > 0 || len(m.release) > 0 }
 
+// RecoveriesInFlight: staged blocks whose data has not been handed out (the connection re-polls
+// while there are any).
+func (m *batchManager) RecoveriesInFlight() bool { return m.pending > 0 }
+
 // Close is the connection's teardown (go/patches/connection.go.diff, after the run loop ends):
 // the library encoder / decoder is freed first, which waits for a batch still in flight (the
 // device may be reading pool buffers by reference), then every pool buffer this manager still

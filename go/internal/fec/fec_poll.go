@@ -20,11 +20,14 @@ type RepairPoller interface {
 // HandleRepairFrame stages a block that becomes recoverable and returns no data
 // (manager.go:181-193 returns it at once), and the block data of finished blocks
 // (recoverSymbolPayloads' result, reed_solomon.go:128-133) comes from PollRecovered in staging
-// order. wait: start and wait for every staged block. RecoveryPending reports staged blocks
-// whose data has not been handed out yet.
+// order. wait: start and wait for every staged block; else hand over what has finished and start
+// what is staged. RecoveryPending reports staged blocks whose data has not been handed out yet
+// (or received buffers to give back); RecoveriesInFlight only the former, for which the
+// connection schedules a re-poll (go/patches/connection.go.diff, maybeResetTimer).
 type RecoveredPoller interface {
 	PollRecovered(wait bool) ([][]byte, error)
 	RecoveryPending() bool
+	RecoveriesInFlight() bool
 }
 
 // PayloadAllocator is a Sender that wants SOURCE_SYMBOL payloads built in buffers of its own (the

@@ -427,6 +427,40 @@ def test_rs_plan_forms_match_oracle(codec, oracle, torch, pv, k, m):
         codec.set_tuning(**old)
 
 
+# The plan kernels of later sub-batches on a side stream beside the rebuild of earlier ones (knob
+# dec_povl): batches of several sub-batches with a ragged last one, out of place and in place.
+@pytest.mark.parametrize("povl,pv", [(2, 1), (4, 2), (8, 1), (3, 2)])
+@pytest.mark.parametrize("k,m", [(16, 8), (20, 10)])
+def test_rs_plan_overlap_matches_oracle(codec, oracle, torch, povl, pv, k, m):
+    rng = np.random.default_rng(7 * k + povl + pv)
+    n, B, L = k + m, 9000 + 37, 1202
+    S = (L + 15) // 16 * 16
+    sh = _rand_shards(rng, B, n, S, L)
+    oracle.rs_encode(k, m, sh)
+    masks = _random_masks(rng, B, k, m)
+    data_np = np.ascontiguousarray(sh[:, :k]).copy()
+    lost = ~((masks[:, None] >> np.arange(k)[None, :]) & 1).astype(bool)
+    data_np[lost] = 0x77
+    par = torch.from_numpy(np.ascontiguousarray(sh[:, k:])).cuda()
+    dm = torch.from_numpy(masks.view(np.int32)).cuda()
+    old = codec.set_tuning(dec_povl=povl, dec_pv=pv, dec_direct=0)
+    try:
+        data = torch.from_numpy(data_np).cuda()
+        out = torch.full((B, m, S), 0xEE, dtype=torch.uint8, device="cuda")
+        codec.rs_recover_split(k, m, data, par, dm, out, shard_len=L)
+        codec.sync()
+        got = out.cpu().numpy()
+        ne = lost.sum(axis=1)
+        for b in np.flatnonzero(ne):
+            miss = np.flatnonzero(lost[b])
+            assert np.array_equal(got[b, :len(miss), :L], sh[b, miss, :L]), b
+        codec.rs_reconstruct_split(k, m, data, par, dm, shard_len=L)
+        codec.sync()
+        assert np.array_equal(data.cpu().numpy()[:, :, :L], sh[:, :k, :L])
+    finally:
+        codec.set_tuning(**old)
+
+
 def test_rs_32_0_fully_present_is_untouched(codec, torch, fec):
     """k = 32, m = 0 (n = 32: the widest present mask): a fully present block rebuilds nothing,
     in place or out of place (klauspost ReconstructData with every shard present is a no-op)."""

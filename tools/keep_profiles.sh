@@ -20,5 +20,12 @@ cp_if "$S/kernel_trace_summary.json" "$D/bench_${TAG}_kernel_trace_summary.json"
 cp_if "$S/prof/run_kernel_stats.csv" "$D/bench_${TAG}_kernel_stats.csv"
 cp_if "$S/pmc_traffic.json" "$D/pmc_traffic_$TAG.json"
 cp_if "$S/counters/counters.json" "$D/counters_$TAG.json"
+cp_if "$S/go_burst.log" "$D/go_burst_$TAG.log"
+cp_if "$S/pcie_duplex_probe.log" "$D/pcie_duplex_probe_$TAG.log"
+cp_if "$S/zerocopy_probe.log" "$D/zerocopy_probe_$TAG.log"
+cp_if "$S/pytest_variants.log" "$D/pytest_variants_$TAG.log"
+cp_if "$S/bench_torchrun_n1_rccl.log" "$D/bench_torchrun_n1_rccl_$TAG.log"
+for f in "$S"/ab_*.log; do cp_if "$f" "$D/$(basename "$f" .log)_$TAG.log"; done
+for d in "$S"/counters_*/; do cp_if "$d/counters.json" "$D/$(basename "$d")_$TAG.json"; done
 if [ -f "$S/pmc_traffic.json" ]; then cp "$S/pmc_traffic.json" profiles/pmc_traffic_latest.json; fi
 ls "$D" | grep "$TAG"
