@@ -38,6 +38,57 @@ def source_hash(tu):
     return h.hexdigest()[:16]
 
 
+def kernel_code_hashes(lib=LIB):
+    """sha256 (first 16 hex digits) of each gfx950 kernel's machine code in the built library:
+    {demangled kernel name: hash}. The code objects are read from the clang offload bundles in
+    the library's .hip_fatbin data, each kernel's bytes from its symbol in the code object's
+    .text. A PMC traffic profile records these (tools/pmc_traffic.py) and bench.py reports the
+    profile's traffic only while the kernel it runs has the same code: edits elsewhere (another
+    kernel, a host launch knob in a shared header) do not retire a profile, a changed kernel does."""
+    import hashlib
+    import shutil
+    import struct
+    with open(lib, "rb") as fh:
+        blob = fh.read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    syms = {}
+    at = blob.find(magic)
+    while at >= 0:
+        nent = struct.unpack_from("<Q", blob, at + 24)[0]
+        off = at + 32
+        for _ in range(nent):
+            eo, esz, tl = struct.unpack_from("<QQQ", blob, off)
+            triple = blob[off + 24:off + 24 + tl].decode()
+            off += 24 + tl
+            if triple.endswith("gfx950") and esz:
+                elf = blob[at + eo:at + eo + esz]
+                shoff, = struct.unpack_from("<Q", elf, 0x28)
+                shentsize, shnum = struct.unpack_from("<HH", elf, 0x3A)
+                secs = [struct.unpack_from("<IIQQQQIIQQ", elf, shoff + i * shentsize) for i in range(shnum)]
+                for name_i, typ, _, addr, soff, size, link, _, _, entsize in secs:
+                    if typ != 2:   # SHT_SYMTAB
+                        continue
+                    stroff = secs[link][4]
+                    for s in range(size // entsize):
+                        st_name, st_info, _, st_shndx, st_value, st_size = struct.unpack_from(
+                            "<IBBHQQ", elf, soff + s * entsize)
+                        if st_info & 0xF != 2 or not st_size or st_shndx >= len(secs):   # STT_FUNC
+                            continue
+                        end = elf.index(b"\0", stroff + st_name)
+                        sym = elf[stroff + st_name:end].decode()
+                        tsec = secs[st_shndx]
+                        start = tsec[4] + (st_value - tsec[3])
+                        syms[sym] = hashlib.sha256(elf[start:start + st_size]).hexdigest()[:16]
+        at = blob.find(magic, at + 1)
+    filt = next((c for c in ("/opt/rocm/lib/llvm/bin/llvm-cxxfilt", shutil.which("llvm-cxxfilt"),
+                             shutil.which("c++filt")) if c and os.path.exists(c)), None)
+    names = list(syms)
+    if filt and names:
+        out = subprocess.run([filt], input="\n".join(names), capture_output=True, text=True, check=True).stdout
+        return dict(zip(out.splitlines(), (syms[n] for n in names)))
+    return syms
+
+
 def _hipcc():
     for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
         if c and (os.path.sep not in c or os.path.exists(c)):

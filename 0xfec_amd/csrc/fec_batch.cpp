@@ -602,10 +602,18 @@ Error BatchDecoder::init() {
             (h = hipHostMalloc(&s.h_desc, maxBlocks_ * n * sizeof(fk::GatherDesc), hipHostMallocDefault)) != hipSuccess ||
             (h = hipMalloc(&s.d_desc, maxBlocks_ * n * sizeof(fk::GatherDesc))) != hipSuccess)
             return hip_error(h, "staging allocation");
-        void* in_dev = nullptr;
-        if ((h = hipHostGetDevicePointer(&in_dev, s.h_in, 0)) != hipSuccess)
+        void *in_dev = nullptr, *out_dev = nullptr, *masks_dev = nullptr, *status_dev = nullptr, *desc_dev = nullptr;
+        if ((h = hipHostGetDevicePointer(&in_dev, s.h_in, 0)) != hipSuccess ||
+            (h = hipHostGetDevicePointer(&out_dev, s.h_out, 0)) != hipSuccess ||
+            (h = hipHostGetDevicePointer(&masks_dev, s.h_masks, 0)) != hipSuccess ||
+            (h = hipHostGetDevicePointer(&status_dev, s.h_status, 0)) != hipSuccess ||
+            (h = hipHostGetDevicePointer(&desc_dev, s.h_desc, 0)) != hipSuccess)
             return hip_error(h, "hipHostGetDevicePointer");
         s.in_dev = (uint64_t)(uintptr_t)in_dev;
+        s.out_dev = static_cast<uint8_t*>(out_dev);
+        s.masks_dev = static_cast<uint32_t*>(masks_dev);
+        s.status_dev = static_cast<int32_t*>(status_dev);
+        s.desc_dev = desc_dev;
         hipEvent_t ev;
         if ((h = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hip_error(h, "hipEventCreate");
         s.done = ev;
@@ -800,31 +808,47 @@ Error BatchDecoder::flushImpl(size_t* delivered) {
     const size_t B = s.blocks.size(), n = (size_t)k_ + m_, S = s.slot;
     const size_t nin = rs_ ? n : (size_t)k_;   // XOR stages its k inputs only
     hipError_t h;
+    // a small set (a receive burst of a few blocks) is coded straight from and into its pinned
+    // buffers: one launch (two when gathered) and an event, where the copy form makes four copies
+    // around the kernels, each a call of its own and a copy-engine round trip (knob bat_zc: input
+    // bytes up to which; go_batch_bench burst)
+    const bool zc = B * n * S <= (size_t)std::max(0, fk::g_tune.bat_zc);
+    uint8_t* in = zc ? reinterpret_cast<uint8_t*>((uintptr_t)s.in_dev) : s.d_in;
+    uint8_t* out = zc ? s.out_dev : s.d_out;
+    uint32_t* masks = zc ? s.masks_dev : s.d_masks;
+    int32_t* status = zc ? s.status_dev : s.d_status;
     if (s.gather) {   // referenced payloads: the device pulls every shard of the set itself
-        if ((h = hipMemcpyAsync(s.d_desc, s.h_desc, B * n * sizeof(fk::GatherDesc), hipMemcpyHostToDevice, st)) !=
-            hipSuccess)
-            return hip_error(h, "hipMemcpyAsync H2D");
+        const void* desc = s.desc_dev;
+        if (!zc) {
+            if ((h = hipMemcpyAsync(s.d_desc, s.h_desc, B * n * sizeof(fk::GatherDesc), hipMemcpyHostToDevice, st)) !=
+                hipSuccess)
+                return hip_error(h, "hipMemcpyAsync H2D");
+            desc = s.d_desc;
+        }
         if ((h = hipSetDevice(engine_->device())) != hipSuccess) return hip_error(h, "hipSetDevice");
-        if ((h = fk::launch_gather_desc(static_cast<const fk::GatherDesc*>(s.d_desc), (uint32_t)(B * n), s.d_in, S,
-                                        st)) != hipSuccess)
+        if ((h = fk::launch_gather_desc(static_cast<const fk::GatherDesc*>(desc), (uint32_t)(B * n), s.d_in, S, st)) !=
+            hipSuccess)
             return hip_error(h, "gather launch");
-    } else if ((h = hipMemcpyAsync(s.d_in, s.h_in, B * n * S, hipMemcpyHostToDevice, st)) != hipSuccess) {
+        in = s.d_in;
+    } else if (!zc && (h = hipMemcpyAsync(s.d_in, s.h_in, B * n * S, hipMemcpyHostToDevice, st)) != hipSuccess) {
         return hip_error(h, "hipMemcpyAsync H2D");
     }
     int rc;
     if (rs_) {
-        if ((h = hipMemcpyAsync(s.d_masks, s.h_masks, B * 4, hipMemcpyHostToDevice, st)) != hipSuccess)
+        if (!zc && (h = hipMemcpyAsync(s.d_masks, s.h_masks, B * 4, hipMemcpyHostToDevice, st)) != hipSuccess)
             return hip_error(h, "hipMemcpyAsync H2D");
-        rc = fec_rs_recover_batch(ctx, k_, m_, s.maxLen, B, s.d_in, n * S, s.d_in + (size_t)k_ * S, n * S, S,
-                                  s.d_masks, s.d_out, s.outSlots * S, (int)s.outSlots, s.d_status, FEC_DEVICE);
+        rc = fec_rs_recover_batch(ctx, k_, m_, s.maxLen, B, in, n * S, in + (size_t)k_ * S, n * S, S, masks, out,
+                                  s.outSlots * S, (int)s.outSlots, status, FEC_DEVICE);
     } else {
-        rc = fec_xor_encode_batch(ctx, (int)nin, s.maxLen, B, s.d_in, n * S, s.d_out, S, S, FEC_DEVICE);
+        rc = fec_xor_encode_batch(ctx, (int)nin, s.maxLen, B, in, n * S, out, S, S, FEC_DEVICE);
     }
     if (rc) return codec_rc(rc);
-    if ((h = hipMemcpyAsync(s.h_out, s.d_out, B * s.outSlots * S, hipMemcpyDeviceToHost, st)) != hipSuccess)
-        return hip_error(h, "hipMemcpyAsync D2H");
-    if (rs_ && (h = hipMemcpyAsync(s.h_status, s.d_status, B * 4, hipMemcpyDeviceToHost, st)) != hipSuccess)
-        return hip_error(h, "hipMemcpyAsync D2H");
+    if (!zc) {
+        if ((h = hipMemcpyAsync(s.h_out, s.d_out, B * s.outSlots * S, hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return hip_error(h, "hipMemcpyAsync D2H");
+        if (rs_ && (h = hipMemcpyAsync(s.h_status, s.d_status, B * 4, hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return hip_error(h, "hipMemcpyAsync D2H");
+    }
     if ((h = hipEventRecord((hipEvent_t)s.done, st)) != hipSuccess) return hip_error(h, "hipEventRecord");
     s.inFlight = true;
     s.delivered = 0;

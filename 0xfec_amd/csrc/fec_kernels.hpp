@@ -206,12 +206,21 @@ struct Tuning {
                               // decode time, RS(16,24) -3 % (rebuild rows; a cheaper ranking); 256 / 512
                               // cost the plan kernel residency (its LDS) more than the rebuild gains (r03y)
     int dec_s64 = 0;          // fec_rebuild.hip: input splits by 64-bit shifts (two dwords a shift)
+    int bat_zc = 0;           // batch decoder (fec_batch.cpp): sets of at most this many input bytes are coded
+                              // straight from / into their pinned buffers (device-mapped), no copies
+    int dec_lpad = 0;         // fec_rebuild.hip: the two blocks' PermTab rows of a wave slice 32 banks apart
+                              // (RS(16,24)'s unpadded rows share banks: 24 % LDS conflict cycles)
     int dec_povl = 0;         // multi-erasure decode (sorted plans + fec_rebuild.hip): sub-batches per launch
                               // whose plan kernels run on a high-priority side stream beside the rebuild of
-                              // the sub-batches before them (0 / 1: one plan launch, then one rebuild)
-    int dec_pv = 1;           // sorted plan kernel form: 1, or 2 (log(i ^ j) of shard indices from a 4-copy
+                              // the sub-batches before them (0 / 1: one plan launch, then one rebuild).
+                              // Measured slower (r04b: RS(20,30) 2 / 4 / 8 sub-batches -0.8 / -1.9 / -3.5 %,
+                              // RS(16,24) -0.9 / -2.0 / -4.3 %): the rebuild is VALU-bound, so a plan beside
+                              // it takes issue slots, and each sub-batch adds a launch tail. Off.
+    int dec_pv = 2;           // sorted plan kernel form: 1, or 2 (log(i ^ j) of shard indices from a 4-copy
                               // table no half-wave meets on a bank; D_p and N_r in one merged pass; exp
-                              // over [0, 768) so the coefficient sums need no reduction)
+                              // over [0, 768) so the coefficient sums need no reduction). Form 2: VALU
+                              // per plan wave 4446 -> 3171 (RS(20,30)), plan 211 -> 153 us, decode
+                              // U{1..10} 2930 -> 2872 us (+2.0 %); RS(16,24) +0.2 % (r04b)
     int host_gather = 1;      // FEC_HOST_PINNED reconstruct: parity planes that few blocks read are pulled by
                               // the device straight from the caller's pinned buffer, the rest by 2D DMA (0:
                               // every plane by DMA; 2: every plane by the device)

@@ -71,15 +71,22 @@ static_assert(kSplitCheck.t01[0xFF][0] == 0x1CE3FF00u && kSplitCheck.t01[0xFF][3
 constexpr uint32_t kTabLds = 256 * 16 + 256 * 4;   // the workgroup's copy of kPermTabSplit
 
 // A wave's LDS slice: PermTab words of R rows x K inputs for each of its WB blocks, the blocks'
-// input offsets, their plan records.
-template <int K, int R>
+// input offsets, their plan records. PAD: each block's table words start 128 bytes past a 256-byte
+// row from the other block's, so the two blocks' rows of one read sit 32 banks apart. Unpadded,
+// RS(16,24)'s 2048-byte T0|T1 and 512-byte T2 block strides are whole 256-byte rows: every table
+// read of a wave spanning two blocks meets itself on the same banks (SQ_LDS_BANK_CONFLICT 24 % of
+// the LDS cycles, r04b; RS(20,30)'s 3200-byte stride is 128 off already: 9 %).
+__host__ __device__ constexpr uint32_t half_row_off(uint32_t x) { return x + (128u + 256u - x % 256u) % 256u; }
+template <int K, int R, bool PAD = false>
 struct Slice {
     static constexpr uint32_t WB = 2;
-    static constexpr uint32_t t01 = 0;                        // uint4    [WB][R][K]
-    static constexpr uint32_t t2 = t01 + WB * R * K * 16;     // uint32_t [WB][R][K]
-    static constexpr uint32_t offs = t2 + WB * R * K * 4;     // uint64_t [WB][K]
+    static constexpr uint32_t bs01 = PAD ? half_row_off(R * K * 16) : R * K * 16;   // bytes per block
+    static constexpr uint32_t bs2 = PAD ? half_row_off(R * K * 4) : R * K * 4;
+    static constexpr uint32_t t01 = 0;                        // uint4    [WB][R][K], blocks bs01 apart
+    static constexpr uint32_t t2 = t01 + WB * bs01;           // uint32_t [WB][R][K], blocks bs2 apart
+    static constexpr uint32_t offs = t2 + WB * bs2;           // uint64_t [WB][K]
     static constexpr uint32_t plans = offs + WB * K * 8;      // [WB][stride]
-    static_assert(t2 % 16 == 0 && offs % 16 == 0 && plans % 16 == 0, "16-byte aligned parts");
+    static_assert(bs01 % 16 == 0 && t2 % 16 == 0 && offs % 16 == 0 && plans % 16 == 0, "16-byte aligned parts");
     __host__ __device__ static size_t bytes(uint32_t stride) { return plans + (size_t)WB * stride; }
 };
 
@@ -199,10 +206,10 @@ __device__ __forceinline__ void rebuild_rows(const ReconArgs& a, const uint8_t* 
 
 // Flat grid, one wave per 64 consecutive items of the (sorted) plan order; R: the code's largest
 // rebuilt row count (min(k, m)).
-template <int K, int R, int W, int POL, bool RP, bool S64>
+template <int K, int R, int W, int POL, bool RP, bool S64, bool PAD>
 __global__ __launch_bounds__(kThreads) void rs_rebuild_k_kernel(ReconArgs a) {
     constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
-    using S = Slice<K, R>;
+    using S = Slice<K, R, PAD>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     if (a.gate && *a.gate != a.gate_want) return;   // the classify kernel picked the direct path
     uint4* g01 = reinterpret_cast<uint4*>(smem);
@@ -214,8 +221,6 @@ __global__ __launch_bounds__(kThreads) void rs_rebuild_k_kernel(ReconArgs a) {
     const uint32_t lane = threadIdx.x & 63;
     const PlanLayout lay = a.lay;
     uint8_t* slice = smem + kTabLds + (size_t)wave * S::bytes(lay.stride);
-    uint4* t01 = reinterpret_cast<uint4*>(slice + S::t01);
-    uint32_t* t2 = reinterpret_cast<uint32_t*>(slice + S::t2);
     uint64_t* offs = reinterpret_cast<uint64_t*>(slice + S::offs);
     uint8_t* plans = slice + S::plans;
     const uint32_t total = a.nblocks * a.cps;
@@ -243,9 +248,8 @@ __global__ __launch_bounds__(kThreads) void rs_rebuild_k_kernel(ReconArgs a) {
             const uint32_t g = i >= c0 ? 1u : 0u;
             const uint32_t rem = i - (g ? c0 : 0u);
             const uint32_t coef = plans[g * lay.stride + lay.coef_off + rem];
-            const uint32_t at = g * (R * K) + rem;
-            t01[at] = g01[coef];
-            t2[at] = g2[coef];
+            reinterpret_cast<uint4*>(slice + S::t01 + g * S::bs01)[rem] = g01[coef];
+            reinterpret_cast<uint32_t*>(slice + S::t2 + g * S::bs2)[rem] = g2[coef];
         }
         // input j of block g at its data chunk + offs[g][j] (64-bit, wrapping)
         if (lane < nb * K) {
@@ -274,8 +278,8 @@ __global__ __launch_bounds__(kThreads) void rs_rebuild_k_kernel(ReconArgs a) {
     const uint32_t rb = a.sorted ? *reinterpret_cast<const uint32_t*>(P + lay.blk_off) : blk;
     uint8_t* dbase = a.data + (uint64_t)rb * a.dbs + (uint64_t)c * kChunk;
     uint8_t* obase = a.out ? a.out + (uint64_t)rb * a.out_bs + (uint64_t)c * kChunk : nullptr;
-    const uint4* T01 = t01 + g * (R * K);
-    const uint32_t* T2 = t2 + g * (R * K);
+    const uint4* T01 = reinterpret_cast<const uint4*>(slice + S::t01 + g * S::bs01);
+    const uint32_t* T2 = reinterpret_cast<const uint32_t*>(slice + S::t2 + g * S::bs2);
     const uint64_t* O = offs + g * K;
     const uint8_t* oi = P + lay.out_off;
     static_assert(R <= 10, "row bodies 1..10");
@@ -295,16 +299,22 @@ __global__ __launch_bounds__(kThreads) void rs_rebuild_k_kernel(ReconArgs a) {
 #undef FEC_RB_ROWS
 }
 
-// W: loads in flight per lane (knob dec_win; 0: by code)
-template <int K, int R, bool RP>
+// W: loads in flight per lane (knob dec_win; 0: by code); DW: the code's default window, the one
+// built with the padded slice too (knob dec_lpad)
+template <int K, int R, bool RP, int DW>
 hipError_t rebuild_launch(const ReconArgs& a, int w, hipStream_t s) {
     const uint64_t total = (uint64_t)a.nblocks * a.cps;
     const int grid = (int)((total + kThreads - 1) / kThreads);
     if (grid == 0) return hipSuccess;
+    const bool s64 = g_tune.dec_s64 != 0;
+    if (g_tune.dec_lpad && w == DW && !s64) {
+        const size_t lds = occupancy_lds(g_tune.dec_wpc, kTabLds + 4 * Slice<K, R, true>::bytes(a.lay.stride));
+        hipLaunchKernelGGL((rs_rebuild_k_kernel<K, R, DW, 3, RP, false, true>), dim3(grid), dim3(kThreads), lds, s, a);
+        return hipGetLastError();
+    }
     const size_t lds = occupancy_lds(g_tune.dec_wpc, kTabLds + 4 * Slice<K, R>::bytes(a.lay.stride));
 #define FEC_RB_LAUNCH(WW, S) \
-    hipLaunchKernelGGL((rs_rebuild_k_kernel<K, R, WW, 3, RP, S>), dim3(grid), dim3(kThreads), lds, s, a)
-    const bool s64 = g_tune.dec_s64 != 0;
+    hipLaunchKernelGGL((rs_rebuild_k_kernel<K, R, WW, 3, RP, S, false>), dim3(grid), dim3(kThreads), lds, s, a)
     if (w == 4 && s64) FEC_RB_LAUNCH(4, true);
     else if (w == 4) FEC_RB_LAUNCH(4, false);
     else if (w == 6 && s64) FEC_RB_LAUNCH(6, true);
@@ -326,8 +336,8 @@ hipError_t launch_rs_rebuild_k(const ReconArgs& a, hipStream_t s) {
     // windows by interleaved A/B (dec_select.py, r03k): RS(16,24) 8 -> 4 +0.3 %; RS(20,30) 8 -> 6 +6.7 %
     // (137 -> 125 VGPRs: 4 instead of 3 waves per SIMD)
     const int w = g_tune.dec_win;
-    if (a.k == 16) return rebuild_launch<16, 8, false>(a, w ? w : 4, s);
-    return rebuild_launch<20, 10, true>(a, w ? w : 6, s);
+    if (a.k == 16) return rebuild_launch<16, 8, false, 4>(a, w ? w : 4, s);
+    return rebuild_launch<20, 10, true, 6>(a, w ? w : 6, s);
 }
 
 }  // namespace fk

@@ -38,8 +38,8 @@ SHARD_LEN = PAYLOAD + 2          # + big-endian uint16 length trailer
 SHARD_STRIDE = 1216              # 16-byte aligned device slot per shard
 HBM_PEAK = 8.0e12                # MI355X HBM3E spec, bytes/s (MI355X_MICROARCH.md)
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of this bench (separate passes, tools/pmc_traffic.py,
-# gfx950 FETCH_SIZE x2 correction): HBM bytes per launch of each codec kernel, with the source
-# hash of the kernel's translation unit at profiling time (tools/gpu_round.sh refreshes it)
+# gfx950 FETCH_SIZE x2 correction): HBM bytes per launch of each codec kernel, with the hash of
+# the kernel's machine code at profiling time (tools/gpu_round.sh pmc refreshes it)
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
 
 
@@ -53,12 +53,14 @@ def encode_kernel_name(k, m):
 
 def committed_traffic(kernel_prefix, tu):
     """HBM bytes per launch of the kernel from the committed PMC profile, or None when there is
-    none or when the profile was taken from other kernel sources than the ones built now (its
-    recorded source hash differs: the number would describe a different kernel)."""
+    none or when the profile describes another kernel than the one built now: its recorded hash
+    of the kernel's machine code (or, for older profiles, of its translation unit's sources)
+    differs from the built library's."""
     sys.path.insert(0, os.path.join(ROOT, "0xfec_amd"))
     try:
         import _build
-        now = _build.source_hash(tu)
+        now_src = _build.source_hash(tu)
+        now_code = _build.kernel_code_hashes()
     finally:
         sys.path.pop(0)
     try:
@@ -68,10 +70,15 @@ def committed_traffic(kernel_prefix, tu):
         return None, {"source": None, "note": "no PMC profile committed"}
     for name, rec in prof.items():
         if kernel_prefix in name and rec.get("traffic_bytes"):
-            info = {"source": os.path.relpath(TRAFFIC_JSON, ROOT), "profile_source_hash": rec.get("source_hash"),
-                    "built_source_hash": now}
-            if rec.get("source_hash") != now:
-                info["note"] = "stale: the kernel's sources changed since this profile; traffic not reported"
+            info = {"source": os.path.relpath(TRAFFIC_JSON, ROOT), "kernel": name}
+            if rec.get("code_hash"):
+                info.update(profile_code_hash=rec["code_hash"], built_code_hash=now_code.get(name))
+                same = rec["code_hash"] == now_code.get(name)
+            else:
+                info.update(profile_source_hash=rec.get("source_hash"), built_source_hash=now_src)
+                same = rec.get("source_hash") == now_src
+            if not same:
+                info["note"] = "stale: the kernel changed since this profile; traffic not reported"
                 return None, info
             return rec["traffic_bytes"], info
     return None, {"source": os.path.relpath(TRAFFIC_JSON, ROOT), "note": "kernel not in the profile"}

@@ -320,6 +320,12 @@ private:
         void* h_desc = nullptr;     // pinned [maxBlocks][n] gather descriptors (fk::GatherDesc)
         void* d_desc = nullptr;
         uint64_t in_dev = 0;        // h_in as the device sees it
+        // the other pinned buffers as the device sees them (small sets are coded straight from and
+        // into pinned memory: no copy engine round trips, fewer calls per flush)
+        uint8_t* out_dev = nullptr;
+        uint32_t* masks_dev = nullptr;
+        int32_t* status_dev = nullptr;
+        const void* desc_dev = nullptr;
         bool gather = false;        // a block of the set is referenced: the device gathers the set
         std::vector<std::shared_ptr<PacketPool>> pools;   // pools the set's references point into
     };

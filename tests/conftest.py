@@ -27,6 +27,25 @@ def fec():
     return importlib.import_module("0xfec_amd")
 
 
+@pytest.fixture
+def tune(fec):
+    """tune(knob=value, ...): set process-wide kernel-selection knobs (Codec.set_tuning) for one
+    test; every knob set is restored afterwards."""
+    codec, saved = [], {}
+
+    def set_knobs(**kv):
+        if not codec:
+            codec.append(fec.Codec(0))
+        old = codec[0].set_tuning(**kv)
+        for k_, v in old.items():
+            saved.setdefault(k_, v)
+
+    yield set_knobs
+    if codec:
+        codec[0].set_tuning(**saved)
+        codec[0].close()
+
+
 @pytest.fixture(scope="session")
 def golden():
     import json

@@ -135,16 +135,20 @@ def test_submit_never_fails_on_a_full_queue(B, S, oracle):
     assert len(want) == nblocks * m and got == want
 
 
+# zc: the decoder's sets are coded straight from / into their pinned buffers (knob bat_zc) when
+# their input is at most this many bytes (1 << 30: every set; 0: the copy form)
+@pytest.mark.parametrize("zc", [0, 1 << 30])
 @pytest.mark.parametrize("scheme,k,m,max_blocks,lens,loss", [
     ("rs", 20, 10, 4, [1200], 0.15),
     ("rs", 8, 4, 3, [1, 17, 600, 1200, 1434], 0.25),
     ("rs", 2, 1, 64, [1200, 1434], 0.3),
     ("xor", 2, 1, 3, [1, 100, 1200, 1434], 0.3),
 ])
-def test_batched_recovery_equals_per_block_recovery(B, S, oracle, scheme, k, m, max_blocks, lens, loss):
+def test_batched_recovery_equals_per_block_recovery(B, S, oracle, tune, scheme, k, m, max_blocks, lens, loss, zc):
     """Receiver: the payloads HandleRepairFrame returns per block (manager.go:160-198) equal,
     in order, those the batched path delivers to the connection's RecoveredQueue, under random
     source and repair losses (some blocks unrecoverable, some complete before any repair)."""
+    tune(bat_zc=zc)
     rng = np.random.default_rng(k * 7 + max_blocks)
     sid = S.XOR_FEC_SCHEME if scheme == "xor" else S.REED_SOLOMON_FEC_SCHEME
     nconn, nblocks = 3, 9

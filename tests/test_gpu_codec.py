@@ -352,9 +352,11 @@ def test_rs_encode_kernel_variants_match_oracle(codec, oracle, torch, variant, k
 # rolling windows of 4 and 6 loads, 20 is 17 with the inputs split by 64-bit shifts, 21 is 17 with the
 # plan records sorted over 256-block windows (dec_psort 4; the rest over 64, the default), 22 is 17
 # with the records sorted per segment (dec_psort 0, the round-2 order); 23 and 24 are 17 and 22 with
-# the plan kernel's form 2 (dec_pv 2: conflict-free log(i ^ j) table copies, merged D / N sums)
+# the plan kernel's form 2 (dec_pv 2, the default: conflict-free log(i ^ j) table copies, merged D / N
+# sums; the rest run form 1), 25 is 23 with the padded rebuild slice (dec_lpad: the wave's two blocks'
+# PermTab rows 32 banks apart)
 @pytest.mark.parametrize("wave", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22,
-                                  23, 24])
+                                  23, 24, 25])
 @pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10)])
 # L = 1008 / 1017: shards of 63 / 64 chunks, the edge of the two-block wave slices (rolling window)
 @pytest.mark.parametrize("L", [513, 1008, 1017, 1202, 1436])
@@ -377,9 +379,10 @@ def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, 
                            dec_direct=1 if wave in (7, 13, 14, 15) else 0,
                            dec_direct_big=1 if wave in (13, 14, 15) else 0, dec_gate=1 if wave in (14, 15) else 0,
                            dec_gate_pm=1000 if wave == 15 else 10,
-                           dec_sorted=0 if wave == 8 else 1, dec_fixk={9: 1, 16: 3, 17: 4, 18: 4, 19: 4, 20: 4, 21: 4, 22: 4, 23: 4, 24: 4}.get(wave, 2),
+                           dec_sorted=0 if wave == 8 else 1, dec_fixk={9: 1, 16: 3, 17: 4, 18: 4, 19: 4, 20: 4, 21: 4, 22: 4, 23: 4, 24: 4, 25: 4}.get(wave, 2),
                            dec_win={18: 4, 19: 6}.get(wave, 0), dec_s64=1 if wave == 20 else 0,
-                           dec_psort={21: 4, 22: 0, 24: 0}.get(wave, 1), dec_pv=2 if wave in (23, 24) else 1,
+                           dec_psort={21: 4, 22: 0, 24: 0}.get(wave, 1), dec_pv=2 if wave in (23, 24, 25) else 1,
+                           dec_lpad=1 if wave == 25 else 0,
                            dec_tier={10: 1, 11: 2, 12: 4}.get(wave, 0))
     try:
         out = torch.full((B, m, S), 0xEE, dtype=torch.uint8, device="cuda")
@@ -429,9 +432,9 @@ def test_rs_plan_forms_match_oracle(codec, oracle, torch, pv, k, m):
 
 # The plan kernels of later sub-batches on a side stream beside the rebuild of earlier ones (knob
 # dec_povl): batches of several sub-batches with a ragged last one, out of place and in place.
-@pytest.mark.parametrize("povl,pv", [(2, 1), (4, 2), (8, 1), (3, 2)])
+@pytest.mark.parametrize("povl,pv,lpad", [(2, 1, 0), (4, 2, 0), (8, 1, 1), (3, 2, 1), (1, 2, 1)])
 @pytest.mark.parametrize("k,m", [(16, 8), (20, 10)])
-def test_rs_plan_overlap_matches_oracle(codec, oracle, torch, povl, pv, k, m):
+def test_rs_plan_overlap_matches_oracle(codec, oracle, torch, povl, pv, lpad, k, m):
     rng = np.random.default_rng(7 * k + povl + pv)
     n, B, L = k + m, 9000 + 37, 1202
     S = (L + 15) // 16 * 16
@@ -443,7 +446,7 @@ def test_rs_plan_overlap_matches_oracle(codec, oracle, torch, povl, pv, k, m):
     data_np[lost] = 0x77
     par = torch.from_numpy(np.ascontiguousarray(sh[:, k:])).cuda()
     dm = torch.from_numpy(masks.view(np.int32)).cuda()
-    old = codec.set_tuning(dec_povl=povl, dec_pv=pv, dec_direct=0)
+    old = codec.set_tuning(dec_povl=povl, dec_pv=pv, dec_lpad=lpad, dec_direct=0)
     try:
         data = torch.from_numpy(data_np).cuda()
         out = torch.full((B, m, S), 0xEE, dtype=torch.uint8, device="cuda")

@@ -152,13 +152,15 @@ def _bind_dec(lib):
     return lib
 
 
+@pytest.mark.parametrize("zc", [0, 1 << 30])   # knob bat_zc: the copy form, every set zero-copy
 @pytest.mark.parametrize("k,m", [(8, 4), (20, 10), (2, 1)])
-def test_decoder_submit_ref_matches_oracle(fec, oracle, k, m):
+def test_decoder_submit_ref_matches_oracle(fec, oracle, tune, k, m, zc):
     """fec_go_decoder_submit_ref: received sources and repairs in registered packet buffers are
     gathered by the device (sources framed with their trailer at `biggest`, repairs verbatim).
     Every polled payload must equal the oracle's recoverSymbolPayloads (reed_solomon.go:92-136)
     for the same block, with referenced, copied (outside the pool) and empty (missing) shards
     mixed, at unaligned offsets, over several batches of both staging sets."""
+    tune(bat_zc=zc)
     lib = _bind_dec(fec.lib)
     rng = np.random.default_rng(0xDEC + 31 * k + m)
     nblocks, maxb, n = 200, 32, k + m

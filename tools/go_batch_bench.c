@@ -25,6 +25,11 @@
 #include <unistd.h>
 
 #include "fec_go.h"
+#include "fec_hip.h"
+
+/* the library's internal tuning entry (not in the public headers; process-wide knobs) */
+int fec__set_tuning(fec_ctx *ctx, int key, int value);
+enum { kTuneBatZc = 43 };
 
 static double now(void) {
     struct timespec t;
@@ -213,6 +218,8 @@ static double pct(const double *s, int n, double p) {
  *           the time the run loop is held; then non-blocking polls until all N are back: the
  *           completion latency the recovered frames see.
  * Timed per burst over `reps` bursts; prints p50 / p99 / max in microseconds. */
+static int zc_bytes = 0;
+
 static int burst(int k, int m, int N, int reps, size_t len, int ref) {
     const int pool_blocks = N * 4 > 256 ? N * 4 : 256;   /* distinct blocks, reused round robin */
     const size_t maxb = (size_t)(N > 64 ? N : 64);
@@ -319,10 +326,11 @@ static int burst(int k, int m, int N, int reps, size_t len, int ref) {
         qsort(lat, (size_t)reps, sizeof(double), cmp_dbl);
         printf("{\"mode\": \"burst\", \"scheme\": \"RS(%d,%d)\", \"submit\": \"%s\", \"policy\": \"%s\", \"burst_blocks\": %d, "
                "\"bursts\": %d, \"run_loop_held_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f}, "
-               "\"recovered_after_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f}, \"held_us_per_block_p50\": %.2f}\n",
+               "\"recovered_after_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f}, \"held_us_per_block_p50\": %.2f, "
+               "\"zero_copy_set_bytes\": %d}\n",
                k, k + m, ref ? "ref" : "copy", policy ? "poll (wait=0), re-poll" : "block (wait=1)", N, reps,
                pct(held, reps, 0.5), pct(held, reps, 0.99), held[reps - 1], pct(lat, reps, 0.5), pct(lat, reps, 0.99),
-               lat[reps - 1], pct(held, reps, 0.5) / N);
+               lat[reps - 1], pct(held, reps, 0.5) / N, zc_bytes);
         fflush(stdout);
     }
     fec_go_encoder_free(e);
@@ -334,8 +342,17 @@ static int burst(int k, int m, int N, int reps, size_t len, int ref) {
 int main(int argc, char **argv) {
     if (argc >= 2 && !strcmp(argv[1], "burst")) {
         if (argc < 6) {
-            fprintf(stderr, "usage: %s burst k m N reps [len] [copy|ref]\n", argv[0]);
+            fprintf(stderr, "usage: %s burst k m N reps [len] [copy|ref] [zc=BYTES]\n", argv[0]);
             return 2;
+        }
+        if (argc > 8 && !strncmp(argv[8], "zc=", 3)) {   /* the decoder's zero-copy set size (knob bat_zc) */
+            fec_ctx *c = NULL;
+            zc_bytes = atoi(argv[8] + 3);
+            if (fec_ctx_create(0, &c) || fec__set_tuning(c, kTuneBatZc, zc_bytes) < 0) {
+                fprintf(stderr, "tuning: %s\n", fec_last_error());
+                return 1;
+            }
+            fec_ctx_destroy(c);
         }
         const int rc = burst(atoi(argv[2]), atoi(argv[3]), atoi(argv[4]), atoi(argv[5]),
                              argc > 6 ? (size_t)atoi(argv[6]) : 1200, argc > 7 && !strcmp(argv[7], "ref"));

@@ -72,7 +72,9 @@ for s in $STEPS; do
       for km in "8 4" "20 10"; do
         for n in 1 8 64; do
           for mode in copy ref; do
-            timeout -k 10 90 "$R/0xfec_amd/_bin/go_batch_bench" burst $km $n 400 1200 $mode
+            for zc in 0 4194304; do   # the decoder's zero-copy sets (knob bat_zc) off / up to 4 MiB
+              timeout -k 10 90 "$R/0xfec_amd/_bin/go_batch_bench" burst $km $n 400 1200 $mode zc=$zc
+            done
           done
         done
       done > "$O/go_burst.log" 2>&1

@@ -7,8 +7,9 @@ request of a wide coalesced streaming read, i.e. half the bytes; so read bytes =
 
 usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON
 
-Each kernel's record carries the source hash of its translation unit (0xfec_amd/_build.py
-source_hash), so bench.py can tell whether the profile still describes the kernel it runs.
+Each kernel's record carries the hash of its machine code in the library that was profiled
+(0xfec_amd/_build.py kernel_code_hashes) and the source hash of its translation unit, so bench.py
+can tell whether the profile still describes the kernel it runs.
 """
 import csv
 import glob
@@ -52,6 +53,7 @@ def main():
     import _build
     tu_of = {"rs_encode": "fec_encode.hip", "rs_recover": "fec_recover.hip", "rs_reconstruct": "fec_decode.hip",
              "rs_plan": "fec_plan.hip", "xor_": "fec_xor.hip"}
+    code = _build.kernel_code_hashes()
     res = {}
     for k in sorted(set(fetch) | set(write)):
         if not k.startswith("void fk::"):
@@ -68,6 +70,8 @@ def main():
         tu = next((v for pre, v in tu_of.items() if k.startswith("void fk::" + pre)), None)
         if tu:
             res[k]["source_hash"] = _build.source_hash(tu)
+        if k in code:
+            res[k]["code_hash"] = code[k]
     with open(dst, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))
