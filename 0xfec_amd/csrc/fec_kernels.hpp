@@ -206,10 +206,15 @@ struct Tuning {
                               // decode time, RS(16,24) -3 % (rebuild rows; a cheaper ranking); 256 / 512
                               // cost the plan kernel residency (its LDS) more than the rebuild gains (r03y)
     int dec_s64 = 0;          // fec_rebuild.hip: input splits by 64-bit shifts (two dwords a shift)
-    int bat_zc = 0;           // batch decoder (fec_batch.cpp): sets of at most this many input bytes are coded
-                              // straight from / into their pinned buffers (device-mapped), no copies
+    int bat_zc = 4 << 20;     // batch decoder (fec_batch.cpp): sets of at most this many input bytes are coded
+                              // straight from / into their pinned buffers (device-mapped), no copies. Receive
+                              // bursts (go_batch_bench burst, r04c), run loop held p50 by a non-blocking poll:
+                              // RS(8,12) 1 / 8 / 64 blocks 14.6 / 14.7 / 28.2 -> 4.1 / 5.5 / 20.3 us, RS(20,30)
+                              // 15.7 / 15.9 / 48.4 -> 5.0 / 7.8 / 40.1 us; data back 1.3-1.6x sooner
     int dec_lpad = 0;         // fec_rebuild.hip: the two blocks' PermTab rows of a wave slice 32 banks apart
-                              // (RS(16,24)'s unpadded rows share banks: 24 % LDS conflict cycles)
+                              // (RS(16,24)'s unpadded rows share banks: 24 % LDS conflict cycles). Measured
+                              // (r04c): RS(16,24) +0.1 %, RS(20,30) -1.2 %: the conflicts are not on the
+                              // critical path of a VALU-bound wave. Off.
     int dec_povl = 0;         // multi-erasure decode (sorted plans + fec_rebuild.hip): sub-batches per launch
                               // whose plan kernels run on a high-priority side stream beside the rebuild of
                               // the sub-batches before them (0 / 1: one plan launch, then one rebuild).
