@@ -177,10 +177,14 @@ Error BatchEncoder::init() {
         if ((h = hipHostMalloc(&s.h_desc, desc_bytes, hipHostMallocDefault)) != hipSuccess)
             return hip_error(h, "hipHostMalloc");
         if ((h = hipMalloc(&s.d_desc, desc_bytes)) != hipSuccess) return hip_error(h, "hipMalloc");
-        void* in_dev = nullptr;
-        if ((h = hipHostGetDevicePointer(&in_dev, s.h_in, 0)) != hipSuccess)
+        void *in_dev = nullptr, *out_dev = nullptr, *desc_dev = nullptr;
+        if ((h = hipHostGetDevicePointer(&in_dev, s.h_in, 0)) != hipSuccess ||
+            (h = hipHostGetDevicePointer(&out_dev, s.h_out, 0)) != hipSuccess ||
+            (h = hipHostGetDevicePointer(&desc_dev, s.h_desc, 0)) != hipSuccess)
             return hip_error(h, "hipHostGetDevicePointer");
         s.in_dev = (uint64_t)(uintptr_t)in_dev;
+        s.out_dev = static_cast<uint8_t*>(out_dev);
+        s.desc_dev = desc_dev;
         hipEvent_t ev;
         if ((h = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hip_error(h, "hipEventCreate");
         s.done = ev;
@@ -374,26 +378,37 @@ Error BatchEncoder::flushImpl(size_t* delivered) {
     hipStream_t st = (hipStream_t)fec_ctx_stream(ctx);
     const size_t B = s.blocks.size();
     hipError_t h;
+    // a small set is coded straight from and into its pinned buffers: one launch (two when
+    // gathered) and an event instead of a copy up, the launch, a copy down (knob bat_zc, as the
+    // decoder's sets)
+    const bool zc = B * (size_t)k_ * s.slot <= (size_t)std::max(0, fk::g_tune.bat_zc);
+    uint8_t* in = zc ? reinterpret_cast<uint8_t*>((uintptr_t)s.in_dev) : s.d_in;
+    uint8_t* out = zc ? s.out_dev : s.d_out;
     if (s.gather) {   // referenced payloads: the device pulls every shard of the batch itself
-        if ((h = hipMemcpyAsync(s.d_desc, s.h_desc, B * (size_t)k_ * sizeof(fk::GatherDesc), hipMemcpyHostToDevice,
-                                st)) != hipSuccess)
-            return hip_error(h, "hipMemcpyAsync H2D");
+        const void* desc = s.desc_dev;
+        if (!zc) {
+            if ((h = hipMemcpyAsync(s.d_desc, s.h_desc, B * (size_t)k_ * sizeof(fk::GatherDesc), hipMemcpyHostToDevice,
+                                    st)) != hipSuccess)
+                return hip_error(h, "hipMemcpyAsync H2D");
+            desc = s.d_desc;
+        }
         if ((h = hipSetDevice(engine_->device())) != hipSuccess) return hip_error(h, "hipSetDevice");
-        if ((h = fk::launch_gather_desc(static_cast<const fk::GatherDesc*>(s.d_desc), (uint32_t)(B * (size_t)k_), s.d_in,
+        if ((h = fk::launch_gather_desc(static_cast<const fk::GatherDesc*>(desc), (uint32_t)(B * (size_t)k_), s.d_in,
                                         s.slot, st)) != hipSuccess)
             return hip_error(h, "gather launch");
-    } else if ((h = hipMemcpyAsync(s.d_in, s.h_in, B * (size_t)k_ * s.slot, hipMemcpyHostToDevice, st)) != hipSuccess) {
+        in = s.d_in;
+    } else if (!zc &&
+               (h = hipMemcpyAsync(s.d_in, s.h_in, B * (size_t)k_ * s.slot, hipMemcpyHostToDevice, st)) != hipSuccess) {
         return hip_error(h, "hipMemcpyAsync H2D");
     }
     int rc;
     if (rs_)
-        rc = fec_rs_encode_batch(ctx, k_, m_, s.maxLen, B, s.d_in, (size_t)k_ * s.slot, s.d_out, (size_t)m_ * s.slot,
-                                 s.slot, FEC_DEVICE);
+        rc = fec_rs_encode_batch(ctx, k_, m_, s.maxLen, B, in, (size_t)k_ * s.slot, out, (size_t)m_ * s.slot, s.slot,
+                                 FEC_DEVICE);
     else
-        rc = fec_xor_encode_batch(ctx, k_, s.maxLen, B, s.d_in, (size_t)k_ * s.slot, s.d_out, s.slot, s.slot,
-                                  FEC_DEVICE);
+        rc = fec_xor_encode_batch(ctx, k_, s.maxLen, B, in, (size_t)k_ * s.slot, out, s.slot, s.slot, FEC_DEVICE);
     if (rc) return codec_rc(rc);
-    if ((h = hipMemcpyAsync(s.h_out, s.d_out, B * (size_t)m_ * s.slot, hipMemcpyDeviceToHost, st)) != hipSuccess)
+    if (!zc && (h = hipMemcpyAsync(s.h_out, s.d_out, B * (size_t)m_ * s.slot, hipMemcpyDeviceToHost, st)) != hipSuccess)
         return hip_error(h, "hipMemcpyAsync D2H");
     if ((h = hipEventRecord((hipEvent_t)s.done, st)) != hipSuccess) return hip_error(h, "hipEventRecord");
     s.inFlight = true;

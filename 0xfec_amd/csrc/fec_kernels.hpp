@@ -206,7 +206,7 @@ struct Tuning {
                               // decode time, RS(16,24) -3 % (rebuild rows; a cheaper ranking); 256 / 512
                               // cost the plan kernel residency (its LDS) more than the rebuild gains (r03y)
     int dec_s64 = 0;          // fec_rebuild.hip: input splits by 64-bit shifts (two dwords a shift)
-    int bat_zc = 4 << 20;     // batch decoder (fec_batch.cpp): sets of at most this many input bytes are coded
+    int bat_zc = 4 << 20;     // batch encoder / decoder (fec_batch.cpp): sets of at most this many input bytes are coded
                               // straight from / into their pinned buffers (device-mapped), no copies. Receive
                               // bursts (go_batch_bench burst, r04c), run loop held p50 by a non-blocking poll:
                               // RS(8,12) 1 / 8 / 64 blocks 14.6 / 14.7 / 28.2 -> 4.1 / 5.5 / 20.3 us, RS(20,30)
@@ -225,7 +225,8 @@ struct Tuning {
                               // table no half-wave meets on a bank; D_p and N_r in one merged pass; exp
                               // over [0, 768) so the coefficient sums need no reduction). Form 2: VALU
                               // per plan wave 4446 -> 3171 (RS(20,30)), plan 211 -> 153 us, decode
-                              // U{1..10} 2930 -> 2872 us (+2.0 %); RS(16,24) +0.2 % (r04b)
+                              // U{1..10} 2930 -> 2872 us (+2.0 %); RS(16,24) +0.2 % (r04b). 3: RS(16,24) and
+                              // RS(20,30) by a kernel compiled for the code (fec_plan.hip form 3), the rest 2
     int host_gather = 1;      // FEC_HOST_PINNED reconstruct: parity planes that few blocks read are pulled by
                               // the device straight from the caller's pinned buffer, the rest by 2D DMA (0:
                               // every plane by DMA; 2: every plane by the device)

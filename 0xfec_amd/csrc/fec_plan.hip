@@ -34,12 +34,12 @@ constexpr uint32_t kV2Exp = 0, kV2Log = 768, kV2Log32 = 1024, kV2Tables = 1152;
 constexpr uint32_t kRankBins = 33;   // erasure counts 0..32
 // recs: the records of `win` segments of `groups` blocks, sorted together (sort window)
 __host__ __device__ inline SortLds sort_lds(uint32_t m, uint32_t k, uint32_t groups, uint32_t stride,
-                                            uint32_t win = 1, bool v2 = false) {
+                                            uint32_t win = 1, bool v2 = false, uint32_t gscratch = kGroupScratch) {
     SortLds l;
     l.prows = v2 ? kV2Tables : 768;
     l.dall = l.prows + (size_t)m * k;
     l.scratch = (l.dall + 32 + 15) & ~(size_t)15;
-    l.pos = l.scratch + (size_t)groups * kGroupScratch;
+    l.pos = l.scratch + (size_t)groups * gscratch;
     // ranking scratch: per wave of records and bin, a count (then its prefix), and per bin a start
     l.rank = l.pos + (size_t)groups * win * 4;
     l.recs = (l.rank + ((size_t)(groups * win + 63) / 64 + 1) * kRankBins * 4 + 15) & ~(size_t)15;
@@ -56,6 +56,60 @@ __host__ __device__ inline uint32_t sort_window(uint32_t groups, int psort) {
     return groups < blocks ? blocks / groups : 1u;
 }
 
+// The window's nw record slots (first block base0) from LDS to their storage order in a.plans:
+// erasure count descending, then block order (stable). Workgroup-wide (barriers inside).
+__device__ __forceinline__ void sort_window_out(const PlanArgs& a, uint8_t* smem, const SortLds& L, uint32_t nw,
+                                                uint32_t base0) {
+    const PlanLayout lay = a.lay;
+    uint32_t* s_pos = reinterpret_cast<uint32_t*>(smem + L.pos);
+    __syncthreads();   // every record of the window written
+    const uint32_t nvalid = min(nw, a.nblocks - base0);
+    // counting sort: position = records with a larger count + earlier records with the same
+    // count (past-the-batch groups: nothing to rebuild, last indices, so they rank last).
+    // Per wave of records and bin, a ballot gives the count and each record's rank in its wave.
+    const uint32_t U = a.maxe + 1, nwv = (nw + 63) / 64;
+    uint32_t* wc = reinterpret_cast<uint32_t*>(smem + L.rank);   // [nwv][U], then start[U]
+    uint32_t* start = wc + nwv * U;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (uint32_t t = threadIdx.x; t < nwv * 64; t += kPlanSortThreads) {   // wave-uniform bound
+        const uint32_t v = t < nw ? smem[L.recs + (size_t)t * lay.stride + lay.nout_off] : kRankBins;
+        uint32_t rin = 0;
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint64_t bm = __ballot(v == u);
+            if (v == u) rin = (uint32_t)__popcll(bm & lt);
+            if (lane == 0) wc[(t >> 6) * U + u] = (uint32_t)__popcll(bm);
+        }
+        if (t < nw) s_pos[t] = rin;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // bins in descending order; within a bin, waves in order: wc becomes each wave's offset
+        uint32_t acc = 0;
+        for (uint32_t u = U; u-- > 0;) {
+            start[u] = acc;
+            for (uint32_t w = 0; w < nwv; ++w) {
+                const uint32_t c = wc[w * U + u];
+                wc[w * U + u] = acc;
+                acc += c;
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < nw; t += kPlanSortThreads) {
+        const uint32_t v = smem[L.recs + (size_t)t * lay.stride + lay.nout_off];
+        s_pos[t] += wc[(t >> 6) * U + v];
+    }
+    __syncthreads();
+    const uint32_t per = lay.stride / 16;
+    const uint4* src = reinterpret_cast<const uint4*>(smem + L.recs);
+    uint4* dst = reinterpret_cast<uint4*>(a.plans + (uint64_t)base0 * lay.stride);
+    for (uint32_t i = threadIdx.x; i < nvalid * per; i += kPlanSortThreads) {
+        const uint32_t r = i / per, q = i - r * per;
+        dst[(size_t)s_pos[r] * per + q] = src[i];
+    }
+}
+
 template <uint32_t LPB, bool V2>
 __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanArgs a, uint32_t segs, uint32_t win) {
     constexpr uint32_t G = kPlanSortThreads / LPB;   // blocks per workgroup segment
@@ -68,7 +122,6 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
     // form 2: this lane's copy of log(0..31)
     const uint8_t* s_l32 = smem + kV2Log32 + (threadIdx.x & 3u) * 32u;
     uint8_t* s_prows = smem + L.prows;
-    uint32_t* s_pos = reinterpret_cast<uint32_t*>(smem + L.pos);
     const uint32_t k = a.k, m = a.m, n = k + m;
     const uint32_t gb = threadIdx.x / LPB, gl = threadIdx.x % LPB;   // block group, lane in group
     // exp | log (768 bytes, contiguous in gf::kTables) as dwords (form 2: the layout above), then
@@ -220,60 +273,190 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
         // erasure count descending, then block order (stable)
         const bool last = sg + 1 == segs || base + G >= a.nblocks;
         if (wl + 1 < win && !last) continue;   // workgroup-uniform
-        __syncthreads();   // every record of the window written
-        const uint32_t nw = (wl + 1) * G;           // record slots of the window
-        const uint32_t base0 = base - wl * G;       // its first block
-        const uint32_t nvalid = min(nw, a.nblocks - base0);
-        // counting sort: position = records with a larger count + earlier records with the same
-        // count (past-the-batch groups: nothing to rebuild, last indices, so they rank last).
-        // Per wave of records and bin, a ballot gives the count and each record's rank in its wave.
-        const uint32_t U = a.maxe + 1, nwv = (nw + 63) / 64;
-        uint32_t* wc = reinterpret_cast<uint32_t*>(smem + L.rank);   // [nwv][U], then start[U]
-        uint32_t* start = wc + nwv * U;
-        const uint32_t lane = threadIdx.x & 63u;
-        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-        for (uint32_t t = threadIdx.x; t < nwv * 64; t += kPlanSortThreads) {   // wave-uniform bound
-            const uint32_t v = t < nw ? smem[L.recs + (size_t)t * lay.stride + lay.nout_off] : kRankBins;
-            uint32_t rin = 0;
-            for (uint32_t u = 0; u < U; ++u) {
-                const uint64_t bm = __ballot(v == u);
-                if (v == u) rin = (uint32_t)__popcll(bm & lt);
-                if (lane == 0) wc[(t >> 6) * U + u] = (uint32_t)__popcll(bm);
+        sort_window_out(a, smem, L, (wl + 1) * G, base - wl * G);
+    }
+}
+
+// Form 3 (knob dec_pv = 3): the same plans for one code known at compile time, K data and M parity
+// shards with M < K (the complement sums: RS(16,24), RS(20,30)), so every loop is unrolled and the
+// sums are built for the fewest instructions:
+//   * tables: exp over [0, 768), then 255 - log j for j < 32 in 4 copies (j = 0: 255, i.e. log 0 = 0),
+//     then log; lane l reads copy l & 3, and its table address t ^ y ^ (copy << 5) is one XOR of
+//     a shard index y with the lane's t ^ (copy << 5);
+//   * with nl(j) = 255 - log j the complement sum D = dall[t] + 255*32 - sum_y log(t ^ y) is
+//     dall[t] + sum_y nl(t ^ y) mod 255: no compare, no subtraction;
+//   * the others X, the erased O and the numerators N sit in dword scratch, read into registers
+//     by wide LDS loads, and coef = exp(N_r + nl(O_r ^ s_p) + (255 - D_p)) is one three-input add
+//     (the argument < 765: exp needs no reduction).
+constexpr uint32_t kV3Exp = 0, kV3NLog32 = 768, kV3Log = 896, kV3Tables = 1152;
+typedef const __attribute__((address_space(3))) uint8_t lds_cu8;
+// LDS address of a pointer into the kernel's LDS, and a byte load from one: lets the table
+// address be formed as one XOR (the compiler, given generic pointers, adds the LDS base per load)
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ uint32_t lds_ld8(uint32_t addr) { return *(lds_cu8*)(uintptr_t)addr; }
+static_assert(kV3Tables == kV2Tables, "forms 2 and 3 share sort_lds's table area");
+// group scratch: S bytes [0, 32), X dwords [32, 80), O dwords [80, 128), N dwords [128, 176), 255 - D_p
+// bytes [176, 208)
+constexpr uint32_t kV3S = 0, kV3X = 32, kV3O = 80, kV3N = 128, kV3D = 176, kGroupScratch3 = 208;
+
+template <uint32_t K, uint32_t M>
+__global__ __launch_bounds__(kPlanSortThreads) void rs_plan_code_kernel(PlanArgs a, uint32_t segs, uint32_t win) {
+    constexpr uint32_t N = K + M, LPB = K <= 16 ? 16u : 32u, G = kPlanSortThreads / LPB, MAXE = M;
+    static_assert(M < K && M <= 12 && K <= LPB && N <= 32, "complement-sum codes with the scratch above");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (a.gate && *a.gate != a.gate_want) return;   // the classify kernel picked the direct path
+    const PlanLayout lay = a.lay;
+    const SortLds L = sort_lds(M, K, G, lay.stride, win, true, kGroupScratch3);
+    const uint8_t* s_exp = smem + kV3Exp;
+    const uint8_t* s_log = smem + kV3Log;
+    const uint8_t* s_nl = smem + kV3NLog32;
+    const uint32_t copy5 = (threadIdx.x & 3u) << 5;
+    // nl(t ^ y) of the lane's copy at nlb ^ y, nlb = the table's LDS address + (t ^ copy << 5): one
+    // XOR per term, exact while the table starts on a 128-byte boundary (dynamic LDS starts at
+    // LDS address 0 in these kernels; anything else is reported, not computed wrong)
+    const uint32_t nl_base = lds_addr(s_nl);
+    if (nl_base & 127u) {
+        if (threadIdx.x == 0) atomicOr(a.err, 4);
+        return;
+    }
+    uint8_t* s_prows = smem + L.prows;
+    const uint32_t gb = threadIdx.x / LPB, gl = threadIdx.x % LPB;
+    for (uint32_t i = threadIdx.x; i < kV3Tables; i += kPlanSortThreads) {
+        const uint32_t j = (i - kV3NLog32) & 31u;
+        smem[i] = i < kV3NLog32 ? gf::kTables.exp[i % 255u]
+                : i < kV3Log ? (uint8_t)(j ? 255u - gf::kTables.log[j] : 255u)
+                : gf::kTables.log[i - kV3Log];
+    }
+    for (uint32_t i = threadIdx.x; i < M * K; i += kPlanSortThreads) s_prows[i] = a.prows[i];
+    uint8_t* s_dall = smem + L.dall;
+    if (threadIdx.x < N) s_dall[threadIdx.x] = a.dall[threadIdx.x];
+    uint8_t* grp = smem + L.scratch + gb * kGroupScratch3;
+    uint8_t* S = grp + kV3S;
+    uint32_t* Xd = reinterpret_cast<uint32_t*>(grp + kV3X);
+    uint32_t* Od = reinterpret_cast<uint32_t*>(grp + kV3O);
+    uint32_t* Nd = reinterpret_cast<uint32_t*>(grp + kV3N);
+    uint8_t* Dn = grp + kV3D;
+    constexpr uint32_t all = N >= 32 ? 0xFFFFFFFFu : (1u << N) - 1u, kmask = (1u << K) - 1u;
+    const uint32_t seg0 = blockIdx.x * segs;
+    uint32_t mask_next = seg0 * G + gb < a.nblocks ? a.masks[seg0 * G + gb] : 0u;
+    for (uint32_t sg = 0; sg < segs; ++sg) {
+        const uint32_t base = (seg0 + sg) * G;
+        if (base >= a.nblocks) break;   // workgroup-uniform
+        const uint32_t b = base + gb;
+        const bool valid = b < a.nblocks;
+        const uint32_t mask_in = mask_next;
+        const uint32_t bn = b + G;
+        mask_next = (sg + 1 < segs && bn < a.nblocks) ? a.masks[bn] : 0u;
+        const uint32_t wl = sg % win;
+        if (wl == 0) __syncthreads();
+        else wave_sync();
+        uint8_t* P = smem + L.recs + ((size_t)wl * G + gb) * lay.stride;
+        const uint32_t mask = valid ? mask_in & all : all;
+        const uint32_t e = K - __popc(mask & kmask);
+        int32_t st = a.max_out ? (int32_t)e : 0;
+        uint32_t nout = 0;
+        if (e != 0) {
+            if ((uint32_t)__popc(mask) < K) {
+                st = -4;   // FEC_ERR_TOO_FEW_SHARDS
+                if (gl == 0) atomicOr(a.err, 1);
+            } else if (a.max_out && e > a.max_out) {
+                st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
+                if (gl == 0) atomicOr(a.err, 2);
+            } else {
+                nout = e;
             }
-            if (t < nw) s_pos[t] = rin;
         }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            // bins in descending order; within a bin, waves in order: wc becomes each wave's offset
-            uint32_t acc = 0;
-            for (uint32_t u = U; u-- > 0;) {
-                start[u] = acc;
-                for (uint32_t w = 0; w < nwv; ++w) {
-                    const uint32_t c = wc[w * U + u];
-                    wc[w * U + u] = acc;
-                    acc += c;
+        if (gl == 0) {
+            P[lay.nout_off] = (uint8_t)nout;
+            *reinterpret_cast<uint32_t*>(P + lay.blk_off) = b;
+            if (valid && a.status) a.status[b] = st;
+        }
+        if (nout) {
+#pragma unroll
+            for (uint32_t t0 = 0; t0 < N; t0 += LPB) {
+                const uint32_t t = t0 + gl;
+                if (t < N) {
+                    const uint32_t below = mask & ((1u << t) - 1u);   // t < 32
+                    const uint32_t pos = __popc(below);
+                    if (((mask >> t) & 1u) && pos < K) {
+                        S[pos] = (uint8_t)t;
+                    } else {
+                        Xd[t - min(pos, K)] = t;   // not an input: erased, or present past the first K
+                        if (t < K && !((mask >> t) & 1u)) Od[t - pos] = t;   // erased data shards below t: t - pos
+                    }
                 }
             }
         }
-        __syncthreads();
-        for (uint32_t t = threadIdx.x; t < nw; t += kPlanSortThreads) {
-            const uint32_t v = smem[L.recs + (size_t)t * lay.stride + lay.nout_off];
-            s_pos[t] += wc[(t >> 6) * U + v];
+        wave_sync();
+        if (nout) {
+            if (gl < K) P[lay.in_off + gl] = S[gl];
+            if (gl < nout) P[lay.out_off + gl] = (uint8_t)Od[gl];
+            if (e == 1) {
+                // one erasure: x_E = inv(A[R0][E]) * (p_R0 ^ sum_j A[R0][j] x_j)
+                const uint32_t E0 = Od[0];
+                const uint32_t R0 = __ffs(mask >> K) - 1;
+                const uint8_t* row = s_prows + R0 * K;
+                const uint32_t inv = s_exp[255 - s_log[row[E0]]];
+                if (gl < K) {
+                    const uint32_t sj = S[gl];
+                    P[lay.coef_off + gl] = (uint8_t)(sj < K ? (row[sj] ? s_exp[s_log[inv] + s_log[row[sj]]] : 0u) : inv);
+                }
+            } else {
+                uint32_t x[M];
+#pragma unroll
+                for (uint32_t u = 0; u < M; ++u) x[u] = Xd[u];
+#pragma unroll
+                for (uint32_t q0 = 0; q0 < K + MAXE; q0 += LPB) {
+                    const uint32_t q = q0 + gl;
+                    if (q < K + e) {
+                        const uint32_t t = q < K ? (uint32_t)S[q] : Od[q - K];
+                        const uint32_t tb = nl_base + (t ^ copy5);
+                        uint32_t sum = s_dall[t];
+#pragma unroll
+                        for (uint32_t u = 0; u < M; ++u) sum += lds_ld8(tb ^ x[u]);
+                        sum %= 255u;
+                        if (q < K) Dn[q] = (uint8_t)(255u - sum);
+                        else Nd[q - K] = sum;
+                    }
+                }
+            }
         }
-        __syncthreads();
-        const uint32_t per = lay.stride / 16;
-        const uint4* src = reinterpret_cast<const uint4*>(smem + L.recs);
-        uint4* dst = reinterpret_cast<uint4*>(a.plans + (uint64_t)base0 * lay.stride);
-        for (uint32_t i = threadIdx.x; i < nvalid * per; i += kPlanSortThreads) {
-            const uint32_t r = i / per, q = i - r * per;
-            dst[(size_t)s_pos[r] * per + q] = src[i];
+        wave_sync();
+        if (nout >= 2 && gl < K) {
+            const uint32_t sb = nl_base + ((uint32_t)S[gl] ^ copy5), dn = Dn[gl];
+            const uint32_t exp_base = lds_addr(s_exp);
+            uint8_t* C = P + lay.coef_off + gl;
+#pragma unroll
+            for (uint32_t r = 0; r < MAXE; ++r)
+                if (r < nout) C[r * K] = (uint8_t)lds_ld8(exp_base + Nd[r] + lds_ld8(sb ^ Od[r]) + dn);
         }
+        const bool last = sg + 1 == segs || base + G >= a.nblocks;
+        if (wl + 1 < win && !last) continue;   // workgroup-uniform
+        sort_window_out(a, smem, L, (wl + 1) * G, base - wl * G);
     }
+}
+
+template <uint32_t K, uint32_t M>
+hipError_t code_launch(const PlanArgs& a, hipStream_t s) {
+    constexpr uint32_t LPB = K <= 16 ? 16u : 32u, G = kPlanSortThreads / LPB;
+    const uint32_t nseg = (a.nblocks + G - 1) / G;
+    if (nseg == 0) return hipSuccess;
+    uint32_t segs = g_tune.dec_pseg > 0 ? (uint32_t)g_tune.dec_pseg : std::max<uint32_t>(1, nseg / 4096);
+    if (a.gate) segs = 64;
+    segs = std::min<uint32_t>(segs, 64);
+    const uint32_t win = std::min<uint32_t>(sort_window(G, g_tune.dec_psort), 64);
+    if (win > 1) segs = (segs + win - 1) / win * win;
+    const uint32_t grid = (nseg + segs - 1) / segs;
+    const size_t lds = sort_lds(M, K, G, a.lay.stride, win, true, kGroupScratch3).total;
+    hipLaunchKernelGGL((rs_plan_code_kernel<K, M>), dim3(grid), dim3(kPlanSortThreads), lds, s, a, segs, win);
+    return hipGetLastError();
 }
 
 template <uint32_t LPB>
 hipError_t sorted_launch(const PlanArgs& a, hipStream_t s) {
-    const bool v2 = g_tune.dec_pv == 2;
+    const bool v2 = g_tune.dec_pv >= 2;   // form 3 covers two codes; the rest take form 2
     constexpr uint32_t G = kPlanSortThreads / LPB;
     const uint32_t nseg = (a.nblocks + G - 1) / G;
     if (nseg == 0) return hipSuccess;
@@ -297,6 +480,8 @@ hipError_t sorted_launch(const PlanArgs& a, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_rs_plan_sorted(const PlanArgs& a, hipStream_t s) {
+    if (g_tune.dec_pv == 3 && a.k == 16 && a.m == 8 && a.maxe == 8) return code_launch<16, 8>(a, s);
+    if (g_tune.dec_pv == 3 && a.k == 20 && a.m == 10 && a.maxe == 10) return code_launch<20, 10>(a, s);
     switch (plan_lanes(a.k)) {
         case 2: return sorted_launch<2>(a, s);
         case 4: return sorted_launch<4>(a, s);

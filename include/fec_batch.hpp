@@ -186,6 +186,8 @@ private:
         void* h_desc = nullptr;     // pinned [maxBlocks][k] gather descriptors (fk::GatherDesc)
         void* d_desc = nullptr;
         uint64_t in_dev = 0;        // device address of h_in (pinned, mapped)
+        uint8_t* out_dev = nullptr; // h_out and h_desc as the device sees them (small sets are coded
+        const void* desc_dev = nullptr;   // straight from and into pinned memory, knob bat_zc)
         void* done = nullptr;       // hipEvent_t
         std::vector<Pending> blocks;
         std::vector<std::shared_ptr<PacketPool>> pools;   // pools the batch's references point into

@@ -34,13 +34,15 @@ def _streams(rng, nconn, nblocks, k, lens):
     return out
 
 
+@pytest.mark.parametrize("zc", [0, 1 << 30])   # knob bat_zc: the copy form, every set zero-copy
 @pytest.mark.parametrize("scheme,k,m,max_blocks,lens", [
     ("rs", 20, 10, 4, [1200]),                       # the reference's RS factory code
     ("rs", 8, 4, 5, [1, 17, 600, 1200, 1434]),       # mixed lengths: slot-overflow flushes
     ("rs", 2, 1, 64, [1200, 1434]),
     ("xor", 2, 1, 3, [1, 100, 1200, 1434]),          # the reference's XOR factory code
 ])
-def test_batched_frames_equal_per_block_frames(B, S, oracle, scheme, k, m, max_blocks, lens):
+def test_batched_frames_equal_per_block_frames(B, S, oracle, tune, scheme, k, m, max_blocks, lens, zc):
+    tune(bat_zc=zc)
     rng = np.random.default_rng(k * 100 + max_blocks)
     sid = S.XOR_FEC_SCHEME if scheme == "xor" else S.REED_SOLOMON_FEC_SCHEME
     nconn, nblocks = 3, 7

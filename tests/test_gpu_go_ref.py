@@ -44,8 +44,10 @@ def _oracle_repairs(oracle, scheme, k, m, payloads):
     return [f[2] for f in frames]
 
 
+@pytest.mark.parametrize("zc", [0, 1 << 30])   # knob bat_zc: the copy form, every set zero-copy
 @pytest.mark.parametrize("scheme,k,m", [(RS, 8, 4), (RS, 20, 10), (RS, 2, 1), (XOR, 4, 1)])
-def test_submit_ref_matches_oracle(fec, oracle, scheme, k, m):
+def test_submit_ref_matches_oracle(fec, oracle, tune, scheme, k, m, zc):
+    tune(bat_zc=zc)
     lib = _bind(fec.lib)
     rng = np.random.default_rng(0x9A7 + 31 * k + m)
     nblocks, maxb = 300, 64          # several batches of both staging sets

@@ -77,6 +77,7 @@ def main():
         for ps in (0, 2, 4):
             variants["table-copy rebuild (fixk 4), plans sorted over %d blocks" % (64 * ps)] = dict(D, dec_fixk=4, dec_psort=ps)
         variants["plan form 1 (round 3)"] = dict(D, dec_pv=1)
+        variants["plan form 3 (compiled for the code)"] = dict(D, dec_pv=3)
         variants["padded rebuild slice (lpad)"] = dict(D, dec_lpad=1)
         variants["padded rebuild slice (lpad), wpc 3"] = dict(D, dec_lpad=1, dec_wpc=3)
         for ov in (2, 4, 8):

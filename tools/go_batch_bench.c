@@ -270,6 +270,45 @@ static int burst(int k, int m, int N, int reps, size_t len, int ref) {
         }
     }
     double *held = malloc((size_t)reps * sizeof(double)), *lat = malloc((size_t)reps * sizeof(double));
+    /* send side: N completed blocks submitted, then one non-blocking poll (the packer's
+     * PollRepairFrames, which launches the staged set): the hold; then polls until every block's
+     * repair frames are back */
+    uint64_t sid = (uint64_t)pool_blocks;
+    for (int r = -8; r < reps; ++r) {
+        const double t0 = now();
+        for (int j = 0; j < N; ++j) {
+            const int b = (int)(sid % (uint64_t)pool_blocks);
+            for (int i = 0; i < k; ++i) {
+                ptrs[i] = pay + ((size_t)b * k + i) * len;
+                lens[i] = len;
+            }
+            if (fec_go_encoder_submit(e, sid++, ptrs, lens, k)) return 1;
+        }
+        size_t done = 0, got = 0;
+        if (fec_go_encoder_poll(e, 0, ids, rl, rp, maxb, &got)) return 1;
+        done += got;
+        const double t_held = now() - t0;
+        while (done < (size_t)N) {
+            if (fec_go_encoder_poll(e, 0, ids, rl, rp, maxb, &got)) return 1;
+            done += got;
+        }
+        const double t_done = now() - t0;
+        const int b = (int)((sid - 1) % (uint64_t)pool_blocks);   /* the last block's frames */
+        for (int p = 0; got && p < m; ++p)
+            if (memcmp(rp + ((got - 1) * m + p) * FEC_GO_SLOT, reps_buf + ((size_t)b * m + p) * FEC_GO_SLOT, rl[got - 1])) {
+                fprintf(stderr, "send mismatch at burst %d\n", r);
+                return 1;
+            }
+        if (r >= 0) held[r] = t_held * 1e6, lat[r] = t_done * 1e6;
+    }
+    qsort(held, (size_t)reps, sizeof(double), cmp_dbl);
+    qsort(lat, (size_t)reps, sizeof(double), cmp_dbl);
+    printf("{\"mode\": \"burst\", \"side\": \"send\", \"scheme\": \"RS(%d,%d)\", \"submit\": \"copy\", \"policy\": "
+           "\"poll (wait=0), re-poll\", \"burst_blocks\": %d, \"bursts\": %d, \"run_loop_held_us\": {\"p50\": %.1f, "
+           "\"p99\": %.1f, \"max\": %.1f}, \"frames_after_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f}, "
+           "\"zero_copy_set_bytes\": %d}\n",
+           k, k + m, N, reps, pct(held, reps, 0.5), pct(held, reps, 0.99), held[reps - 1], pct(lat, reps, 0.5),
+           pct(lat, reps, 0.99), lat[reps - 1], zc_bytes);
     uint64_t next_id = 0;
     for (int policy = 0; policy < 2; ++policy) {
         for (int r = -8; r < reps; ++r) {   /* 8 untimed bursts first */
