@@ -332,6 +332,10 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_code_kernel(PlanArgs
     for (uint32_t i = threadIdx.x; i < M * K; i += kPlanSortThreads) s_prows[i] = a.prows[i];
     uint8_t* s_dall = smem + L.dall;
     if (threadIdx.x < N) s_dall[threadIdx.x] = a.dall[threadIdx.x];
+    // the group scratch starts zeroed: the coefficient rows below read O and N past a block's own
+    // erasure count (stale or zero shard indices and sums, always table-range values)
+    for (uint32_t i = threadIdx.x; i < G * kGroupScratch3 / 4; i += kPlanSortThreads)
+        reinterpret_cast<uint32_t*>(smem + L.scratch)[i] = 0u;
     uint8_t* grp = smem + L.scratch + gb * kGroupScratch3;
     uint8_t* S = grp + kV3S;
     uint32_t* Xd = reinterpret_cast<uint32_t*>(grp + kV3X);
@@ -424,13 +428,28 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_code_kernel(PlanArgs
             }
         }
         wave_sync();
-        if (nout >= 2 && gl < K) {
+        // coefficient rows in chunks of 4, each chunk computed whole (rows past a block's count read
+        // stale but in-range scratch, and are not stored) so its 12 LDS loads are in flight together;
+        // a chunk runs while some block of the wave needs it
+        uint32_t nw = nout;
+#pragma unroll
+        for (uint32_t o = LPB; o < 64; o <<= 1) nw = max(nw, (uint32_t)__shfl_xor((int)nw, (int)o));
+        nw = (uint32_t)__builtin_amdgcn_readfirstlane((int)nw);
+        if (nw >= 2 && gl < K) {
             const uint32_t sb = nl_base + ((uint32_t)S[gl] ^ copy5), dn = Dn[gl];
             const uint32_t exp_base = lds_addr(s_exp);
             uint8_t* C = P + lay.coef_off + gl;
 #pragma unroll
-            for (uint32_t r = 0; r < MAXE; ++r)
-                if (r < nout) C[r * K] = (uint8_t)lds_ld8(exp_base + Nd[r] + lds_ld8(sb ^ Od[r]) + dn);
+            for (uint32_t r0 = 0; r0 < MAXE; r0 += 4) {
+                if (r0 >= nw) break;   // wave-uniform
+                uint32_t c[4];
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                    if (r0 + j < MAXE) c[j] = lds_ld8(exp_base + Nd[r0 + j] + lds_ld8(sb ^ Od[r0 + j]) + dn);
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                    if (r0 + j < MAXE && r0 + j < nout && nout >= 2) C[(r0 + j) * K] = (uint8_t)c[j];
+            }
         }
         const bool last = sg + 1 == segs || base + G >= a.nblocks;
         if (wl + 1 < win && !last) continue;   // workgroup-uniform
