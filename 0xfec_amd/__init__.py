@@ -78,6 +78,7 @@ lib.fec_synth_data.argtypes = [_vp, _u64, _u64, _sz, _i, _sz, _vp, _sz, _sz]
 lib.fec_synth_single_erasures.argtypes = [_vp, _u64, _u64, _sz, _i, _i, _vp, _vp]
 lib.fec_probe_encode_traffic.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz]
 lib.fec_probe_recover_traffic.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _vp, _vp, _sz]
+lib.fec_probe_rebuild_traffic.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _vp, _vp, _sz]
 lib.fec_probe_link.argtypes = [_vp, _sz, _i, ctypes.POINTER(ctypes.c_double)]
 
 
@@ -306,6 +307,10 @@ class Codec:
     def probe_recover_traffic_raw(self, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss, masks, out, out_bs):
         return _check(lib.fec_probe_recover_traffic(self._h, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss,
                                                     masks, out, out_bs), "fec_probe_recover_traffic")
+
+    def probe_rebuild_traffic_raw(self, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss, masks, out, out_bs):
+        return _check(lib.fec_probe_rebuild_traffic(self._h, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss,
+                                                    masks, out, out_bs), "fec_probe_rebuild_traffic")
 
     def probe_link(self, nbytes=512 << 20, reps=3):
         """{h2d, d2h, duplex_each} GB/s of pinned hipMemcpyAsync on this ctx's device."""

@@ -9,6 +9,10 @@
 //   encode twin   rs_encode_fixed_kernel<K, M, ..> (fec_encode.hip): K shard loads, M stores
 //   recover twin  rs_recover_direct_kernel<K, ..> (fec_recover.hip) on single-erasure blocks:
 //                 the k-1 other data shards and the first present parity, one store to `out`
+//   rebuild twin  the multi-erasure decode (sorted plans + fec_rebuild.hip) of RS(16,24) / RS(20,30):
+//                 per block the first k present shards and one store per erased data shard, in
+//                 block order (the rebuild walks the same blocks in plan order within 64-block
+//                 windows), at the rebuild's residency; no plan kernel
 #include <string.h>
 
 #include <algorithm>
@@ -99,6 +103,38 @@ __global__ __launch_bounds__(kThreads) void probe_recover_kernel(RecoverProbeArg
     if (a.swz == 0x5A5A5A5Au) smem[0] = 1;   // never: keeps the LDS allocation
 }
 
+template <int K, int R>
+__global__ __launch_bounds__(kThreads) void probe_rebuild_kernel(RecoverProbeArgs a, uint32_t m) {
+    extern __shared__ uint8_t smem[];   // residency only, as the rebuild's table and wave slices
+    const uint32_t item = xcd_order(a.swz) * kThreads + threadIdx.x;
+    if (item >= a.total) return;
+    const uint32_t blk = fdiv(item, a.div_cps);
+    const uint32_t c = item - blk * a.cps;
+    const uint32_t mask = a.masks[blk] & low_mask(K + m);
+    const uint32_t e = K - __popc(mask & low_mask(K));
+    if (e == 0 || (uint32_t)__popc(mask) < K) return;   // nothing to rebuild / unrecoverable: nothing read
+    const uint8_t* d0 = a.data + (uint64_t)blk * a.dbs + (uint64_t)c * kChunk;
+    const uint8_t* p0 = a.parity + (uint64_t)blk * a.pbs + (uint64_t)c * kChunk;
+    uint32_t rest = mask;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {   // the first K present shards, in index order
+        const uint32_t s = __ffs(rest) - 1;
+        rest &= rest - 1;
+        const uint4 x = ld16<true>(s < (uint32_t)K ? d0 + (uint64_t)s * a.ss : p0 + (uint64_t)(s - K) * a.ss);
+        acc.x ^= x.x;
+        acc.y ^= x.y;
+        acc.z ^= x.z;
+        acc.w ^= x.w;
+    }
+    const uint32_t nb = min(a.len - c * kChunk, (uint32_t)kChunk);
+    uint8_t* o = a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if ((uint32_t)r < e) st16<true>(o + (uint64_t)r * a.ss, keep_bytes(acc, nb));
+    if (a.swz == 0x5A5A5A5Au) smem[0] = 1;   // never: keeps the LDS allocation
+}
+
 int stream_of(fec_ctx* ctx, hipStream_t* s) {
     if (!ctx) return FEC_ERR_INVALID_ARG;
     *s = (hipStream_t)fec_ctx_stream(ctx);
@@ -123,7 +159,8 @@ extern "C" int fec_probe_encode_traffic(fec_ctx* ctx, int k, int m, size_t shard
     hipStream_t s;
     int rc = stream_of(ctx, &s);
     if (rc) return rc;
-    if (!((k == 2 && m == 1) || (k == 8 && m == 4) || (k == 16 && m == 8))) return FEC_ERR_INVALID_ARG;
+    if (!((k == 2 && m == 1) || (k == 8 && m == 4) || (k == 16 && m == 8) || (k == 20 && m == 10)))
+        return FEC_ERR_INVALID_ARG;
     if (!layout_ok(data, dbs, ss, shard_len) || !layout_ok(parity, pbs, ss, shard_len) || shard_len == 0)
         return FEC_ERR_ALIGNMENT;
     const uint32_t cps = (uint32_t)((shard_len + kChunk - 1) / kChunk);
@@ -143,11 +180,15 @@ extern "C" int fec_probe_encode_traffic(fec_ctx* ctx, int k, int m, size_t shard
     a.div_cps = make_fastdiv(cps);
     a.swz = (uint32_t)g_tune.xcd_swz;
     const int grid = (int)((a.total + kThreads - 1) / kThreads);
-    // the fixed encode's residency: g_tune.enc_wpc workgroups per CU, RS(2,3) uncapped
-    const size_t lds = occupancy_lds(k == 2 ? 0 : g_tune.enc_wpc, (size_t)m * k * 32);
+    // the fixed encode's residency: g_tune.enc_wpc workgroups per CU, RS(2,3) uncapped; RS(16,24) and
+    // RS(20,30) as the bit-sliced encode, uncapped (g_tune.enc_bwpc; the bit-sliced kernel takes two
+    // chunks a lane, the twin one)
+    const size_t lds = k >= 16 ? occupancy_lds(g_tune.enc_bwpc, 0)
+                               : occupancy_lds(k == 2 ? 0 : g_tune.enc_wpc, (size_t)m * k * 32);
     if (k == 2) hipLaunchKernelGGL((probe_encode_kernel<2, 1>), dim3(grid), dim3(kThreads), lds, s, a);
     else if (k == 8) hipLaunchKernelGGL((probe_encode_kernel<8, 4>), dim3(grid), dim3(kThreads), lds, s, a);
-    else hipLaunchKernelGGL((probe_encode_kernel<16, 8>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (k == 16) hipLaunchKernelGGL((probe_encode_kernel<16, 8>), dim3(grid), dim3(kThreads), lds, s, a);
+    else hipLaunchKernelGGL((probe_encode_kernel<20, 10>), dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
 }
 
@@ -191,6 +232,45 @@ extern "C" int fec_probe_recover_traffic(fec_ctx* ctx, int k, int m, size_t shar
     else if (k == 8) hipLaunchKernelGGL((probe_recover_kernel<8>), dim3(grid), dim3(kThreads), lds, s, a, um);
     else if (k == 16) hipLaunchKernelGGL((probe_recover_kernel<16>), dim3(grid), dim3(kThreads), lds, s, a, um);
     else hipLaunchKernelGGL((probe_recover_kernel<20>), dim3(grid), dim3(kThreads), lds, s, a, um);
+    return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
+}
+
+extern "C" int fec_probe_rebuild_traffic(fec_ctx* ctx, int k, int m, size_t shard_len, size_t nblocks,
+                                         const void* data, size_t dbs, const void* parity, size_t pbs, size_t ss,
+                                         const uint32_t* masks, void* out, size_t out_bs) {
+    using namespace fk;
+    hipStream_t s;
+    int rc = stream_of(ctx, &s);
+    if (rc) return rc;
+    if (!((k == 16 && m == 8) || (k == 20 && m == 10))) return FEC_ERR_INVALID_ARG;
+    if (!masks || !layout_ok(data, dbs, ss, shard_len) || !layout_ok(parity, pbs, ss, shard_len) ||
+        !layout_ok(out, out_bs, 16, 0) || shard_len == 0 || out_bs < (size_t)m * ((shard_len + 15) & ~size_t(15)) ||
+        (ss | out_bs) >> 32)
+        return FEC_ERR_ALIGNMENT;
+    const uint32_t cps = (uint32_t)((shard_len + kChunk - 1) / kChunk);
+    if ((uint64_t)nblocks * cps >= (uint64_t(1) << 31)) return FEC_ERR_INVALID_ARG;
+    if (nblocks == 0) return FEC_OK;
+    RecoverProbeArgs a{};
+    a.data = (const uint8_t*)data;
+    a.parity = (const uint8_t*)parity;
+    a.out = (uint8_t*)out;
+    a.masks = masks;
+    a.dbs = dbs;
+    a.pbs = pbs;
+    a.ss = ss;
+    a.out_bs = out_bs;
+    a.len = (uint32_t)shard_len;
+    a.cps = cps;
+    a.total = (uint32_t)(nblocks * cps);
+    a.nblocks = (uint32_t)nblocks;
+    a.swz = (uint32_t)g_tune.dec_swz;
+    a.div_cps = make_fastdiv(cps);
+    const int grid = (int)((a.total + kThreads - 1) / kThreads);
+    // the rebuild's residency: its VGPRs allow 4 workgroups per CU (fec_rebuild.hip, uncapped)
+    const size_t lds = occupancy_lds(4, 0);
+    const uint32_t um = (uint32_t)m;
+    if (k == 16) hipLaunchKernelGGL((probe_rebuild_kernel<16, 8>), dim3(grid), dim3(kThreads), lds, s, a, um);
+    else hipLaunchKernelGGL((probe_rebuild_kernel<20, 10>), dim3(grid), dim3(kThreads), lds, s, a, um);
     return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
 }
 

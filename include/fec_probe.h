@@ -8,11 +8,16 @@
  *   fec_probe_encode_traffic    the bytes and launch shape of fec_rs_encode_batch's fixed-shape
  *                               kernel (k shard loads, m stores per 16-B chunk, XCD-contiguous
  *                               flat grid, its residency, non-temporal), RS(2,3), RS(8,12),
- *                               RS(16,24); parity receives the XOR of the inputs, not parity
+ *                               RS(16,24), RS(20,30); parity receives the XOR of the inputs, not
+ *                               parity
  *   fec_probe_recover_traffic   the bytes and launch shape of fec_rs_recover_batch's direct
  *                               single-erasure kernel: per block the k-1 other data shards and the
  *                               first present parity, one store to out; blocks whose mask is not
  *                               a single data erasure move nothing
+ *   fec_probe_rebuild_traffic   the bytes of the multi-erasure decode of RS(16,24) / RS(20,30)
+ *                               (sorted plans + rebuild): per block the first k present shards
+ *                               and one store per erased data shard into out (block b, row r at
+ *                               out + b*out_bs + r*ss), in block order, at the rebuild's residency
  *   fec_probe_link              the host link as the FEC_HOST paths drive it: hipMemcpyAsync of
  *                               `bytes` between pinned host and device buffers, H2D alone, D2H
  *                               alone and both at once on two streams (best of reps); GB/s into
@@ -35,6 +40,9 @@ extern "C" {
 int fec_probe_encode_traffic(fec_ctx *ctx, int k, int m, size_t shard_len, size_t nblocks, const void *data,
                              size_t dbs, void *parity, size_t pbs, size_t ss);
 int fec_probe_recover_traffic(fec_ctx *ctx, int k, int m, size_t shard_len, size_t nblocks, const void *data,
+                              size_t dbs, const void *parity, size_t pbs, size_t ss, const uint32_t *masks,
+                              void *out, size_t out_bs);
+int fec_probe_rebuild_traffic(fec_ctx *ctx, int k, int m, size_t shard_len, size_t nblocks, const void *data,
                               size_t dbs, const void *parity, size_t pbs, size_t ss, const uint32_t *masks,
                               void *out, size_t out_bs);
 int fec_probe_link(fec_ctx *ctx, size_t bytes, int reps, double *out);

@@ -72,7 +72,8 @@ def run_rs(torch, fec, codec, k, m, B, multi, iters, seed):
     masks = (((~lost).to(torch.int64) * weights).sum(dim=1)).to(torch.int32)
     e_d = lost[:, :k].sum(dim=1)
     slots = int(e_d.max().item())
-    out = torch.zeros((B, max(slots, 1), S), dtype=torch.uint8, device="cuda")
+    # multi-erasure configs: m output rows per block, as the rebuild traffic twin writes
+    out = torch.zeros((B, m if multi else max(slots, 1), S), dtype=torch.uint8, device="cuda")
     status = torch.zeros((B,), dtype=torch.int32, device="cuda")
 
     # raw C-ABI calls with the arguments precomputed: the shapes whose launches take tens of
@@ -107,6 +108,22 @@ def run_rs(torch, fec, codec, k, m, B, multi, iters, seed):
     t_dec = timed(torch, dec, iters)
     enc_bytes = B * n * L
     dec_bytes = int(((k + e_d) * (e_d > 0)).sum().item()) * L
+    # traffic twins (include/fec_probe.h): the kernels' bytes and launch shape without the field
+    # arithmetic, timed after the kernels (they overwrite parity and out): this box's ceiling
+    probe = {}
+    if (k, m) in ((2, 1), (8, 4), (16, 8), (20, 10)):
+        def enc_twin():
+            codec.probe_encode_traffic_raw(k, m, L, B, dp, k * S, pp, m * S, S)
+        probe["encode_probe_TB/s"] = round(enc_bytes / timed(torch, enc_twin, iters) / 1e9, 3)
+        probe["encode_frac_of_probe"] = round(enc_bytes / t_enc / 1e9 / probe["encode_probe_TB/s"], 4)
+        if multi and (k, m) in ((16, 8), (20, 10)):
+            def dec_twin():
+                codec.probe_rebuild_traffic_raw(k, m, L, B, dp, k * S, pp, m * S, S, mp, op, slots_ * S)
+        else:
+            def dec_twin():
+                codec.probe_recover_traffic_raw(k, m, L, B, dp, k * S, pp, m * S, S, mp, op, slots_ * S)
+        probe["decode_probe_TB/s"] = round(dec_bytes / timed(torch, dec_twin, iters) / 1e9, 3)
+        probe["decode_frac_of_probe"] = round(dec_bytes / t_dec / 1e9 / probe["decode_probe_TB/s"], 4)
     return {"config": "RS(%d,%d)" % (k, n), "blocks": B,
             "erasures": ("U{1..%d} of %d shards" % (multi, n)) if multi else "1 data shard",
             "mean_data_erasures": round(float(e_d.float().mean().item()), 3),
@@ -114,7 +131,7 @@ def run_rs(torch, fec, codec, k, m, B, multi, iters, seed):
             "encode_TB/s": round(enc_bytes / t_enc / 1e9, 3), "decode_TB/s": round(dec_bytes / t_dec / 1e9, 3),
             "payload_GiB/s": round(B * k * PAYLOAD / 2**30 / ((t_enc + t_dec) / 1e3), 1),
             "step_frac": round((enc_bytes + dec_bytes) / ((t_enc + t_dec) / 1e3) / 8e12, 4),
-            "check": ok}
+            "check": ok, **probe}
 
 
 def run_xor(torch, fec, codec, k, B, iters, seed):
