@@ -221,12 +221,14 @@ struct Tuning {
                               // Measured slower (r04b: RS(20,30) 2 / 4 / 8 sub-batches -0.8 / -1.9 / -3.5 %,
                               // RS(16,24) -0.9 / -2.0 / -4.3 %): the rebuild is VALU-bound, so a plan beside
                               // it takes issue slots, and each sub-batch adds a launch tail. Off.
-    int dec_pv = 2;           // sorted plan kernel form: 1, or 2 (log(i ^ j) of shard indices from a 4-copy
+    int dec_pv = 3;           // sorted plan kernel form: 1, or 2 (log(i ^ j) of shard indices from a 4-copy
                               // table no half-wave meets on a bank; D_p and N_r in one merged pass; exp
                               // over [0, 768) so the coefficient sums need no reduction). Form 2: VALU
                               // per plan wave 4446 -> 3171 (RS(20,30)), plan 211 -> 153 us, decode
                               // U{1..10} 2930 -> 2872 us (+2.0 %); RS(16,24) +0.2 % (r04b). 3: RS(16,24) and
-                              // RS(20,30) by a kernel compiled for the code (fec_plan.hip form 3), the rest 2
+                              // RS(20,30) by a kernel compiled for the code (fec_plan.hip form 3), the rest 2.
+                              // Form 3 over form 2 (r04d, r04e): VALU per plan wave 3171 -> 2064 (RS(20,30)),
+                              // 2176 -> 1380 (RS(16,24)); decode +0.8-0.9 % on both
     int host_gather = 1;      // FEC_HOST_PINNED reconstruct: parity planes that few blocks read are pulled by
                               // the device straight from the caller's pinned buffer, the rest by 2D DMA (0:
                               // every plane by DMA; 2: every plane by the device)

@@ -2,7 +2,8 @@
 reads all k data shards of every block and writes all m output shards (output r = XOR of inputs
 j with j % m == r, bytes past the shard length zero), the recover twin reads exactly the k-1
 other data shards and the first present parity of each single-erasure block and writes their XOR
-to the block's output slot (other blocks untouched). Checked against numpy on the same bytes, so
+to the block's output slot (other blocks untouched), and the rebuild twin reads the first k present
+shards of each block and writes their XOR into one output row per erased data shard. Checked against numpy on the same bytes, so
 a twin that skipped or re-read shards would show up here before it skewed a bench line."""
 import numpy as np
 import pytest
@@ -19,7 +20,7 @@ def torch():
     return t
 
 
-@pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8)])
+@pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10)])
 def test_encode_twin_reads_and_writes_every_shard(fec, torch, k, m):
     codec = fec.Codec(0)
     B = 777
@@ -74,4 +75,41 @@ def test_recover_twin_reads_the_decode_inputs(fec, torch, k, m):
                 w ^= dh[b, j]
         w[L:] = 0
         assert np.array_equal(got[b], w), b
+    codec.close()
+
+
+@pytest.mark.parametrize("k,m", [(16, 8), (20, 10)])
+def test_rebuild_twin_reads_the_first_k_present(fec, torch, k, m):
+    codec = fec.Codec(0)
+    B = 613
+    n = k + m
+    rng = np.random.default_rng(300 + k)
+    dh = rng.integers(0, 256, (B, k, S), dtype=np.uint8)
+    ph = rng.integers(0, 256, (B, m, S), dtype=np.uint8)
+    masks = np.empty(B, dtype=np.uint32)
+    for b in range(B):
+        lost = rng.choice(n, size=int(rng.integers(0, m + 1)), replace=False)
+        masks[b] = ((1 << n) - 1) & ~int(sum(1 << int(i) for i in lost))
+    masks[5] = ((1 << n) - 1) & ~((1 << (m + 1)) - 1)   # m + 1 losses: unrecoverable, nothing moved
+    data, par = torch.from_numpy(dh).cuda(), torch.from_numpy(ph).cuda()
+    dm = torch.from_numpy(masks.view(np.int32)).cuda()
+    out = torch.full((B, m, S), 0xCD, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    codec.probe_rebuild_traffic_raw(k, m, L, B, data.data_ptr(), k * S, par.data_ptr(), m * S, S, dm.data_ptr(),
+                                    out.data_ptr(), m * S)
+    codec.sync()
+    got = out.cpu().numpy()
+    for b in range(B):
+        mk = int(masks[b])
+        present = [i for i in range(n) if mk >> i & 1]
+        e = sum(1 for i in range(k) if not mk >> i & 1)
+        if e == 0 or len(present) < k:
+            assert (got[b] == 0xCD).all(), b
+            continue
+        w = np.zeros(S, dtype=np.uint8)
+        for i in present[:k]:
+            w ^= dh[b, i] if i < k else ph[b, i - k]
+        w[L:] = 0
+        for r in range(m):
+            assert np.array_equal(got[b, r], w) if r < e else (got[b, r] == 0xCD).all(), (b, r)
     codec.close()
