@@ -1302,7 +1302,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 38 ? &fk::g_tune.dec_s64
               : key == 39 ? &fk::g_tune.dec_psort : key == 40 ? &fk::g_tune.dec_pv
               : key == 41 ? &fk::g_tune.dec_povl : key == 42 ? &fk::g_tune.dec_lpad
-              : key == 43 ? &fk::g_tune.bat_zc : nullptr;
+              : key == 43 ? &fk::g_tune.bat_zc
+              : key == 44 ? &fk::g_tune.enc_early : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

@@ -216,16 +216,41 @@ __device__ __forceinline__ const gf::PermTab* stage_tabs(uint8_t* smem, const ui
     return reinterpret_cast<const gf::PermTab*>(smem);
 }
 
-// Flat launch: one item per lane, XCD-contiguous workgroup order.
+// Flat launch: one item per lane, XCD-contiguous workgroup order. POL bit 4 (knob enc_early): the
+// table words' loads go out first, then the item's K shard loads, and the tables reach LDS behind an
+// LDS-only barrier, so the shard loads are in flight while the tables stage (without it the
+// workgroup's __syncthreads waits for the table loads before any shard load is issued: one memory
+// round trip per workgroup, which a 40-us RS(2,3) launch of ~20 000 workgroups feels).
 template <int K, int M, int POL>
 __global__ __launch_bounds__(kThreads) void rs_encode_fixed_kernel(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const FixedEncode<K, M, POL> f{a, stage_tabs<K, M>(smem, a.tabs)};
     const uint32_t it = xcd_order(a.swz) * kThreads + threadIdx.x;
-    if (it >= a.total) return;
-    uint4 x[K];
-    f.load(x, it);
-    f.compute_store(x, it);
+    if constexpr ((POL & 16) != 0) {
+        constexpr uint32_t W = M * K * 8, R = (W + kThreads - 1) / kThreads;   // table dwords, per lane
+        uint32_t tw[R];
+#pragma unroll
+        for (uint32_t q = 0; q < R; ++q) {
+            const uint32_t i = threadIdx.x + q * kThreads;
+            tw[q] = i < W ? a.tabs[i] : 0u;
+        }
+        const FixedEncode<K, M, POL> f{a, reinterpret_cast<const gf::PermTab*>(smem)};
+        uint4 x[K];
+        if (it < a.total) f.load(x, it);
+#pragma unroll
+        for (uint32_t q = 0; q < R; ++q) {
+            const uint32_t i = threadIdx.x + q * kThreads;
+            if (i < W) reinterpret_cast<uint32_t*>(smem)[i] = tw[q];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (it >= a.total) return;
+        f.compute_store(x, it);
+    } else {
+        const FixedEncode<K, M, POL> f{a, stage_tabs<K, M>(smem, a.tabs)};
+        if (it >= a.total) return;
+        uint4 x[K];
+        f.load(x, it);
+        f.compute_store(x, it);
+    }
 }
 
 // Persistent ticket-queue launch (the default for the fixed shapes). The items are split into
@@ -526,12 +551,16 @@ static hipError_t enc_fixed_dispatch(const EncodeArgs& a, int grid, size_t lds, 
     } else if (g_tune.enc_dyadic && a.dytabs && K >= 4) {
         EncodeArgs d = a;
         d.tabs = a.dytabs;
-        if (g_tune.enc_nt & 1)
+        if (g_tune.enc_early && (g_tune.enc_nt & 1))
+            hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 27>), dim3(grid), dim3(kThreads), lds, s, d);
+        else if (g_tune.enc_nt & 1)
             hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 11>), dim3(grid), dim3(kThreads), lds, s, d);
         else
             hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 10>), dim3(grid), dim3(kThreads), lds, s, d);
     } else {
-        if (g_tune.enc_nt & 1)
+        if (g_tune.enc_early && (g_tune.enc_nt & 1))
+            hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 19>), dim3(grid), dim3(kThreads), lds, s, a);
+        else if (g_tune.enc_nt & 1)
             hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 3>), dim3(grid), dim3(kThreads), lds, s, a);
         else
             hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 2>), dim3(grid), dim3(kThreads), lds, s, a);

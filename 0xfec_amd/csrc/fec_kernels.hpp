@@ -147,6 +147,8 @@ struct XorArgs {
 // the internal fec__set_tuning() entry point; results in DESIGN.md).
 struct Tuning {
     int enc_nt = 3;           // encode/XOR cache policy: 0 plain, nonzero non-temporal loads and stores
+    int enc_early = 0;        // fixed-shape flat encode: shard loads issued before the table staging, LDS-only
+                              // barrier (fec_encode.hip rs_encode_fixed_kernel POL bit 4)
     int dec_nt = 3;           // reconstruct cache policy, same values
     int grid_mult = 1;        // persistent grids: workgroups = grid_mult * CUs * resident/CU
     int dec_max_rounds = 8;   // bound on item rounds per decode tile (pick_tile_blocks)

@@ -293,6 +293,9 @@ ENC_VARIANTS = {
     "generic": dict(enc_fixed=0),
     "fixed_flat": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=1),
     "fixed_flat_matrix": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=0),
+    # shard loads issued before the table staging (knob enc_early), dyadic and matrix bodies
+    "fixed_flat_early": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=1, enc_bits=0, enc_early=1),
+    "fixed_flat_matrix_early": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=0, enc_bits=0, enc_early=1),
     "queue_d0": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=0),
     "queue_d0_nodrain": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=-1),
     "queue_d1": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=1),

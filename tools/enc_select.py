@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Diagnostics: pick the fixed-shape encode form by interleaved A/B in one process (matrix vs
 dyadic split-recursive body, flat grid at several residencies, ticket queue), many rounds.
-usage: enc_select.py [k,m]   (8,4 default; 2^23 / k blocks)"""
+usage: enc_select.py [k,m] [blocks] [only]   (8,4 default; 2^23 / k blocks; only: comma-separated
+       substrings of the variant names to keep)"""
 import importlib
 import json
 import os
@@ -14,7 +15,8 @@ def main():
     import torch
     fec = importlib.import_module("0xfec_amd")
     k, m = (int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "8,4").split(","))
-    B, L, S = (1 << 23) // k, 1202, 1216
+    B, L, S = (int(sys.argv[2]) if len(sys.argv) > 2 and int(sys.argv[2]) else (1 << 23) // k), 1202, 1216
+    only = [x for x in (sys.argv[3] if len(sys.argv) > 3 else "").split(",") if x]
     codec = fec.Codec(0).use_torch_stream()
     data = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device="cuda")
     par = torch.zeros((B, m, S), dtype=torch.uint8, device="cuda")
@@ -27,14 +29,19 @@ def main():
     for w in (3, 4):
         variants["dyadic flat wpc%d, plain loads" % w] = dict(enc_queue=0, enc_wpc=w, enc_dyadic=1, enc_nt=2)
     variants["matrix flat wpc3, plain loads"] = dict(enc_queue=0, enc_wpc=3, enc_dyadic=0, enc_nt=2)
+    for w in (0, 3):   # shard loads before the table staging (knob enc_early)
+        variants["dyadic flat wpc%d early" % w] = dict(enc_queue=0, enc_wpc=w, enc_dyadic=1, enc_early=1)
+        variants["matrix flat wpc%d early" % w] = dict(enc_queue=0, enc_wpc=w, enc_dyadic=0, enc_early=1)
     for w in (0, 2, 3):
         variants["bits wpc%d" % w] = dict(enc_queue=0, enc_bits=11, enc_bwpc=w)
         variants["bits stream wpc%d" % w] = dict(enc_queue=0, enc_bits=15, enc_bwpc=w)
     variants["bits wpc0, plain loads"] = dict(enc_queue=0, enc_bits=11, enc_bwpc=0, enc_nt=2)
     if k == 8:
         variants["matrix queue d0 wpc2"] = dict(enc_queue=1, enc_qwpc=2, enc_qdepth=0, enc_dyadic=0)
+    if only:
+        variants = {n: kv for n, kv in variants.items() if any(x in n for x in only)}
     base = codec.set_tuning(enc_queue=0, enc_wpc=3, enc_qwpc=2, enc_qdepth=0, enc_dyadic=1, enc_nt=3, enc_bits=0,
-                            enc_bwpc=0)
+                            enc_bwpc=0, enc_early=0)
     ref = None
     for n, kv in variants.items():   # every form writes the same parity bytes
         codec.set_tuning(**kv)
@@ -47,7 +54,7 @@ def main():
         codec.set_tuning(**base)
     del ref
 
-    def t(iters=5):
+    def t(iters=5 if B * k > (1 << 22) else 100):
         codec.rs_encode_raw(k, m, L, B, dp, k * S, pp, m * S, S, fec.FEC_DEVICE)
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

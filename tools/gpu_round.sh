@@ -18,6 +18,7 @@
 #   counters    SQ / TCC / LDS counter passes of the configs furthest from the roofline
 #   counters:KNOB=V,..  the same passes of RS(16,24) / RS(20,30) with tuning knobs set
 #   ab:K:M:MULTI:ONLY   tools/dec_select.py interleaved A/B (ONLY: comma list, '_' for spaces)
+#   enc:K,M:BLOCKS:ONLY tools/enc_select.py interleaved encode A/B (BLOCKS 0: 2^23 / k)
 #   torchrun1   bench.py under torchrun with one rank (the RCCL branch on one device)
 #   rehearse2   bench.py --gpus 2 --rehearse-one-gpu (the N-rank code path, gloo, one device)
 #   duplex      tools/pcie_duplex_probe (host link per direction and both at once)
@@ -84,6 +85,10 @@ for s in $STEPS; do
     counters:*)
       TUNE=${s#counters:}
       tools/pmc_configs.sh "$TAG/counters_${TUNE//[=,]/_}" "rs1624,rs2030m" --tune "$TUNE" ;;
+    enc:*)
+      IFS=: read -r _ KM BLK ONLY <<< "$s"
+      timeout -k 10 200 python -u tools/enc_select.py "$KM" "$BLK" "$ONLY" > "$O/enc_${KM/,/_}_$BLK.log" 2>&1
+      tail -30 "$O/enc_${KM/,/_}_$BLK.log" ;;
     ab:*)
       IFS=: read -r _ K M MULTI ONLY <<< "$s"
       timeout -k 10 200 python -u tools/dec_select.py --k "$K" --m "$M" --blocks 524288 --multi "$MULTI" --rounds 7 \

@@ -25,7 +25,7 @@ cp_if "$S/pcie_duplex_probe.log" "$D/pcie_duplex_probe_$TAG.log"
 cp_if "$S/zerocopy_probe.log" "$D/zerocopy_probe_$TAG.log"
 cp_if "$S/pytest_variants.log" "$D/pytest_variants_$TAG.log"
 cp_if "$S/bench_torchrun_n1_rccl.log" "$D/bench_torchrun_n1_rccl_$TAG.log"
-for f in "$S"/ab_*.log; do cp_if "$f" "$D/$(basename "$f" .log)_$TAG.log"; done
+for f in "$S"/ab_*.log "$S"/enc_*.log; do cp_if "$f" "$D/$(basename "$f" .log)_$TAG.log"; done
 for d in "$S"/counters_*/; do cp_if "$d/counters.json" "$D/$(basename "$d")_$TAG.json"; done
 if [ -f "$S/pmc_traffic.json" ]; then cp "$S/pmc_traffic.json" profiles/pmc_traffic_latest.json; fi
 ls "$D" | grep "$TAG"
