@@ -87,7 +87,7 @@ for s in $STEPS; do
       tools/pmc_configs.sh "$TAG/counters_${TUNE//[=,]/_}" "rs1624,rs2030m" --tune "$TUNE" ;;
     enc:*)
       IFS=: read -r _ KM BLK ONLY <<< "$s"
-      timeout -k 10 200 python -u tools/enc_select.py "$KM" "$BLK" "$ONLY" > "$O/enc_${KM/,/_}_$BLK.log" 2>&1
+      timeout -k 10 200 python -u tools/enc_select.py "$KM" "$BLK" "${ONLY//_/ }" > "$O/enc_${KM/,/_}_$BLK.log" 2>&1
       tail -30 "$O/enc_${KM/,/_}_$BLK.log" ;;
     ab:*)
       IFS=: read -r _ K M MULTI ONLY <<< "$s"
