@@ -551,14 +551,14 @@ static hipError_t enc_fixed_dispatch(const EncodeArgs& a, int grid, size_t lds, 
     } else if (g_tune.enc_dyadic && a.dytabs && K >= 4) {
         EncodeArgs d = a;
         d.tabs = a.dytabs;
-        if (g_tune.enc_early && (g_tune.enc_nt & 1))
+        if ((g_tune.enc_early == 1 || (g_tune.enc_early == 2 && K == 2)) && (g_tune.enc_nt & 1))
             hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 27>), dim3(grid), dim3(kThreads), lds, s, d);
         else if (g_tune.enc_nt & 1)
             hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 11>), dim3(grid), dim3(kThreads), lds, s, d);
         else
             hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 10>), dim3(grid), dim3(kThreads), lds, s, d);
     } else {
-        if (g_tune.enc_early && (g_tune.enc_nt & 1))
+        if ((g_tune.enc_early == 1 || (g_tune.enc_early == 2 && K == 2)) && (g_tune.enc_nt & 1))
             hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 19>), dim3(grid), dim3(kThreads), lds, s, a);
         else if (g_tune.enc_nt & 1)
             hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 3>), dim3(grid), dim3(kThreads), lds, s, a);

@@ -147,8 +147,10 @@ struct XorArgs {
 // the internal fec__set_tuning() entry point; results in DESIGN.md).
 struct Tuning {
     int enc_nt = 3;           // encode/XOR cache policy: 0 plain, nonzero non-temporal loads and stores
-    int enc_early = 0;        // fixed-shape flat encode: shard loads issued before the table staging, LDS-only
-                              // barrier (fec_encode.hip rs_encode_fixed_kernel POL bit 4)
+    int enc_early = 2;        // fixed-shape flat encode: shard loads issued before the table staging, LDS-only
+                              // barrier (fec_encode.hip rs_encode_fixed_kernel POL bit 4); 1: every shape, 2:
+                              // RS(2,3) only. enc_select r04g: RS(2,3) (65 536 blocks, 40-us launches) +1.7 %,
+                              // RS(8,12) +0.03 %, RS(16,24) dyadic -2.9 % (four table dwords held per lane)
     int dec_nt = 3;           // reconstruct cache policy, same values
     int grid_mult = 1;        // persistent grids: workgroups = grid_mult * CUs * resident/CU
     int dec_max_rounds = 8;   // bound on item rounds per decode tile (pick_tile_blocks)
