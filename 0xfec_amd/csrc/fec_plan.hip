@@ -305,7 +305,7 @@ template <uint32_t K, uint32_t M>
 __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_code_kernel(PlanArgs a, uint32_t segs, uint32_t win) {
     constexpr uint32_t N = K + M, LPB = K <= 16 ? 16u : 32u, G = kPlanSortThreads / LPB, MAXE = M;
     static_assert(M < K && M <= 12 && K <= LPB && N <= 32, "complement-sum codes with the scratch above");
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    extern __shared__ __attribute__((aligned(128))) uint8_t smem[];
     if (a.gate && *a.gate != a.gate_want) return;   // the classify kernel picked the direct path
     const PlanLayout lay = a.lay;
     const SortLds L = sort_lds(M, K, G, lay.stride, win, true, kGroupScratch3);
@@ -314,8 +314,9 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_code_kernel(PlanArgs
     const uint8_t* s_nl = smem + kV3NLog32;
     const uint32_t copy5 = (threadIdx.x & 3u) << 5;
     // nl(t ^ y) of the lane's copy at nlb ^ y, nlb = the table's LDS address + (t ^ copy << 5): one
-    // XOR per term, exact while the table starts on a 128-byte boundary (dynamic LDS starts at
-    // LDS address 0 in these kernels; anything else is reported, not computed wrong)
+    // XOR per term, exact while the table starts on a 128-byte boundary: smem is declared 128-byte
+    // aligned and the table sits 768 bytes into it (the check below cannot fire; if it ever did,
+    // the sticky error fails the call)
     const uint32_t nl_base = lds_addr(s_nl);
     if (nl_base & 127u) {
         if (threadIdx.x == 0) atomicOr(a.err, 4);

@@ -21,6 +21,7 @@
 #   enc:K,M:BLOCKS:ONLY tools/enc_select.py interleaved encode A/B (BLOCKS 0: 2^23 / k)
 #   torchrun1   bench.py under torchrun with one rank (the RCCL branch on one device)
 #   rehearse2   bench.py --gpus 2 --rehearse-one-gpu (the N-rank code path, gloo, one device)
+#   hostsweep   tools/host_chunk_sweep.py (host-resident pipeline chunk size)
 #   duplex      tools/pcie_duplex_probe (host link per direction and both at once)
 #   zerocopy    tools/zerocopy_probe (kernel reads of pinned host memory)
 set -eo pipefail
@@ -102,6 +103,9 @@ for s in $STEPS; do
       timeout -k 10 300 python bench.py --gpus 2 --rehearse-one-gpu --steps 10 --warmup 3 --no-cpu-baseline --host-blocks 0 \
         > "$O/bench_n2_rehearse.log" 2>&1
       tail -1 "$O/bench_n2_rehearse.log" | cut -c1-400 ;;
+    hostsweep)
+      timeout -k 10 400 python -u tools/host_chunk_sweep.py --chunks 0,3072,4096,6144,8192 > "$O/host_chunk_sweep.log" 2>&1
+      grep -v amdgpu.ids "$O/host_chunk_sweep.log" | cut -c1-400 ;;
     duplex)
       timeout -k 10 120 tools/pcie_duplex_probe > "$O/pcie_duplex_probe.log" 2>&1
       cat "$O/pcie_duplex_probe.log" ;;
