@@ -22,6 +22,7 @@
 #   torchrun1   bench.py under torchrun with one rank (the RCCL branch on one device)
 #   rehearse2   bench.py --gpus 2 --rehearse-one-gpu (the N-rank code path, gloo, one device)
 #   hostsweep   tools/host_chunk_sweep.py (host-resident pipeline chunk size)
+#   twins       tools/twin_sweep.py (RS(8,12) encode and its traffic twin at several residencies)
 #   duplex      tools/pcie_duplex_probe (host link per direction and both at once)
 #   zerocopy    tools/zerocopy_probe (kernel reads of pinned host memory)
 set -eo pipefail
@@ -103,6 +104,9 @@ for s in $STEPS; do
       timeout -k 10 300 python bench.py --gpus 2 --rehearse-one-gpu --steps 10 --warmup 3 --no-cpu-baseline --host-blocks 0 \
         > "$O/bench_n2_rehearse.log" 2>&1
       tail -1 "$O/bench_n2_rehearse.log" | cut -c1-400 ;;
+    twins)
+      timeout -k 10 300 python -u tools/twin_sweep.py > "$O/twin_sweep.log" 2>&1
+      grep -v amdgpu.ids "$O/twin_sweep.log" ;;
     hostsweep)
       timeout -k 10 400 python -u tools/host_chunk_sweep.py --chunks 0,3072,4096,6144,8192 > "$O/host_chunk_sweep.log" 2>&1
       grep -v amdgpu.ids "$O/host_chunk_sweep.log" | cut -c1-400 ;;
