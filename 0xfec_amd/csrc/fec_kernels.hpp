@@ -232,7 +232,8 @@ struct Tuning {
                               // U{1..10} 2930 -> 2872 us (+2.0 %); RS(16,24) +0.2 % (r04b). 3: RS(16,24) and
                               // RS(20,30) by a kernel compiled for the code (fec_plan.hip form 3), the rest 2.
                               // Form 3 over form 2 (r04d, r04e): VALU per plan wave 3171 -> 2064 (RS(20,30)),
-                              // 2176 -> 1380 (RS(16,24)); decode +0.8-0.9 % on both
+                              // 2176 -> 1380 (RS(16,24)); decode +0.8-0.9 % on both. 4: form 3 on two
+                              // segments at a time (r04i: plan busy cycles unchanged, decode +0.2-0.35 %)
     int host_gather = 1;      // FEC_HOST_PINNED reconstruct: parity planes that few blocks read are pulled by
                               // the device straight from the caller's pinned buffer, the rest by 2D DMA (0:
                               // every plane by DMA; 2: every plane by the device)

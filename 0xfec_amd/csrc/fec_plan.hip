@@ -301,14 +301,18 @@ static_assert(kV3Tables == kV2Tables, "forms 2 and 3 share sort_lds's table area
 // bytes [176, 208)
 constexpr uint32_t kV3S = 0, kV3X = 32, kV3O = 80, kV3N = 128, kV3D = 176, kGroupScratch3 = 208;
 
-template <uint32_t K, uint32_t M>
+// H segments (knob dec_pv 4: H = 2) run interleaved in each wave: their fills, sums and coefficient
+// chunks are independent chains the wave issues back to back, so one segment's LDS round trips
+// overlap the other's VALU work (form 3 with H = 1 leaves the SIMD half idle on both pipes)
+template <uint32_t K, uint32_t M, uint32_t H>
 __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_code_kernel(PlanArgs a, uint32_t segs, uint32_t win) {
     constexpr uint32_t N = K + M, LPB = K <= 16 ? 16u : 32u, G = kPlanSortThreads / LPB, MAXE = M;
     static_assert(M < K && M <= 12 && K <= LPB && N <= 32, "complement-sum codes with the scratch above");
+    static_assert(H == 1 || H == 2, "one or two segments at a time");
     extern __shared__ __attribute__((aligned(128))) uint8_t smem[];
     if (a.gate && *a.gate != a.gate_want) return;   // the classify kernel picked the direct path
     const PlanLayout lay = a.lay;
-    const SortLds L = sort_lds(M, K, G, lay.stride, win, true, kGroupScratch3);
+    const SortLds L = sort_lds(M, K, G, lay.stride, win, true, H * kGroupScratch3);
     const uint8_t* s_exp = smem + kV3Exp;
     const uint8_t* s_log = smem + kV3Log;
     const uint8_t* s_nl = smem + kV3NLog32;
@@ -335,95 +339,119 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_code_kernel(PlanArgs
     if (threadIdx.x < N) s_dall[threadIdx.x] = a.dall[threadIdx.x];
     // the group scratch starts zeroed: the coefficient rows below read O and N past a block's own
     // erasure count (stale or zero shard indices and sums, always table-range values)
-    for (uint32_t i = threadIdx.x; i < G * kGroupScratch3 / 4; i += kPlanSortThreads)
+    for (uint32_t i = threadIdx.x; i < H * G * kGroupScratch3 / 4; i += kPlanSortThreads)
         reinterpret_cast<uint32_t*>(smem + L.scratch)[i] = 0u;
-    uint8_t* grp = smem + L.scratch + gb * kGroupScratch3;
-    uint8_t* S = grp + kV3S;
-    uint32_t* Xd = reinterpret_cast<uint32_t*>(grp + kV3X);
-    uint32_t* Od = reinterpret_cast<uint32_t*>(grp + kV3O);
-    uint32_t* Nd = reinterpret_cast<uint32_t*>(grp + kV3N);
-    uint8_t* Dn = grp + kV3D;
+    uint8_t* S[H];
+    uint32_t *Xd[H], *Od[H], *Nd[H];
+    uint8_t* Dn[H];
+#pragma unroll
+    for (uint32_t h = 0; h < H; ++h) {
+        uint8_t* grp = smem + L.scratch + (h * G + gb) * kGroupScratch3;
+        S[h] = grp + kV3S;
+        Xd[h] = reinterpret_cast<uint32_t*>(grp + kV3X);
+        Od[h] = reinterpret_cast<uint32_t*>(grp + kV3O);
+        Nd[h] = reinterpret_cast<uint32_t*>(grp + kV3N);
+        Dn[h] = grp + kV3D;
+    }
     constexpr uint32_t all = N >= 32 ? 0xFFFFFFFFu : (1u << N) - 1u, kmask = (1u << K) - 1u;
     const uint32_t seg0 = blockIdx.x * segs;
-    uint32_t mask_next = seg0 * G + gb < a.nblocks ? a.masks[seg0 * G + gb] : 0u;
-    for (uint32_t sg = 0; sg < segs; ++sg) {
+    uint32_t mask_next[H];
+#pragma unroll
+    for (uint32_t h = 0; h < H; ++h) {
+        const uint32_t bh = (seg0 + h) * G + gb;
+        mask_next[h] = h < segs && bh < a.nblocks ? a.masks[bh] : 0u;
+    }
+    // segs and win are multiples of H (code_launch); the window's segments wl .. wl + H - 1
+    for (uint32_t sg = 0; sg < segs; sg += H) {
         const uint32_t base = (seg0 + sg) * G;
         if (base >= a.nblocks) break;   // workgroup-uniform
-        const uint32_t b = base + gb;
-        const bool valid = b < a.nblocks;
-        const uint32_t mask_in = mask_next;
-        const uint32_t bn = b + G;
-        mask_next = (sg + 1 < segs && bn < a.nblocks) ? a.masks[bn] : 0u;
         const uint32_t wl = sg % win;
         if (wl == 0) __syncthreads();
         else wave_sync();
-        uint8_t* P = smem + L.recs + ((size_t)wl * G + gb) * lay.stride;
-        const uint32_t mask = valid ? mask_in & all : all;
-        const uint32_t e = K - __popc(mask & kmask);
-        int32_t st = a.max_out ? (int32_t)e : 0;
-        uint32_t nout = 0;
-        if (e != 0) {
-            if ((uint32_t)__popc(mask) < K) {
-                st = -4;   // FEC_ERR_TOO_FEW_SHARDS
-                if (gl == 0) atomicOr(a.err, 1);
-            } else if (a.max_out && e > a.max_out) {
-                st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
-                if (gl == 0) atomicOr(a.err, 2);
-            } else {
-                nout = e;
+        uint8_t* P[H];
+        uint32_t mask[H], e[H], nout[H];
+#pragma unroll
+        for (uint32_t h = 0; h < H; ++h) {
+            // a segment past the batch (the second of a pair) makes records with no output for
+            // blocks >= nblocks: ranked last and never copied out (sort_window_out)
+            const uint32_t b = base + h * G + gb;
+            const bool valid = b < a.nblocks;
+            const uint32_t mask_in = mask_next[h];
+            const uint32_t bn = b + H * G;
+            mask_next[h] = (sg + H + h < segs && bn < a.nblocks) ? a.masks[bn] : 0u;
+            P[h] = smem + L.recs + ((size_t)(wl + h) * G + gb) * lay.stride;
+            mask[h] = valid ? mask_in & all : all;
+            e[h] = K - __popc(mask[h] & kmask);
+            int32_t st = a.max_out ? (int32_t)e[h] : 0;
+            nout[h] = 0;
+            if (e[h] != 0) {
+                if ((uint32_t)__popc(mask[h]) < K) {
+                    st = -4;   // FEC_ERR_TOO_FEW_SHARDS
+                    if (gl == 0) atomicOr(a.err, 1);
+                } else if (a.max_out && e[h] > a.max_out) {
+                    st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
+                    if (gl == 0) atomicOr(a.err, 2);
+                } else {
+                    nout[h] = e[h];
+                }
+            }
+            if (gl == 0) {
+                P[h][lay.nout_off] = (uint8_t)nout[h];
+                *reinterpret_cast<uint32_t*>(P[h] + lay.blk_off) = b;
+                if (valid && a.status) a.status[b] = st;
             }
         }
-        if (gl == 0) {
-            P[lay.nout_off] = (uint8_t)nout;
-            *reinterpret_cast<uint32_t*>(P + lay.blk_off) = b;
-            if (valid && a.status) a.status[b] = st;
-        }
-        if (nout) {
 #pragma unroll
-            for (uint32_t t0 = 0; t0 < N; t0 += LPB) {
-                const uint32_t t = t0 + gl;
-                if (t < N) {
-                    const uint32_t below = mask & ((1u << t) - 1u);   // t < 32
-                    const uint32_t pos = __popc(below);
-                    if (((mask >> t) & 1u) && pos < K) {
-                        S[pos] = (uint8_t)t;
-                    } else {
-                        Xd[t - min(pos, K)] = t;   // not an input: erased, or present past the first K
-                        if (t < K && !((mask >> t) & 1u)) Od[t - pos] = t;   // erased data shards below t: t - pos
+        for (uint32_t h = 0; h < H; ++h) {
+            if (nout[h]) {
+#pragma unroll
+                for (uint32_t t0 = 0; t0 < N; t0 += LPB) {
+                    const uint32_t t = t0 + gl;
+                    if (t < N) {
+                        const uint32_t below = mask[h] & ((1u << t) - 1u);   // t < 32
+                        const uint32_t pos = __popc(below);
+                        if (((mask[h] >> t) & 1u) && pos < K) {
+                            S[h][pos] = (uint8_t)t;
+                        } else {
+                            Xd[h][t - min(pos, K)] = t;   // not an input: erased, or present past the first K
+                            if (t < K && !((mask[h] >> t) & 1u)) Od[h][t - pos] = t;   // erased data shards below t: t - pos
+                        }
                     }
                 }
             }
         }
         wave_sync();
-        if (nout) {
-            if (gl < K) P[lay.in_off + gl] = S[gl];
-            if (gl < nout) P[lay.out_off + gl] = (uint8_t)Od[gl];
-            if (e == 1) {
+#pragma unroll
+        for (uint32_t h = 0; h < H; ++h) {
+            if (!nout[h]) continue;
+            if (gl < K) P[h][lay.in_off + gl] = S[h][gl];
+            if (gl < nout[h]) P[h][lay.out_off + gl] = (uint8_t)Od[h][gl];
+            if (e[h] == 1) {
                 // one erasure: x_E = inv(A[R0][E]) * (p_R0 ^ sum_j A[R0][j] x_j)
-                const uint32_t E0 = Od[0];
-                const uint32_t R0 = __ffs(mask >> K) - 1;
+                const uint32_t E0 = Od[h][0];
+                const uint32_t R0 = __ffs(mask[h] >> K) - 1;
                 const uint8_t* row = s_prows + R0 * K;
                 const uint32_t inv = s_exp[255 - s_log[row[E0]]];
                 if (gl < K) {
-                    const uint32_t sj = S[gl];
-                    P[lay.coef_off + gl] = (uint8_t)(sj < K ? (row[sj] ? s_exp[s_log[inv] + s_log[row[sj]]] : 0u) : inv);
+                    const uint32_t sj = S[h][gl];
+                    P[h][lay.coef_off + gl] = (uint8_t)(sj < K ? (row[sj] ? s_exp[s_log[inv] + s_log[row[sj]]] : 0u) : inv);
                 }
             } else {
                 uint32_t x[M];
 #pragma unroll
-                for (uint32_t u = 0; u < M; ++u) x[u] = Xd[u];
+                for (uint32_t u = 0; u < M; ++u) x[u] = Xd[h][u];
 #pragma unroll
                 for (uint32_t q0 = 0; q0 < K + MAXE; q0 += LPB) {
                     const uint32_t q = q0 + gl;
-                    if (q < K + e) {
-                        const uint32_t t = q < K ? (uint32_t)S[q] : Od[q - K];
+                    if (q < K + e[h]) {
+                        const uint32_t t = q < K ? (uint32_t)S[h][q] : Od[h][q - K];
                         const uint32_t tb = nl_base + (t ^ copy5);
                         uint32_t sum = s_dall[t];
 #pragma unroll
                         for (uint32_t u = 0; u < M; ++u) sum += lds_ld8(tb ^ x[u]);
                         sum %= 255u;
-                        if (q < K) Dn[q] = (uint8_t)(255u - sum);
-                        else Nd[q - K] = sum;
+                        if (q < K) Dn[h][q] = (uint8_t)(255u - sum);
+                        else Nd[h][q - K] = sum;
                     }
                 }
             }
@@ -432,33 +460,38 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_code_kernel(PlanArgs
         // coefficient rows in chunks of 4, each chunk computed whole (rows past a block's count read
         // stale but in-range scratch, and are not stored) so its 12 LDS loads are in flight together;
         // a chunk runs while some block of the wave needs it
-        uint32_t nw = nout;
+        uint32_t nw[H];
 #pragma unroll
-        for (uint32_t o = LPB; o < 64; o <<= 1) nw = max(nw, (uint32_t)__shfl_xor((int)nw, (int)o));
-        nw = (uint32_t)__builtin_amdgcn_readfirstlane((int)nw);
-        if (nw >= 2 && gl < K) {
-            const uint32_t sb = nl_base + ((uint32_t)S[gl] ^ copy5), dn = Dn[gl];
-            const uint32_t exp_base = lds_addr(s_exp);
-            uint8_t* C = P + lay.coef_off + gl;
+        for (uint32_t h = 0; h < H; ++h) {
+            nw[h] = nout[h];
 #pragma unroll
-            for (uint32_t r0 = 0; r0 < MAXE; r0 += 4) {
-                if (r0 >= nw) break;   // wave-uniform
+            for (uint32_t o = LPB; o < 64; o <<= 1) nw[h] = max(nw[h], (uint32_t)__shfl_xor((int)nw[h], (int)o));
+            nw[h] = (uint32_t)__builtin_amdgcn_readfirstlane((int)nw[h]);
+        }
+        const uint32_t exp_base = lds_addr(s_exp);
+#pragma unroll
+        for (uint32_t r0 = 0; r0 < MAXE; r0 += 4) {
+#pragma unroll
+            for (uint32_t h = 0; h < H; ++h) {
+                if (r0 >= nw[h] || nw[h] < 2 || gl >= K) continue;   // wave-uniform but for gl
+                const uint32_t sb = nl_base + ((uint32_t)S[h][gl] ^ copy5), dn = Dn[h][gl];
                 uint32_t c[4];
 #pragma unroll
                 for (uint32_t j = 0; j < 4; ++j)
-                    if (r0 + j < MAXE) c[j] = lds_ld8(exp_base + Nd[r0 + j] + lds_ld8(sb ^ Od[r0 + j]) + dn);
+                    if (r0 + j < MAXE) c[j] = lds_ld8(exp_base + Nd[h][r0 + j] + lds_ld8(sb ^ Od[h][r0 + j]) + dn);
+                uint8_t* C = P[h] + lay.coef_off + gl;
 #pragma unroll
                 for (uint32_t j = 0; j < 4; ++j)
-                    if (r0 + j < MAXE && r0 + j < nout && nout >= 2) C[(r0 + j) * K] = (uint8_t)c[j];
+                    if (r0 + j < MAXE && r0 + j < nout[h] && nout[h] >= 2) C[(r0 + j) * K] = (uint8_t)c[j];
             }
         }
-        const bool last = sg + 1 == segs || base + G >= a.nblocks;
-        if (wl + 1 < win && !last) continue;   // workgroup-uniform
-        sort_window_out(a, smem, L, (wl + 1) * G, base - wl * G);
+        const bool last = sg + H >= segs || base + H * G >= a.nblocks;
+        if (wl + H < win && !last) continue;   // workgroup-uniform
+        sort_window_out(a, smem, L, (wl + H) * G, base - wl * G);
     }
 }
 
-template <uint32_t K, uint32_t M>
+template <uint32_t K, uint32_t M, uint32_t H>
 hipError_t code_launch(const PlanArgs& a, hipStream_t s) {
     constexpr uint32_t LPB = K <= 16 ? 16u : 32u, G = kPlanSortThreads / LPB;
     const uint32_t nseg = (a.nblocks + G - 1) / G;
@@ -466,11 +499,12 @@ hipError_t code_launch(const PlanArgs& a, hipStream_t s) {
     uint32_t segs = g_tune.dec_pseg > 0 ? (uint32_t)g_tune.dec_pseg : std::max<uint32_t>(1, nseg / 4096);
     if (a.gate) segs = 64;
     segs = std::min<uint32_t>(segs, 64);
-    const uint32_t win = std::min<uint32_t>(sort_window(G, g_tune.dec_psort), 64);
-    if (win > 1) segs = (segs + win - 1) / win * win;
+    uint32_t win = std::min<uint32_t>(sort_window(G, g_tune.dec_psort), 64);
+    win = (win + H - 1) / H * H;   // a window holds whole groups of H segments
+    segs = (segs + win - 1) / win * win;
     const uint32_t grid = (nseg + segs - 1) / segs;
-    const size_t lds = sort_lds(M, K, G, a.lay.stride, win, true, kGroupScratch3).total;
-    hipLaunchKernelGGL((rs_plan_code_kernel<K, M>), dim3(grid), dim3(kPlanSortThreads), lds, s, a, segs, win);
+    const size_t lds = sort_lds(M, K, G, a.lay.stride, win, true, H * kGroupScratch3).total;
+    hipLaunchKernelGGL((rs_plan_code_kernel<K, M, H>), dim3(grid), dim3(kPlanSortThreads), lds, s, a, segs, win);
     return hipGetLastError();
 }
 
@@ -500,8 +534,11 @@ hipError_t sorted_launch(const PlanArgs& a, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_rs_plan_sorted(const PlanArgs& a, hipStream_t s) {
-    if (g_tune.dec_pv == 3 && a.k == 16 && a.m == 8 && a.maxe == 8) return code_launch<16, 8>(a, s);
-    if (g_tune.dec_pv == 3 && a.k == 20 && a.m == 10 && a.maxe == 10) return code_launch<20, 10>(a, s);
+    const int pv = g_tune.dec_pv;
+    if (pv >= 3 && a.k == 16 && a.m == 8 && a.maxe == 8)
+        return pv == 4 ? code_launch<16, 8, 2>(a, s) : code_launch<16, 8, 1>(a, s);
+    if (pv >= 3 && a.k == 20 && a.m == 10 && a.maxe == 10)
+        return pv == 4 ? code_launch<20, 10, 2>(a, s) : code_launch<20, 10, 1>(a, s);
     switch (plan_lanes(a.k)) {
         case 2: return sorted_launch<2>(a, s);
         case 4: return sorted_launch<4>(a, s);

@@ -78,6 +78,7 @@ def main():
             variants["table-copy rebuild (fixk 4), plans sorted over %d blocks" % (64 * ps)] = dict(D, dec_fixk=4, dec_psort=ps)
         variants["plan form 1 (round 3)"] = dict(D, dec_pv=1)
         variants["plan form 2 (runtime code)"] = dict(D, dec_pv=2)
+        variants["plan form 3 paired segments"] = dict(D, dec_pv=4)
         variants["padded rebuild slice (lpad)"] = dict(D, dec_lpad=1)
         variants["padded rebuild slice (lpad), wpc 3"] = dict(D, dec_lpad=1, dec_wpc=3)
         for ov in (2, 4, 8):

@@ -7,7 +7,7 @@
 #   tests smoke bench prof pmc configs go counters
 # steps:
 #   tests       pytest -m gpu (the whole GPU suite)
-#   variants    pytest -m gpu -k kernel_variants (every kernel variant against the oracle)
+#   variants    pytest -m gpu -k kernel_variants / plan forms (every kernel variant against the oracle)
 #   smoke       __graft_entry__.smoke()
 #   bench       bench.py (the contract line)
 #   prof        rocprofv3 --kernel-trace --stats of bench.py -> kernel_trace_summary.json
@@ -41,7 +41,7 @@ for s in $STEPS; do
       timeout -k 10 600 $PYT tests --maxfail=3 > "$O/pytest_gpu.log" 2>&1 || { tail -30 "$O/pytest_gpu.log"; exit 1; }
       tail -2 "$O/pytest_gpu.log" ;;
     variants)
-      timeout -k 10 300 $PYT tests/test_gpu_codec.py -x -k kernel_variants > "$O/pytest_variants.log" 2>&1 || { tail -30 "$O/pytest_variants.log"; exit 1; }
+      timeout -k 10 300 $PYT tests/test_gpu_codec.py -x -k "kernel_variants or plan_forms or plan_overlap" > "$O/pytest_variants.log" 2>&1 || { tail -30 "$O/pytest_variants.log"; exit 1; }
       tail -1 "$O/pytest_variants.log" ;;
     smoke)
       timeout -k 10 120 python -u -c 'import __graft_entry__ as g; g.smoke()' > "$O/smoke.log" 2>&1
