@@ -10,7 +10,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <functional>
+#include <mutex>
 #include <map>
 #include <thread>
 #include <utility>
@@ -706,15 +708,86 @@ static size_t host_chunk_blocks(size_t bytes_per_block) {
     return std::max<size_t>(1, kStageBytes / std::max<size_t>(1, bytes_per_block));
 }
 
-// fn(lo, hi) over [0, n) on up to 8 threads: the staging and scatter copies of FEC_HOST
-// (one core copies ~10 GB/s, a fifth of PCIe).
+// Copy workers made once per process for parallel_for: a chunk's staging or scatter copy then
+// costs two condition-variable hand-offs instead of creating and joining a thread per part
+// (tens of microseconds each, ~40 times per pageable bench step). One call at a time: a caller
+// that finds the pool busy (another thread's FEC_HOST call) makes its own threads as before.
+class CopyPool {
+   public:
+    static CopyPool& get() {
+        static CopyPool* p = new CopyPool();   // never destroyed: workers may outlive static teardown
+        return *p;
+    }
+    // false: busy, nothing run
+    bool run(unsigned parts, size_t n, const std::function<void(size_t, size_t)>& fn) {
+        std::unique_lock<std::mutex> call(call_mu_, std::try_to_lock);
+        if (!call.owns_lock()) return false;
+        std::unique_lock<std::mutex> lk(mu_);
+        while (th_.size() + 1 < parts) th_.emplace_back([this] { work(); });
+        fn_ = &fn;
+        n_ = n;
+        per_ = (n + parts - 1) / parts;
+        parts_ = (unsigned)((n + per_ - 1) / per_);
+        next_ = 1;   // part 0 is the caller's
+        left_ = parts_;
+        ++gen_;
+        lk.unlock();
+        cv_.notify_all();
+        fn(0, std::min(n, per_));
+        lk.lock();
+        --left_;
+        for (;;) {   // the caller takes parts too while any are unclaimed
+            if (next_ >= parts_) break;
+            const unsigned i = next_++;
+            lk.unlock();
+            fn(i * per_, std::min(n, (i + 1) * per_));
+            lk.lock();
+            --left_;
+        }
+        done_.wait(lk, [this] { return left_ == 0; });
+        fn_ = nullptr;
+        return true;
+    }
+
+   private:
+    void work() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return gen_ != seen; });
+            seen = gen_;
+            while (fn_ && next_ < parts_) {
+                const unsigned i = next_++;
+                const auto* fn = fn_;
+                const size_t lo = i * per_, hi = std::min(n_, (i + 1) * per_);
+                lk.unlock();
+                (*fn)(lo, hi);
+                lk.lock();
+                if (--left_ == 0) done_.notify_all();
+            }
+        }
+    }
+    std::mutex call_mu_, mu_;
+    std::condition_variable cv_, done_;
+    std::vector<std::thread> th_;
+    const std::function<void(size_t, size_t)>* fn_ = nullptr;
+    size_t n_ = 0, per_ = 0;
+    unsigned parts_ = 0, next_ = 0, left_ = 0;
+    uint64_t gen_ = 0;
+};
+
+// fn(lo, hi) over [0, n) on up to host_threads threads (knob, 8): the staging and scatter copies
+// of FEC_HOST (one core copies ~10 GB/s, a fifth of PCIe). Knob host_pool (1): on CopyPool's
+// persistent workers; 0: threads made per call (round 4 before r04j).
 template <class F>
 static void parallel_for(size_t n, F fn) {
-    const unsigned T = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+    const unsigned T = std::min<unsigned>((unsigned)std::max(1, fk::g_tune.host_threads),
+                                          std::max(1u, std::thread::hardware_concurrency()));
     if (n < 512 || T == 1) {
         fn((size_t)0, n);
         return;
     }
+    if (fk::g_tune.host_pool && CopyPool::get().run(T, n, std::function<void(size_t, size_t)>(fn))) return;
     std::vector<std::thread> th;
     const size_t per = (n + T - 1) / T;
     for (size_t lo = 0; lo < n; lo += per) th.emplace_back(fn, lo, std::min(n, lo + per));
@@ -1303,7 +1376,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 39 ? &fk::g_tune.dec_psort : key == 40 ? &fk::g_tune.dec_pv
               : key == 41 ? &fk::g_tune.dec_povl : key == 42 ? &fk::g_tune.dec_lpad
               : key == 43 ? &fk::g_tune.bat_zc
-              : key == 44 ? &fk::g_tune.enc_early : nullptr;
+              : key == 44 ? &fk::g_tune.enc_early : key == 45 ? &fk::g_tune.host_threads
+              : key == 46 ? &fk::g_tune.host_pool : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

@@ -177,6 +177,8 @@ struct Tuning {
                               // lookup (1: rows expanded from scalar-loaded coefficients, 2: PermTab rows
                               // copied by a vector load); multi-erasure waves go to a worklist kernel
     int host_chunk = 0;       // host-resident path: blocks per staging chunk (0: 128 MiB worth)
+    int host_threads = 8;     // FEC_HOST (pageable): host threads for the staging / scatter copies
+    int host_pool = 1;        // FEC_HOST copies on persistent workers (fec_capi.cpp CopyPool); 0: per call
     int dec_fixk = 4;         // RS(16,24) / RS(20,30) rebuild with k at compile time (1: all k loads in
                               // flight; 2: a rolling window of 8 loaded inputs, shards of 64+ chunks,
                               // RS(20,30) also with the rows' table reads pipelined one row ahead;

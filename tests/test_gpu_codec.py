@@ -637,6 +637,70 @@ def test_rs_host_pipeline_many_chunks_multi_erasure(codec, oracle, fec, k, m, ch
         codec.set_tuning(**old)
 
 
+@pytest.mark.parametrize("pool,threads,chunk", [(1, 8, 0), (1, 3, 1100), (0, 8, 1100), (1, 16, 600), (0, 5, 0)])
+def test_rs_host_copy_pool_matches_oracle(codec, oracle, fec, pool, threads, chunk):
+    """FEC_HOST (pageable) with chunks of >= 512 blocks, whose staging and scatter copies run on
+    several host threads: the persistent copy workers (knob host_pool 1) or threads made per call
+    (0), with 3..16 parts and one chunk or several. Encode and a multi-erasure reconstruct against
+    the oracle."""
+    rng = np.random.default_rng(300 + pool + threads + chunk)
+    k, m, B, L = 8, 4, 3000, 600
+    n = k + m
+    full = np.zeros((B, n, L), dtype=np.uint8)
+    full[:, :k] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    oracle.rs_encode(k, m, full)
+    old = codec.set_tuning(host_pool=pool, host_threads=threads, host_chunk=chunk)
+    try:
+        data = full[:, :k].copy()
+        par = np.zeros((B, m, L), dtype=np.uint8)
+        codec.rs_encode_split(k, m, data, par, shard_len=L)
+        assert np.array_equal(par, full[:, k:])
+        masks = _random_masks(rng, B, k, m, max_loss=m)
+        dmg = full[:, :k].copy()
+        lost = ~((masks[:, None] >> np.arange(k)[None, :]) & 1).astype(bool)
+        dmg[lost] = 0xA1
+        st = np.full(B, 7, dtype=np.int32)
+        rc = codec.rs_reconstruct_split(k, m, dmg, par, masks, status=st, shard_len=L)
+        assert rc == fec.FEC_OK and (st == 0).all()
+        assert np.array_equal(dmg, full[:, :k])
+    finally:
+        codec.set_tuning(**old)
+
+
+def test_rs_host_copy_pool_concurrent_contexts(oracle, fec):
+    """Two contexts on two threads in FEC_HOST calls at once: one gets the persistent copy
+    workers, the other finds them busy and copies on threads of its own; both results exact."""
+    import threading
+    k, m, B, L = 8, 4, 2000, 900
+    rng = np.random.default_rng(99)
+    full = np.zeros((B, k + m, L), dtype=np.uint8)
+    full[:, :k] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    oracle.rs_encode(k, m, full)
+    errs = []
+
+    def worker(seed):
+        c = fec.Codec(0)
+        try:
+            for _ in range(6):
+                data = full[:, :k].copy()
+                par = np.zeros((B, m, L), dtype=np.uint8)
+                c.rs_encode_split(k, m, data, par, shard_len=L)
+                if not np.array_equal(par, full[:, k:]):
+                    errs.append("encode %d" % seed)
+        except Exception as e:   # reported below, in the main thread
+            errs.append(repr(e))
+        finally:
+            c.close()
+
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in ts)
+    assert not errs, errs
+
+
 def test_stream_switch_orders_shared_workspace(fec, torch):
     """fec_ctx_set_stream between two launches that share the ctx's workspace (the RS(16,24)
     plan records): the second stream must not rewrite the records while the first stream's

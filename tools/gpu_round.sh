@@ -22,6 +22,7 @@
 #   torchrun1   bench.py under torchrun with one rank (the RCCL branch on one device)
 #   rehearse2   bench.py --gpus 2 --rehearse-one-gpu (the N-rank code path, gloo, one device)
 #   hostsweep   tools/host_chunk_sweep.py (host-resident pipeline chunk size)
+#   hostthreads tools/host_chunk_sweep.py --threads (pageable staging copy threads)
 #   twins       tools/twin_sweep.py (RS(8,12) encode and its traffic twin at several residencies)
 #   duplex      tools/pcie_duplex_probe (host link per direction and both at once)
 #   zerocopy    tools/zerocopy_probe (kernel reads of pinned host memory)
@@ -110,6 +111,9 @@ for s in $STEPS; do
     hostsweep)
       timeout -k 10 400 python -u tools/host_chunk_sweep.py --chunks 0,3072,4096,6144,8192 > "$O/host_chunk_sweep.log" 2>&1
       grep -v amdgpu.ids "$O/host_chunk_sweep.log" | cut -c1-400 ;;
+    hostthreads)
+      timeout -k 10 400 python -u tools/host_chunk_sweep.py --threads 8,12,16 --pools 0,1 --reps 3 > "$O/host_thread_sweep.log" 2>&1
+      grep -v amdgpu.ids "$O/host_thread_sweep.log" | tail -1 ;;
     duplex)
       timeout -k 10 120 tools/pcie_duplex_probe > "$O/pcie_duplex_probe.log" 2>&1
       cat "$O/pcie_duplex_probe.log" ;;

@@ -25,6 +25,7 @@ cp_if "$S/pcie_duplex_probe.log" "$D/pcie_duplex_probe_$TAG.log"
 cp_if "$S/zerocopy_probe.log" "$D/zerocopy_probe_$TAG.log"
 cp_if "$S/pytest_variants.log" "$D/pytest_variants_$TAG.log"
 cp_if "$S/host_chunk_sweep.log" "$D/host_chunk_sweep_$TAG.log"
+cp_if "$S/host_thread_sweep.log" "$D/host_thread_sweep_$TAG.log"
 cp_if "$S/twin_sweep.log" "$D/twin_sweep_$TAG.log"
 cp_if "$S/bench_torchrun_n1_rccl.log" "$D/bench_torchrun_n1_rccl_$TAG.log"
 for f in "$S"/ab_*.log "$S"/enc_*.log; do cp_if "$f" "$D/$(basename "$f" .log)_$TAG.log"; done
