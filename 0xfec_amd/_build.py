@@ -14,7 +14,7 @@ OBJ = os.path.join(HERE, "_obj")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 LIB = os.path.join(HERE, "lib0xfec_hip.so")
 
-SOURCES = ["fec_encode.hip", "fec_decode.hip", "fec_rebuild.hip", "fec_recover.hip", "fec_plan.hip", "fec_xor.hip", "fec_synth.hip", "fec_pack.hip", "fec_probe.hip", "fec_kernels.hip", "fec_capi.cpp",
+SOURCES = ["fec_encode.hip", "fec_encode23.hip", "fec_decode.hip", "fec_rebuild.hip", "fec_recover.hip", "fec_plan.hip", "fec_xor.hip", "fec_synth.hip", "fec_pack.hip", "fec_probe.hip", "fec_kernels.hip", "fec_capi.cpp",
            "fec_scheme.cpp", "fec_batch.cpp", "fec_wire.cpp", "fec_go.cpp"]
 HEADERS = ["fec_kernels.hpp", "fec_device.hpp", "fec_recon.hpp", "gf256.h", "rs_matrix.hpp", "fec_bitslice.inc"]
 PUBLIC = ["fec_hip.h", "fec_scheme.h", "fec_batch.h", "fec_batch.hpp", "fec_scheme.hpp", "fec_wire.h", "fec_go.h", "fec_synth.h", "fec_probe.h"]

@@ -592,6 +592,7 @@ hipError_t launch_rs_encode_fixed(EncodeArgs a, int ncu, hipStream_t s) {
         a.per_xcd = ((a.total + 7) / 8 + kThreads - 1) / kThreads * kThreads;
     }
     const size_t lds = occupancy_lds(wpc, (size_t)a.m * a.k * sizeof(gf::PermTab));
+    if (!queue && rs_encode23_applies(a.k, a.m)) return launch_rs_encode23(a, s);
     if (a.k == 2 && a.m == 1) return enc_fixed_dispatch<2, 1>(a, grid, lds, queue, s);
     if (a.k == 8 && a.m == 4) return enc_fixed_dispatch<8, 4>(a, grid, lds, queue, s);
     if (a.k == 16 && a.m == 8) return enc_fixed_dispatch<16, 8>(a, grid, lds, queue, s);

@@ -179,6 +179,8 @@ struct Tuning {
     int host_chunk = 0;       // host-resident path: blocks per staging chunk (0: 128 MiB worth)
     int host_threads = 8;     // FEC_HOST (pageable): host threads for the staging / scatter copies
     int host_pool = 1;        // FEC_HOST copies on persistent workers (fec_capi.cpp CopyPool); 0: per call
+    int enc_x23 = 1;          // RS(2,3) fixed-shape encode by its [3 2] parity row, one GF doubling per byte and
+                              // no tables (fec_encode23.hip); 0: the table-driven fixed kernel
     int dec_fixk = 4;         // RS(16,24) / RS(20,30) rebuild with k at compile time (1: all k loads in
                               // flight; 2: a rolling window of 8 loaded inputs, shards of 64+ chunks,
                               // RS(20,30) also with the rows' table reads pipelined one row ahead;
@@ -268,6 +270,8 @@ hipError_t launch_rs_encode(const EncodeArgs& a, int grid, hipStream_t s);
 // Fixed-shape encode (flat grid, one item per lane) for the shapes it is instantiated for.
 bool fixed_encode_applies(uint32_t k, uint32_t m);
 hipError_t launch_rs_encode_fixed(EncodeArgs a, int ncu, hipStream_t s);
+bool rs_encode23_applies(uint32_t k, uint32_t m);            // fec_encode23.hip
+hipError_t launch_rs_encode23(const EncodeArgs& a, hipStream_t s);
 hipError_t launch_rs_plan(const PlanArgs& a, hipStream_t s);
 // Sorted plans (fec_plan.hip): lanes of a wave cooperate on one block's plan; within each
 // workgroup's segment of blocks the records are stored ordered by erasure count, each naming

@@ -291,11 +291,15 @@ def test_rs_recover_out_of_place(codec, oracle, torch, fec, k, m, slots):
 # ranges empty, partial and ragged (B * ceil(L/16) items vs 8 ranges of 256-item chunks).
 ENC_VARIANTS = {
     "generic": dict(enc_fixed=0),
-    "fixed_flat": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=1),
-    "fixed_flat_matrix": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=0),
+    "fixed_flat": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=1, enc_x23=0),
+    "fixed_flat_matrix": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=0, enc_x23=0),
     # shard loads issued before the table staging (knob enc_early), dyadic and matrix bodies
-    "fixed_flat_early": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=1, enc_bits=0, enc_early=1),
-    "fixed_flat_matrix_early": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=0, enc_bits=0, enc_early=1),
+    "fixed_flat_early": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=1, enc_bits=0, enc_early=1, enc_x23=0),
+    "fixed_flat_matrix_early": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=0, enc_bits=0, enc_early=1,
+                                    enc_x23=0),
+    # RS(2,3) by its [3 2] parity row, no tables (knob enc_x23; other codes: the fixed kernels)
+    "fixed_flat_x23": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_x23=1),
+    "fixed_flat_x23_plain": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_x23=1, enc_nt=0),
     "queue_d0": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=0),
     "queue_d0_nodrain": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=-1),
     "queue_d1": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=1),

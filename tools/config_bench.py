@@ -169,12 +169,27 @@ def run_xor(torch, fec, codec, k, B, iters, seed):
     t_dec = timed(torch, dec, iters)
     enc_bytes = B * (k + 1) * L
     dec_bytes = B * (k + 1) * L
+    probe = {}
+    if k == 2:
+        # the RS(2,3) twins over the interleaved XOR layout: k reads + 1 write per block either way
+        # (the decode twin writes the rebuilt shard to a separate buffer, as many bytes)
+        out = torch.zeros((B, 1, S), dtype=torch.uint8, device="cuda")
+
+        def enc_twin():
+            codec.probe_encode_traffic_raw(k, 1, L, B, shp, n * S, shp + k * S, n * S, S)
+
+        def dec_twin():
+            codec.probe_recover_traffic_raw(k, 1, L, B, shp, n * S, shp + k * S, n * S, S, mp, out.data_ptr(), S)
+        probe["encode_probe_TB/s"] = round(enc_bytes / timed(torch, enc_twin, iters) / 1e9, 3)
+        probe["encode_frac_of_probe"] = round(enc_bytes / t_enc / 1e9 / probe["encode_probe_TB/s"], 4)
+        probe["decode_probe_TB/s"] = round(dec_bytes / timed(torch, dec_twin, iters) / 1e9, 3)
+        probe["decode_frac_of_probe"] = round(dec_bytes / t_dec / 1e9 / probe["decode_probe_TB/s"], 4)
     return {"config": "XOR(%d,1)" % k, "blocks": B, "erasures": "1 data shard",
             "encode_ms": round(t_enc, 4), "decode_ms": round(t_dec, 4),
             "encode_TB/s": round(enc_bytes / t_enc / 1e9, 3), "decode_TB/s": round(dec_bytes / t_dec / 1e9, 3),
             "payload_GiB/s": round(B * k * PAYLOAD / 2**30 / ((t_enc + t_dec) / 1e3), 1),
             "step_frac": round((enc_bytes + dec_bytes) / ((t_enc + t_dec) / 1e3) / 8e12, 4),
-            "check": ok}
+            "check": ok, **probe}
 
 
 def main():

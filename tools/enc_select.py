@@ -38,10 +38,13 @@ def main():
     variants["bits wpc0, plain loads"] = dict(enc_queue=0, enc_bits=11, enc_bwpc=0, enc_nt=2)
     if k == 8:
         variants["matrix queue d0 wpc2"] = dict(enc_queue=1, enc_qwpc=2, enc_qdepth=0, enc_dyadic=0)
+    if k == 2 and m == 1:   # the [3 2] parity row by one GF doubling per byte, no tables (enc_x23)
+        variants["x23"] = dict(enc_queue=0, enc_x23=1)
+        variants["x23, plain loads and stores"] = dict(enc_queue=0, enc_x23=1, enc_nt=0)
     if only:
         variants = {n: kv for n, kv in variants.items() if any(x in n for x in only)}
     base = codec.set_tuning(enc_queue=0, enc_wpc=3, enc_qwpc=2, enc_qdepth=0, enc_dyadic=1, enc_nt=3, enc_bits=0,
-                            enc_bwpc=0, enc_early=0)
+                            enc_bwpc=0, enc_early=0, enc_x23=0)
     ref = None
     for n, kv in variants.items():   # every form writes the same parity bytes
         codec.set_tuning(**kv)
