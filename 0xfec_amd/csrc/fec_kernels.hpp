@@ -179,6 +179,9 @@ struct Tuning {
     int host_chunk = 0;       // host-resident path: blocks per staging chunk (0: 128 MiB worth)
     int host_threads = 8;     // FEC_HOST (pageable): host threads for the staging / scatter copies
     int host_pool = 1;        // FEC_HOST copies on persistent workers (fec_capi.cpp CopyPool); 0: per call
+    int xor_fix2 = 0;         // XOR(2,1) reconstruct by its own one-item-per-lane kernel (fec_xor.hip). r04m,
+                              // three interleaved rounds: 0.6443 vs 0.6395 ms for the generic kernel (-0.7 %):
+                              // the gap to the XOR twin (0.955) is the in-place write, not the loop. Off
     int enc_x23 = 1;          // RS(2,3) fixed-shape encode by its [3 2] parity row, one GF doubling per byte and
                               // no tables (fec_encode23.hip); 0: the table-driven fixed kernel
     int dec_fixk = 4;         // RS(16,24) / RS(20,30) rebuild with k at compile time (1: all k loads in

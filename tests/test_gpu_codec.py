@@ -160,10 +160,10 @@ def test_rs_host_path_matches_oracle(codec, oracle, k, m):
     assert np.array_equal(dmg[:, :k], sh[:, :k])
 
 
-@pytest.mark.parametrize("k", [1, 2, 3, 9, 31])
+@pytest.mark.parametrize("k,fix2", [(1, 1), (2, 1), (2, 0), (3, 1), (9, 1), (31, 1)])   # fix2: XOR(2,1)'s own kernel
 @pytest.mark.parametrize("L", [1, 6, 18, 1202, 1436])
-def test_xor_device_matches_oracle(codec, oracle, torch, k, L):
-    rng = np.random.default_rng(k + L)
+def test_xor_device_matches_oracle(codec, oracle, torch, k, fix2, L):
+    rng = np.random.default_rng(k + L + 100 * fix2)
     n = k + 1
     S = (L + 15) // 16 * 16
     B = 65
@@ -185,11 +185,14 @@ def test_xor_device_matches_oracle(codec, oracle, torch, k, L):
     st_ref = oracle.xor_reconstruct(k, want, masks)
     dd = torch.from_numpy(dmg).cuda()
     ds = torch.zeros(B, dtype=torch.int32, device="cuda")
-    codec.xor_reconstruct(k, dd, torch.from_numpy(masks.view(np.int32)).cuda(), status=ds, shard_len=L)
+    old = codec.set_tuning(xor_fix2=fix2)
     try:
+        codec.xor_reconstruct(k, dd, torch.from_numpy(masks.view(np.int32)).cuda(), status=ds, shard_len=L)
         codec.sync()
     except Exception:
         pass
+    finally:
+        codec.set_tuning(**old)
     got = dd.cpu().numpy()
     st = ds.cpu().numpy()
     assert np.array_equal(st == 0, st_ref == 0)
