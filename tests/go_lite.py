@@ -14,7 +14,8 @@ would reject in it:
   * assignments, := declarations (including comma-ok forms), returns and composite-literal fields
     agree in count and are assignable; binary operators see identical operand types;
   * `var _ I = &T{}` assertions hold: T's method set (with promotion and pointer receivers)
-    has every method of I with an identical signature.
+    has every method of I with an identical signature;
+  * no local variable is declared and never read, and no import goes unused (Go rejects both).
 
 Types of the reference's own packages (internal/fec, internal/wire, internal/protocol, patched as
 go/patches/*.diff patch them) come from their declarations; packages that are not loaded (the
@@ -188,6 +189,7 @@ class Universe:
         self.cmacros = set()
         self.ctypes = set()  # C typedef names (opaque structs)
         self.bodies = []     # (ctx, FuncDecl) of the files to check
+        self.import_errors = []
         self.decl_sites = {}  # (pkg, name) -> [file:line]
 
     # -- C headers
@@ -246,6 +248,11 @@ class Universe:
         p = DeclParser(self, path, toks, check)
         p.parse_file()
         self.loaded.add(p.ctx.pkg)
+        if check:   # an import no code of the file names is a compile error
+            named_ = {toks[i].text for i in range(len(toks) - 1) if toks[i].kind == "id" and toks[i + 1].text == "."}
+            for alias in p.ctx.imports:
+                if alias not in ("_", ".") and alias not in named_:
+                    self.import_errors.append("%s: imported and not used: %s" % (os.path.basename(path), alias))
         return p.ctx
 
     def underlying(self, t, depth=0):
@@ -669,6 +676,16 @@ STDLIB_TYPES = {("unsafe", "Pointer"), ("runtime", "Pinner"), ("sync", "Once"), 
                 ("sync", "Pool"), ("sync", "RWMutex"), ("bytes", "Reader"), ("io", "Reader")}
 
 
+class Var:
+    __slots__ = ("name", "t", "local", "line", "used")
+
+    def __init__(self, name, t, local, line):
+        self.name, self.t, self.local, self.line, self.used = name, t, local, line, False
+
+
+ASSIGN_OPS = {"=", "+=", "-=", "*=", "/=", "%=", "&=", "|=", "^=", "<<=", ">>=", "&^=", "++", "--", ","}
+
+
 class Checker:
     def __init__(self, uni):
         self.uni = uni
@@ -678,6 +695,7 @@ class Checker:
         self.ctx = None
         self.scopes = []
         self.results = []
+        self.lhs_mode = False   # parsing the left side of an assignment: a bare name there is not a use
 
     def err(self, line, msg):
         self.errors.append("%s:%d: %s" % (os.path.basename(self.ctx.path), line, msg))
@@ -687,11 +705,14 @@ class Checker:
         self.scopes.append({})
 
     def pop(self):
-        self.scopes.pop()
+        for v in self.scopes.pop().values():
+            if v.local and not v.used:
+                self.err(v.line, "declared and not used: %s" % v.name)
 
-    def declare(self, name, t):
+    def declare(self, name, t, local=False, line=0):
+        """local: a variable of := / var / range, which Go requires to be read somewhere."""
         if name != "_":
-            self.scopes[-1][name] = t
+            self.scopes[-1][name] = Var(name, t, local, line)
 
     def lookup_local(self, name):
         for s in reversed(self.scopes):
@@ -966,7 +987,7 @@ class Checker:
         if t.kind == "rune":
             return untyped("rune")
         if t.text == "(":
-            x = self.expr(c)
+            x = self.nested(lambda: self.expr(c))
             c.expect(")")
             return x
         if t.text in ("[", "map", "chan", "struct", "interface"):
@@ -986,7 +1007,9 @@ class Checker:
             return UNKNOWN
         loc = self.lookup_local(name)
         if loc is not None:
-            return loc
+            if not (self.lhs_mode and c.peek().text in ASSIGN_OPS):
+                loc.used = True
+            return loc.t
         pkg = self.ctx.pkg
         if (pkg, name) in self.uni.types:
             return ("typeval", named(pkg, name))
@@ -1071,14 +1094,22 @@ class Checker:
                     x = self.select(self.strip_assert(x), name, t.line)
             elif t.text == "[" and t.kind == "op":
                 c.next()
-                x = self.index(c, self.strip_assert(x), t.line)
+                x = self.nested(lambda: self.index(c, self.strip_assert(x), t.line))
             elif t.text == "(" and t.kind == "op":
                 c.next()
-                x = self.call(c, x, t.line)
+                x = self.nested(lambda: self.call(c, x, t.line))
             elif t.text == "{" and t.kind == "op" and x[0] == "typeval" and not nocomp:
-                x = self.composite(c, x[1])
+                x = self.nested(lambda: self.composite(c, x[1]))
             else:
                 return x
+
+    def nested(self, fn):
+        """Parse inside brackets: names there are read, even on an assignment's left side."""
+        saved, self.lhs_mode = self.lhs_mode, False
+        try:
+            return fn()
+        finally:
+            self.lhs_mode = saved
 
     @staticmethod
     def strip_assert(x):
@@ -1426,7 +1457,7 @@ class Checker:
             vt = types[i] if i < len(types) else UNKNOWN
             if ty is not None and vals and not self.assignable(vt, ty):
                 self.err(c.peek().line, "cannot use %s as %s in variable declaration" % (fmt_type(vt), fmt_type(ty)))
-            self.declare(n, ty if ty is not None else self.default_type(vt))
+            self.declare(n, ty if ty is not None else self.default_type(vt), local=True, line=c.peek().line)
 
     def default_type(self, t):
         if t[0] == "untyped":
@@ -1497,12 +1528,12 @@ class Checker:
             for n, vt in zip(names, types):
                 prev = self.scopes[-1].get(n)
                 if prev is not None and n != "_":
-                    if not self.assignable(vt, prev):
-                        self.err(line, "cannot assign %s to %s (type %s)" % (fmt_type(vt), n, fmt_type(prev)))
+                    if not self.assignable(vt, prev.t):
+                        self.err(line, "cannot assign %s to %s (type %s)" % (fmt_type(vt), n, fmt_type(prev.t)))
                     continue
                 if n != "_":
                     new = True
-                self.declare(n, self.default_type(vt))
+                self.declare(n, self.default_type(vt), local=True, line=line)
             if not new and any(n != "_" for n in names):
                 self.err(line, "no new variables on left side of :=")
             return
@@ -1510,7 +1541,11 @@ class Checker:
             c.next()
             self.expr(c, nocomp=header)
             return
-        lhs = self.expr_list(c, nocomp=header)
+        self.lhs_mode = True
+        try:
+            lhs = self.expr_list(c, nocomp=header)
+        finally:
+            self.lhs_mode = False
         t = c.peek()
         if t.kind == "op" and (t.text == "=" or (t.text.endswith("=") and t.text not in ("==", "!=", "<=", ">=", ":="))):
             c.next()
@@ -1556,7 +1591,7 @@ class Checker:
         if len(names) > len(kv):
             self.err(line, "range over %s permits only %d iteration variable(s)" % (fmt_type(x), len(kv)))
         for n, t in zip(names, kv):
-            self.declare(n, t)
+            self.declare(n, t, local=True, line=line)
 
     def header(self, c):
         """if / switch header: [simple ';'] [expr]; the cursor stops at '{'."""
@@ -1727,6 +1762,7 @@ class Checker:
                 self.err(line, msg)
             elif not self.assignable(v, ty):
                 self.err(line, "cannot use %s as %s" % (fmt_type(v), fmt_type(ty)))
+        self.errors.extend(self.uni.import_errors)
         return self.errors
 
 

@@ -11,8 +11,8 @@ What a compiler would reject and the checker catches (each seeded below, on a co
 to prove it does): an unknown field or method, an undefined identifier, a cgo argument of the
 wrong C type (int for C.int, *C.uint32_t for *C.size_t, ...), a wrong argument or return count,
 an assignment count mismatch, a struct literal field that does not exist, mismatched operand
-types, a type that no longer satisfies an interface it is asserted to implement, and a name
-declared twice in one build configuration. Reads /root/reference (skipped where it is absent)."""
+types, a type that no longer satisfies an interface it is asserted to implement, a local declared
+and never read, an unused import, and a name declared twice in one build configuration. Reads /root/reference (skipped where it is absent)."""
 import os
 import re
 import shutil
@@ -133,14 +133,13 @@ def patched_quic(patched, tmp_path_factory):
     return str(root), added
 
 
-def check_quic(patched, patched_quic, overrides=None):
+def check_quic(patched, patched_quic, overrides=None, fechip=True):
     """The functions of package quic the hooks add or change, against package quic's own
-    declarations and internal/fec with the drop-in (tags fechip)."""
+    declarations and internal/fec with the drop-in (either build configuration)."""
     qdir, added = patched_quic
     files = _pkg_files(os.path.join(patched, "internal", "wire")) + \
         _pkg_files(os.path.join(patched, "internal", "protocol")) + \
-        _pkg_files(os.path.join(patched, "internal", "fec")) + [
-            (p, s) for p, s in _ours(True) if not p.endswith("hip_stub.go")]
+        _pkg_files(os.path.join(patched, "internal", "fec")) + _ours(fechip)
     quic = _pkg_files(qdir)
     uni = go_lite.Universe()
     uni.assertions = []
@@ -161,8 +160,9 @@ def check_quic(patched, patched_quic, overrides=None):
 
 
 @needs_ref
-def test_quic_hooks_type_check(patched, patched_quic):
-    errors, stats, funcs = check_quic(patched, patched_quic)
+@pytest.mark.parametrize("fechip", [True, False], ids=["tags_fechip", "default_build"])
+def test_quic_hooks_type_check(patched, patched_quic, fechip):
+    errors, stats, funcs = check_quic(patched, patched_quic, fechip=fechip)
     assert not errors, "\n".join(errors)
     for fn in ("handleRecoveredFEC", "closeFEC", "pollRepairFrames", "fecSourcePayloadBuffer", "Room", "run"):
         assert fn in funcs, funcs
@@ -250,6 +250,13 @@ SEEDED = [
      "m.relase = append(m.release, f.Payload)\n\t\t}\n\t\treturn nil, nil", "has no field or method relase"),
     ("xor_hip.go", "payloadLen := uint16(rec[big])<<8 | uint16(rec[big+1])",
      "payloadLen := uint16(rec[bigg])<<8 | uint16(rec[big+1])", "undefined: bigg"),
+    ("batch_hip.go", "\tn := 0\n\tadd := func(p []byte) {", "\tn := 0\n\tunused := 3\n\tadd := func(p []byte) {",
+     "declared and not used: unused"),
+    ("reed_solomon_hip.go", "\t\tshard, err := rs.addLengthToSourceSymbolPayload(b, ssid)\n\t\tif err != nil {\n\t\t\treturn nil, err\n\t\t}\n\t\tcopy(buf[i*L:(i+1)*L], shard)\n\t\tmask",
+     "\t\tshard, err := rs.addLengthToSourceSymbolPayload(b, ssid)\n\t\tif err != nil {\n\t\t\treturn nil, err\n\t\t}\n\t\tshard = nil\n\t\tmask",
+     "declared and not used: shard"),
+    ("packet_pool_hip.go", '\t"sync"\n\t"unsafe"\n', '\t"sync"\n\t"strings"\n\t"unsafe"\n',
+     "imported and not used: strings"),
 ]
 
 
