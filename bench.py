@@ -180,6 +180,19 @@ def host_threads():
         return os.cpu_count() or 1
 
 
+def oracle_spot_check(k, m, sample):
+    """cpu_baseline leg, the checker half: the parity of 64 blocks the device encoded equals the
+    CPU oracle's (oracle/oracle.py, the reference's buildMatrix and mulTable restated)."""
+    try:
+        import numpy as np
+        from oracle import oracle as orc
+        want = sample[:, :, :SHARD_LEN].copy()
+        orc.rs_encode(k, m, want)
+        return bool(np.array_equal(sample[:, :, :SHARD_LEN], want))
+    except Exception as exc:  # oracle unavailable: report, do not hide
+        return "unchecked: %s" % exc
+
+
 def cpu_baseline(k, m, blocks, seed, budget_s=12.0):
     """The CPU restatement of klauspost's kernels (oracle/fec_simd.c: AVX2 PSHUFB nibble tables,
     GFNI affine forms; the method the reference's calls at reed_solomon.go:51,124 run on x86),
@@ -319,7 +332,7 @@ def host_resident(torch, fec, codec, k, m, blocks, seed, reps=3):
                      "ms_per_step": round(best * 1e3, 2), "pcie_GBps": round(out["pcie_bytes_per_step"] / best / 1e9, 2),
                      "up_GBps": round(up_bytes / best / 1e9, 2), "down_GBps": round(down_bytes / best / 1e9, 2),
                      "frac_of_probe": round(bound_s / best, 4),
-                     "check": ok and bool(np.array_equal(pnp[:64], oracle_parity(k, m, src[:64])))}
+                     "check": ok and bool(np.array_equal(pnp[:64], device_parity(torch, fec, codec, k, m, src[:64])))}
     return out
 
 
@@ -362,14 +375,18 @@ def box_probe(torch, codec, b, step, stream, enc_bytes, dec_bytes, rounds=5, bur
     return out
 
 
-def oracle_parity(k, m, data):
-    """Parity of host data blocks [B, k, L] by the CPU oracle (checker only)."""
-    import numpy as np
-    from oracle import oracle as orc
-    sh = np.zeros((data.shape[0], k + m, data.shape[2]), dtype=np.uint8)
-    sh[:, :k] = data
-    orc.rs_encode(k, m, sh)
-    return sh[:, k:]
+def device_parity(torch, fec, codec, k, m, data):
+    """Parity of host data blocks [B, k, L] by the device-resident encode (FEC_DEVICE, the kernel
+    the oracle checks in tests/ and in the cpu_baseline leg): the host-resident forms must give
+    the same bytes."""
+    b, _, ln = data.shape
+    st = (ln + 15) // 16 * 16
+    d = torch.zeros((b, k, st), dtype=torch.uint8, device="cuda")
+    d[:, :, :ln] = torch.from_numpy(data).cuda()
+    p = torch.zeros((b, m, st), dtype=torch.uint8, device="cuda")
+    codec.rs_encode_raw(k, m, ln, b, d.data_ptr(), k * st, p.data_ptr(), m * st, st, fec.FEC_DEVICE)
+    codec.sync()
+    return p[:, :, :ln].cpu().numpy()
 
 
 def free_port():
@@ -491,19 +508,13 @@ def main():
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok_roundtrip = bool(okt.item())
 
-    # encode parity spot-check against the CPU oracle on 64 random blocks (rank 0)
-    ok_parity = None
+    # 64 random blocks (data + parity) for the oracle spot-check, which runs in the cpu_baseline
+    # leg (N = 1, rank 0): the only part of bench.py that touches oracle/
+    ok_parity = "not run: the oracle spot-check is part of the N = 1 cpu_baseline leg"
+    parity_sample = None
     if rank == 0:
-        try:
-            import numpy as np
-            from oracle import oracle as orc
-            pick = torch.randperm(B, device=dev)[:64]
-            sample = torch.cat([batch.data[pick], batch.parity[pick]], dim=1).cpu().numpy()
-            want = sample[:, :, :SHARD_LEN].copy()
-            orc.rs_encode(k, m, want)
-            ok_parity = bool(np.array_equal(sample[:, :, :SHARD_LEN], want))
-        except Exception as exc:  # oracle unavailable: report, do not hide
-            ok_parity = "unchecked: %s" % exc
+        pick = torch.randperm(B, device=dev)[:64]
+        parity_sample = torch.cat([batch.data[pick], batch.parity[pick]], dim=1).cpu().numpy()
 
     L = SHARD_LEN
     enc_bytes = B * (k + m) * L                  # read k shards, write m shards
@@ -583,6 +594,7 @@ def main():
             torch.cuda.empty_cache()
             out["host_resident"] = host_resident(torch, fec, codec, k, m, args.host_blocks, args.seed)
         if world == 1 and not args.no_cpu_baseline:
+            out["check"]["encode_vs_oracle_64_blocks"] = oracle_spot_check(k, m, parity_sample)
             out["cpu_baseline"] = cpu_baseline(k, m, args.cpu_sample_blocks, args.seed)
         print(json.dumps(out), flush=True)
     codec.close()
