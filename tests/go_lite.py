@@ -15,7 +15,9 @@ would reject in it:
     agree in count and are assignable; binary operators see identical operand types;
   * `var _ I = &T{}` assertions hold: T's method set (with promotion and pointer receivers)
     has every method of I with an identical signature;
-  * no local variable is declared and never read, and no import goes unused (Go rejects both).
+  * no local variable is declared and never read, and no import goes unused (Go rejects both);
+  * every function with results ends in a terminating statement (Go's "missing return"), and if
+    conditions are boolean.
 
 Types of the reference's own packages (internal/fec, internal/wire, internal/protocol, patched as
 go/patches/*.diff patch them) come from their declarations; packages that are not loaded (the
@@ -696,6 +698,7 @@ class Checker:
         self.scopes = []
         self.results = []
         self.lhs_mode = False   # parsing the left side of an assignment: a bare name there is not a use
+        self.breaks = []        # per enclosing for / switch / select: [saw a break]; None: a function boundary
 
     def err(self, line, msg):
         self.errors.append("%s:%d: %s" % (os.path.basename(self.ctx.path), line, msg))
@@ -1326,19 +1329,30 @@ class Checker:
             if n:
                 self.declare(n, t)
         self.results.append(results)
-        self.block(c)
+        self.breaks.append(None)   # a function literal's body is no loop of the enclosing function
+        line = c.peek().line
+        term = self.block(c)
+        self.breaks.pop()
+        if results and not term:
+            self.err(line, "missing return")
         self.results.pop()
         self.pop()
 
     def block(self, c):
+        """Returns whether the block is a terminating statement (its last statement is)."""
         c.expect("{")
         self.push()
+        term = False
         while not c.at("}"):
             if c.peek().kind == "eof":
                 raise GoError("unterminated block")
-            self.stmt(c)
+            if c.at(";"):
+                c.next()
+                continue
+            term = self.stmt(c)
         c.expect("}")
         self.pop()
+        return term
 
     def sync(self, c):
         depth = 0
@@ -1360,12 +1374,13 @@ class Checker:
         self.stats["stmts"] += 1
         start = c.i
         try:
-            self._stmt(c)
+            return bool(self._stmt(c))
         except GoError as e:
             self.err(c.toks[start].line, "cannot check statement: %s" % e)
             c.i = start
             c.next()
             self.sync(c)
+            return True   # unknown: no second report
 
     def _end(self, c):
         if not (c.accept(";") or c.at("}")):
@@ -1379,9 +1394,9 @@ class Checker:
             c.next()
             return
         if k == "{":
-            self.block(c)
+            term = self.block(c)
             c.accept(";")
-            return
+            return term
         if k == "var":
             c.next()
             if c.accept("("):
@@ -1399,17 +1414,13 @@ class Checker:
             self._end(c)
             return
         if k == "if":
-            self.if_stmt(c)
-            return
+            return self.if_stmt(c)
         if k == "for":
-            self.for_stmt(c)
-            return
+            return self.for_stmt(c)
         if k == "switch":
-            self.switch_stmt(c)
-            return
+            return self.switch_stmt(c)
         if k == "select":
-            self.select_stmt(c)
-            return
+            return self.select_stmt(c)
         if k == "return":
             c.next()
             vals = []
@@ -1417,7 +1428,7 @@ class Checker:
                 vals = self.expr_list(c)
             self.check_return(vals, t.line)
             self._end(c)
-            return
+            return True
         if k in ("defer", "go"):
             c.next()
             self.expr(c)
@@ -1425,16 +1436,25 @@ class Checker:
             return
         if k in ("break", "continue", "goto", "fallthrough"):
             c.next()
-            if c.peek().kind == "id":
+            labeled = c.peek().kind == "id"
+            if labeled:
                 c.next()
+            if k == "break":   # the loop / switch it leaves is not terminating (a label: the innermost, conservatively)
+                for i in range(len(self.breaks) - 1, -1, -1):
+                    if self.breaks[i] is None:
+                        break
+                    self.breaks[i][0] = True
+                    break
             self._end(c)
-            return
+            return k in ("goto", "fallthrough")
         if t.kind == "id" and c.at(":", 1) and not c.at("=", 1):
             c.next()
             c.next()
             return
+        is_panic = t.text == "panic" and c.at("(", 1) and self.lookup_local("panic") is None
         self.simple(c)
         self._end(c)
+        return is_panic
 
     def expr_list(self, c, nocomp=False):
         out = [self.expr(c, nocomp)]
@@ -1645,20 +1665,30 @@ class Checker:
     def if_stmt(self, c):
         c.expect("if")
         self.push()
-        self.header(c)
-        self.block(c)
+        line = c.peek().line
+        cond = self.header(c)
+        if cond is not None and cond != UNKNOWN and cond[0] != "?":
+            u = self.uni.underlying(cond) if cond[0] != "untyped" else cond
+            if u not in (named("", "bool"), untyped("bool")) and self.known(cond):
+                self.err(line, "non-boolean condition in if statement (%s)" % fmt_type(cond))
+        term = self.block(c)
         if c.accept("else"):
             if c.at("if"):
-                self.if_stmt(c)
+                t2 = self.if_stmt(c)
                 self.pop()
-                return
-            self.block(c)
+                return term and t2
+            t2 = self.block(c)
+            self.pop()
+            c.accept(";")
+            return term and t2
         self.pop()
         c.accept(";")
+        return False
 
     def for_stmt(self, c):
         line = c.expect("for").line
         self.push()
+        forever = c.at("{")
         if not c.at("{"):
             j, depth, semis = c.i, 0, 0
             while True:
@@ -1684,15 +1714,20 @@ class Checker:
             else:
                 self.simple(c, header=True)
         del line
+        self.breaks.append([False])
         self.block(c)
+        broke = self.breaks.pop()[0]
         self.pop()
         c.accept(";")
+        return forever and not broke
 
     def switch_stmt(self, c):
         c.expect("switch")
         self.push()
         tag = self.header(c)
         c.expect("{")
+        has_default, all_term = False, True
+        self.breaks.append([False])
         while not c.accept("}"):
             if c.accept("case"):
                 vals = self.expr_list(c)
@@ -1702,17 +1737,27 @@ class Checker:
                             self.err(c.peek().line, "invalid case: mismatched types %s and %s" % (fmt_type(v), fmt_type(tag)))
             else:
                 c.expect("default")
+                has_default = True
             c.expect(":")
             self.push()
+            term = False
             while not (c.at("case") or c.at("default") or c.at("}")):
-                self.stmt(c)
+                if c.at(";"):
+                    c.next()
+                    continue
+                term = self.stmt(c)
+            all_term = all_term and term
             self.pop()
+        broke = self.breaks.pop()[0]
         self.pop()
         c.accept(";")
+        return has_default and all_term and not broke
 
     def select_stmt(self, c):
         c.expect("select")
         c.expect("{")
+        all_term = True
+        self.breaks.append([False])
         while not c.accept("}"):
             self.push()
             if c.accept("case"):
@@ -1720,10 +1765,17 @@ class Checker:
             else:
                 c.expect("default")
             c.expect(":")
+            term = False
             while not (c.at("case") or c.at("default") or c.at("}")):
-                self.stmt(c)
+                if c.at(";"):
+                    c.next()
+                    continue
+                term = self.stmt(c)
+            all_term = all_term and term
             self.pop()
+        broke = self.breaks.pop()[0]
         c.accept(";")
+        return all_term and not broke
 
     def check_return(self, vals, line):
         want = self.results[-1] if self.results else []

@@ -12,7 +12,8 @@ to prove it does): an unknown field or method, an undefined identifier, a cgo ar
 wrong C type (int for C.int, *C.uint32_t for *C.size_t, ...), a wrong argument or return count,
 an assignment count mismatch, a struct literal field that does not exist, mismatched operand
 types, a type that no longer satisfies an interface it is asserted to implement, a local declared
-and never read, an unused import, and a name declared twice in one build configuration. Reads /root/reference (skipped where it is absent)."""
+and never read, an unused import, a missing return, a non-boolean condition, and a name declared
+twice in one build configuration. Reads /root/reference (skipped where it is absent)."""
 import os
 import re
 import shutil
@@ -257,6 +258,10 @@ SEEDED = [
      "declared and not used: shard"),
     ("packet_pool_hip.go", '\t"sync"\n\t"unsafe"\n', '\t"sync"\n\t"strings"\n\t"unsafe"\n',
      "imported and not used: strings"),
+    ("hip_cgo.go", 'os.Getenv("FEC_HIP_DEVICE")); err == nil {\n\t\treturn v\n\t}\n\treturn 0\n}',
+     'os.Getenv("FEC_HIP_DEVICE")); err == nil {\n\t\treturn v\n\t}\n}', "missing return"),
+    ("packet_pool_hip.go", "\tif len(pp.free) == 0 {\n\t\treturn nil", "\tif len(pp.free) {\n\t\treturn nil",
+     "non-boolean condition in if statement (int)"),
 ]
 
 
