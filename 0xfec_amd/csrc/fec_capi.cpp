@@ -10,10 +10,12 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
 #include <map>
+#include <memory>
 #include <thread>
 #include <utility>
 #include <vector>
@@ -1384,6 +1386,41 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
     *slot = value;
     memset(ctx->grid_cache, 0, sizeof(ctx->grid_cache));
     return old;
+}
+
+// Internal self-test (not part of the public ABI, no device needed): parallel_for covers [0, n)
+// exactly once on the persistent copy workers and on threads made per call, for sizes around
+// the part boundaries and part counts 2..16, with four threads calling at once (one holds the
+// workers, the others find them busy and make their own). 0 on success, else the failing case.
+extern "C" int fec__selftest_copypool(void) {
+    const fk::Tuning saved = fk::g_tune;
+    int fail = 0;
+    const size_t sizes[] = {511, 512, 513, 1000, 4097, 65536, 100003};
+    for (int pool = 0; pool <= 1 && !fail; ++pool)
+        for (int T : {2, 3, 8, 16}) {
+            fk::g_tune.host_pool = pool;
+            fk::g_tune.host_threads = T;
+            std::vector<std::thread> callers;
+            std::vector<int> bad(4, 0);
+            for (int t = 0; t < 4; ++t)
+                callers.emplace_back([&, t] {
+                    for (size_t n : sizes) {
+                        std::unique_ptr<std::atomic<uint32_t>[]> hits(new std::atomic<uint32_t>[n]);
+                        for (size_t i = 0; i < n; ++i) hits[i].store(0);
+                        parallel_for(n, [&](size_t lo, size_t hi) {
+                            for (size_t i = lo; i < hi; ++i) hits[i].fetch_add(1);
+                        });
+                        for (size_t i = 0; i < n; ++i)
+                            if (hits[i].load() != 1) bad[t] = 1;
+                    }
+                });
+            for (auto& th : callers) th.join();
+            for (int b : bad)
+                if (b) fail = 1 + pool * 100 + T;
+            if (fail) break;
+        }
+    fk::g_tune = saved;
+    return fail;
 }
 
 // Internal self-test (not part of the public ABI, no device needed): the lane-arithmetic PermTab

@@ -72,3 +72,12 @@ def test_lane_permtab_builder_matches_bytewise(fec):
     # builder for all 256 coefficients
     lib = ctypes.CDLL(fec._LIB_PATH)
     assert lib.fec__selftest_permtab() == 0
+
+
+def test_copy_workers_cover_every_index_once(fec):
+    # FEC_HOST's staging / scatter copies run through parallel_for on persistent copy workers
+    # (fec_capi.cpp CopyPool) or on threads made per call: every index exactly once, for sizes
+    # around the part boundaries, 2..16 parts, four callers at once (no device needed; the
+    # sanitized CPU run repeats it under ASan / UBSan)
+    lib = ctypes.CDLL(fec._LIB_PATH)
+    assert lib.fec__selftest_copypool() == 0
