@@ -179,6 +179,8 @@ struct Tuning {
     int host_chunk = 0;       // host-resident path: blocks per staging chunk (0: 128 MiB worth)
     int host_threads = 8;     // FEC_HOST (pageable): host threads for the staging / scatter copies
     int host_pool = 1;        // FEC_HOST copies on persistent workers (fec_capi.cpp CopyPool); 0: per call
+    int dec_rwin = 4;         // plan form 5 (rank-first, dec_pv 5): sort window in units of 64 blocks (1..8).
+                              // r04t: level with form 3 at 64-128 blocks, 0.8-2 % slower at 256-512 (not default)
     int xor_fix2 = 0;         // XOR(2,1) reconstruct by its own one-item-per-lane kernel (fec_xor.hip). r04m,
                               // three interleaved rounds: 0.6443 vs 0.6395 ms for the generic kernel (-0.7 %):
                               // the gap to the XOR twin (0.955) is the in-place write, not the loop. Off

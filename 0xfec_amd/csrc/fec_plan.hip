@@ -34,7 +34,8 @@ constexpr uint32_t kV2Exp = 0, kV2Log = 768, kV2Log32 = 1024, kV2Tables = 1152;
 constexpr uint32_t kRankBins = 33;   // erasure counts 0..32
 // recs: the records of `win` segments of `groups` blocks, sorted together (sort window)
 __host__ __device__ inline SortLds sort_lds(uint32_t m, uint32_t k, uint32_t groups, uint32_t stride,
-                                            uint32_t win = 1, bool v2 = false, uint32_t gscratch = kGroupScratch) {
+                                            uint32_t win = 1, bool v2 = false, uint32_t gscratch = kGroupScratch,
+                                            uint32_t rec_segs = 0) {
     SortLds l;
     l.prows = v2 ? kV2Tables : 768;
     l.dall = l.prows + (size_t)m * k;
@@ -43,7 +44,7 @@ __host__ __device__ inline SortLds sort_lds(uint32_t m, uint32_t k, uint32_t gro
     // ranking scratch: per wave of records and bin, a count (then its prefix), and per bin a start
     l.rank = l.pos + (size_t)groups * win * 4;
     l.recs = (l.rank + ((size_t)(groups * win + 63) / 64 + 1) * kRankBins * 4 + 15) & ~(size_t)15;
-    l.total = l.recs + (size_t)groups * win * stride;
+    l.total = l.recs + (size_t)groups * (rec_segs ? rec_segs : win) * stride;   // rank-first: one segment
     return l;
 }
 
@@ -108,6 +109,62 @@ __device__ __forceinline__ void sort_window_out(const PlanArgs& a, uint8_t* smem
         const uint32_t r = i / per, q = i - r * per;
         dst[(size_t)s_pos[r] * per + q] = src[i];
     }
+}
+
+// Rank-first form (knob dec_pv 5): a record's storage position depends only on its block's
+// output count, which the mask alone gives (the erased data shards; 0 for a block with too few
+// shards or more erasures than output slots, as the plan itself decides). So the window is ranked
+// from the masks before any record exists, and each record goes straight from a one-segment LDS
+// slot to its position: no window of records in LDS (15-61 KB per workgroup at 64-256 blocks),
+// no copy-out pass, and windows as large as the rebuild likes. The order is sort_window_out's:
+// output count descending, then block order; blocks past the batch take no position.
+// s_pos[t] = position in the window of block wbase + t, t < nw. Workgroup-wide (barriers inside).
+template <uint32_t K, uint32_t M>
+__device__ __forceinline__ void rank_window_masks(const PlanArgs& a, uint8_t* smem, const SortLds& L, uint32_t nw,
+                                                  uint32_t wbase) {
+    constexpr uint32_t N = K + M, U = M + 1;
+    constexpr uint32_t all = N >= 32 ? 0xFFFFFFFFu : (1u << N) - 1u, kmask = (1u << K) - 1u;
+    uint32_t* s_pos = reinterpret_cast<uint32_t*>(smem + L.pos);
+    const uint32_t nwv = (nw + 63) / 64;
+    uint32_t* wc = reinterpret_cast<uint32_t*>(smem + L.rank);   // [nwv][U], then start[U]
+    uint32_t* start = wc + nwv * U;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    __syncthreads();   // the previous window's positions are no longer read
+    for (uint32_t t = threadIdx.x; t < nwv * 64; t += kPlanSortThreads) {   // wave-uniform bound
+        uint32_t v = kRankBins;
+        if (t < nw && wbase + t < a.nblocks) {
+            const uint32_t mask = a.masks[wbase + t] & all;
+            const uint32_t e = K - __popc(mask & kmask);
+            v = ((uint32_t)__popc(mask) < K || (a.max_out && e > a.max_out)) ? 0u : e;
+        }
+        uint32_t rin = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint64_t bm = __ballot(v == u);
+            if (v == u) rin = (uint32_t)__popcll(bm & lt);
+            if (lane == 0) wc[(t >> 6) * U + u] = (uint32_t)__popcll(bm);
+        }
+        if (t < nw) s_pos[t] = rin | (v << 16);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (uint32_t u = U; u-- > 0;) {
+            start[u] = acc;
+            for (uint32_t w = 0; w < nwv; ++w) {
+                const uint32_t c = wc[w * U + u];
+                wc[w * U + u] = acc;
+                acc += c;
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < nw; t += kPlanSortThreads) {
+        const uint32_t pv = s_pos[t], v = pv >> 16;
+        s_pos[t] = v < U ? (pv & 0xFFFFu) + wc[(t >> 6) * U + v] : 0xFFFFFFFFu;
+    }
+    __syncthreads();
 }
 
 template <uint32_t LPB, bool V2>
@@ -304,15 +361,16 @@ constexpr uint32_t kV3S = 0, kV3X = 32, kV3O = 80, kV3N = 128, kV3D = 176, kGrou
 // H segments (knob dec_pv 4: H = 2) run interleaved in each wave: their fills, sums and coefficient
 // chunks are independent chains the wave issues back to back, so one segment's LDS round trips
 // overlap the other's VALU work (form 3 with H = 1 leaves the SIMD half idle on both pipes)
-template <uint32_t K, uint32_t M, uint32_t H>
+template <uint32_t K, uint32_t M, uint32_t H, bool RF>
 __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_code_kernel(PlanArgs a, uint32_t segs, uint32_t win) {
     constexpr uint32_t N = K + M, LPB = K <= 16 ? 16u : 32u, G = kPlanSortThreads / LPB, MAXE = M;
     static_assert(M < K && M <= 12 && K <= LPB && N <= 32, "complement-sum codes with the scratch above");
     static_assert(H == 1 || H == 2, "one or two segments at a time");
+    static_assert(!RF || H == 1, "rank-first: one segment at a time");
     extern __shared__ __attribute__((aligned(128))) uint8_t smem[];
     if (a.gate && *a.gate != a.gate_want) return;   // the classify kernel picked the direct path
     const PlanLayout lay = a.lay;
-    const SortLds L = sort_lds(M, K, G, lay.stride, win, true, H * kGroupScratch3);
+    const SortLds L = sort_lds(M, K, G, lay.stride, win, true, H * kGroupScratch3, RF ? 1u : 0u);
     const uint8_t* s_exp = smem + kV3Exp;
     const uint8_t* s_log = smem + kV3Log;
     const uint8_t* s_nl = smem + kV3NLog32;
@@ -366,8 +424,12 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_code_kernel(PlanArgs
         const uint32_t base = (seg0 + sg) * G;
         if (base >= a.nblocks) break;   // workgroup-uniform
         const uint32_t wl = sg % win;
-        if (wl == 0) __syncthreads();
-        else wave_sync();
+        if (wl == 0) {
+            __syncthreads();
+            if constexpr (RF) rank_window_masks<K, M>(a, smem, L, win * G, base);
+        } else {
+            wave_sync();
+        }
         uint8_t* P[H];
         uint32_t mask[H], e[H], nout[H];
 #pragma unroll
@@ -379,7 +441,7 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_code_kernel(PlanArgs
             const uint32_t mask_in = mask_next[h];
             const uint32_t bn = b + H * G;
             mask_next[h] = (sg + H + h < segs && bn < a.nblocks) ? a.masks[bn] : 0u;
-            P[h] = smem + L.recs + ((size_t)(wl + h) * G + gb) * lay.stride;
+            P[h] = smem + L.recs + ((size_t)(RF ? 0u : wl + h) * G + gb) * lay.stride;
             mask[h] = valid ? mask_in & all : all;
             e[h] = K - __popc(mask[h] & kmask);
             int32_t st = a.max_out ? (int32_t)e[h] : 0;
@@ -485,26 +547,42 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_code_kernel(PlanArgs
                     if (r0 + j < MAXE && r0 + j < nout[h] && nout[h] >= 2) C[(r0 + j) * K] = (uint8_t)c[j];
             }
         }
+        if constexpr (RF) {
+            // the group's record, from its LDS slot straight to its ranked position
+            wave_sync();
+            const uint32_t b = base + gb;
+            if (b < a.nblocks) {
+                const uint32_t wbase = base - wl * G;
+                const uint32_t per = lay.stride / 16;
+                const uint4* src = reinterpret_cast<const uint4*>(P[0]);
+                uint4* dst = reinterpret_cast<uint4*>(a.plans + (uint64_t)(wbase + reinterpret_cast<const uint32_t*>(
+                                                                     smem + L.pos)[b - wbase]) * lay.stride);
+                for (uint32_t q = gl; q < per; q += LPB) dst[q] = src[q];
+            }
+            continue;
+        }
         const bool last = sg + H >= segs || base + H * G >= a.nblocks;
         if (wl + H < win && !last) continue;   // workgroup-uniform
         sort_window_out(a, smem, L, (wl + H) * G, base - wl * G);
     }
 }
 
-template <uint32_t K, uint32_t M, uint32_t H>
+template <uint32_t K, uint32_t M, uint32_t H, bool RF>
 hipError_t code_launch(const PlanArgs& a, hipStream_t s) {
     constexpr uint32_t LPB = K <= 16 ? 16u : 32u, G = kPlanSortThreads / LPB;
     const uint32_t nseg = (a.nblocks + G - 1) / G;
     if (nseg == 0) return hipSuccess;
     uint32_t segs = g_tune.dec_pseg > 0 ? (uint32_t)g_tune.dec_pseg : std::max<uint32_t>(1, nseg / 4096);
     if (a.gate) segs = 64;
-    segs = std::min<uint32_t>(segs, 64);
-    uint32_t win = std::min<uint32_t>(sort_window(G, g_tune.dec_psort), 64);
+    // rank-first: its own window (knob dec_rwin, in 64-block units), up to 512 blocks
+    const int psort = RF ? std::max(1, g_tune.dec_rwin) : g_tune.dec_psort;
+    uint32_t win = std::min<uint32_t>(sort_window(G, psort), RF ? 512u / G : 64u);
+    segs = std::min<uint32_t>(segs, std::max<uint32_t>(64, win));
     win = (win + H - 1) / H * H;   // a window holds whole groups of H segments
     segs = (segs + win - 1) / win * win;
     const uint32_t grid = (nseg + segs - 1) / segs;
-    const size_t lds = sort_lds(M, K, G, a.lay.stride, win, true, H * kGroupScratch3).total;
-    hipLaunchKernelGGL((rs_plan_code_kernel<K, M, H>), dim3(grid), dim3(kPlanSortThreads), lds, s, a, segs, win);
+    const size_t lds = sort_lds(M, K, G, a.lay.stride, win, true, H * kGroupScratch3, RF ? 1u : 0u).total;
+    hipLaunchKernelGGL((rs_plan_code_kernel<K, M, H, RF>), dim3(grid), dim3(kPlanSortThreads), lds, s, a, segs, win);
     return hipGetLastError();
 }
 
@@ -536,9 +614,11 @@ hipError_t sorted_launch(const PlanArgs& a, hipStream_t s) {
 hipError_t launch_rs_plan_sorted(const PlanArgs& a, hipStream_t s) {
     const int pv = g_tune.dec_pv;
     if (pv >= 3 && a.k == 16 && a.m == 8 && a.maxe == 8)
-        return pv == 4 ? code_launch<16, 8, 2>(a, s) : code_launch<16, 8, 1>(a, s);
+        return pv == 5 ? code_launch<16, 8, 1, true>(a, s)
+             : pv == 4 ? code_launch<16, 8, 2, false>(a, s) : code_launch<16, 8, 1, false>(a, s);
     if (pv >= 3 && a.k == 20 && a.m == 10 && a.maxe == 10)
-        return pv == 4 ? code_launch<20, 10, 2>(a, s) : code_launch<20, 10, 1>(a, s);
+        return pv == 5 ? code_launch<20, 10, 1, true>(a, s)
+             : pv == 4 ? code_launch<20, 10, 2, false>(a, s) : code_launch<20, 10, 1, false>(a, s);
     switch (plan_lanes(a.k)) {
         case 2: return sorted_launch<2>(a, s);
         case 4: return sorted_launch<4>(a, s);

@@ -366,9 +366,11 @@ def test_rs_encode_kernel_variants_match_oracle(codec, oracle, torch, variant, k
 # sums; the rest run form 1), 25 is 23 with the padded rebuild slice (dec_lpad: the wave's two blocks'
 # PermTab rows 32 banks apart), 26 is 23 with plan form 3 (dec_pv 3: RS(16,24) and RS(20,30) by the
 # kernel compiled for the code), 27 and 28 are 23 and 22 with form 3 on two segments at a time (dec_pv
-# 4; 28's one-segment windows grow to the pair)
+# 4; 28's one-segment windows grow to the pair), 29-31 are 23 with the rank-first form (dec_pv 5:
+# windows ranked from the masks, records straight to their positions) over 256-, 64- and 512-block
+# windows
 @pytest.mark.parametrize("wave", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22,
-                                  23, 24, 25, 26, 27, 28])
+                                  23, 24, 25, 26, 27, 28, 29, 30, 31])
 @pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10)])
 # L = 1008 / 1017: shards of 63 / 64 chunks, the edge of the two-block wave slices (rolling window)
 @pytest.mark.parametrize("L", [513, 1008, 1017, 1202, 1436])
@@ -391,9 +393,10 @@ def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, 
                            dec_direct=1 if wave in (7, 13, 14, 15) else 0,
                            dec_direct_big=1 if wave in (13, 14, 15) else 0, dec_gate=1 if wave in (14, 15) else 0,
                            dec_gate_pm=1000 if wave == 15 else 10,
-                           dec_sorted=0 if wave == 8 else 1, dec_fixk={9: 1, 16: 3, 17: 4, 18: 4, 19: 4, 20: 4, 21: 4, 22: 4, 23: 4, 24: 4, 25: 4, 26: 4, 27: 4, 28: 4}.get(wave, 2),
+                           dec_sorted=0 if wave == 8 else 1, dec_fixk={9: 1, 16: 3, 17: 4, 18: 4, 19: 4, 20: 4, 21: 4, 22: 4, 23: 4, 24: 4, 25: 4, 26: 4, 27: 4, 28: 4, 29: 4, 30: 4, 31: 4}.get(wave, 2),
                            dec_win={18: 4, 19: 6}.get(wave, 0), dec_s64=1 if wave == 20 else 0,
-                           dec_psort={21: 4, 22: 0, 24: 0, 28: 0}.get(wave, 1), dec_pv={23: 2, 24: 2, 25: 2, 26: 3, 27: 4, 28: 4}.get(wave, 1),
+                           dec_psort={21: 4, 22: 0, 24: 0, 28: 0}.get(wave, 1), dec_pv={23: 2, 24: 2, 25: 2, 26: 3, 27: 4, 28: 4, 29: 5, 30: 5, 31: 5}.get(wave, 1),
+                           dec_rwin={30: 1, 31: 8}.get(wave, 4),
                            dec_lpad=1 if wave == 25 else 0,
                            dec_tier={10: 1, 11: 2, 12: 4}.get(wave, 0))
     try:
@@ -416,8 +419,8 @@ def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, 
 # The sorted plan kernel's two forms on codes of both sum forms: n - k < k sums over the
 # complement (RS(16,24), RS(20,30), RS(9,10)), n - k >= k over the inputs (RS(4,12), RS(8,16),
 # RS(10,32), RS(1,4)), with 1..min(k, m) data erasures and parity losses mixed in.
-@pytest.mark.parametrize("pv", [1, 2, 3, 4])   # 3, 4: RS(16,24) / RS(20,30) by the compiled-code form (4: two
-# segments at a time), the rest 2
+@pytest.mark.parametrize("pv", [1, 2, 3, 4, 5])   # 3-5: RS(16,24) / RS(20,30) by the compiled-code form (4: two
+# segments at a time, 5: rank-first), the rest 2
 @pytest.mark.parametrize("k,m", [(16, 8), (20, 10), (9, 1), (4, 8), (8, 8), (10, 22), (1, 3)])
 def test_rs_plan_forms_match_oracle(codec, oracle, torch, pv, k, m):
     rng = np.random.default_rng(1000 * k + m + pv)
@@ -445,7 +448,7 @@ def test_rs_plan_forms_match_oracle(codec, oracle, torch, pv, k, m):
 
 # The plan kernels of later sub-batches on a side stream beside the rebuild of earlier ones (knob
 # dec_povl): batches of several sub-batches with a ragged last one, out of place and in place.
-@pytest.mark.parametrize("povl,pv,lpad", [(2, 1, 0), (4, 2, 0), (8, 1, 1), (3, 2, 1), (1, 2, 1), (1, 3, 0), (3, 3, 0), (1, 4, 0), (3, 4, 1)])
+@pytest.mark.parametrize("povl,pv,lpad", [(2, 1, 0), (4, 2, 0), (8, 1, 1), (3, 2, 1), (1, 2, 1), (1, 3, 0), (3, 3, 0), (1, 4, 0), (3, 4, 1), (1, 5, 0), (3, 5, 1)])
 @pytest.mark.parametrize("k,m", [(16, 8), (20, 10)])
 def test_rs_plan_overlap_matches_oracle(codec, oracle, torch, povl, pv, lpad, k, m):
     rng = np.random.default_rng(7 * k + povl + pv)

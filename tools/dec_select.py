@@ -52,7 +52,7 @@ def main():
     dp, pp, op = data.data_ptr(), par.data_ptr(), out.data_ptr()
     # every knob any variant sets, at its default: tune(D) must undo each variant completely
     D = dict(dec_wave=1, dec_fused=0, dec_wpc=0, dec_swz=1, dec_ipl=0, dec_direct=1, dec_nt=3, dir_wpc=-1, dir_nt=-1,
-             dec_fixk=4, dec_sorted=1, dec_pseg=0, dec_tier=0, dec_direct_big=0, dec_gate=0, dec_gate_pm=10, dec_win=0, dec_s64=0, dec_psort=1, dec_pv=3, dec_povl=0, dec_lpad=0)
+             dec_fixk=4, dec_sorted=1, dec_pseg=0, dec_tier=0, dec_direct_big=0, dec_gate=0, dec_gate_pm=10, dec_win=0, dec_s64=0, dec_psort=1, dec_pv=3, dec_povl=0, dec_lpad=0, dec_rwin=4)
     variants = {"direct (default)": D,
                 "direct, PermTab rows by vector load": dict(D, dec_direct=2),
                 "direct noswz": dict(D, dec_swz=0),
@@ -79,6 +79,8 @@ def main():
         variants["plan form 1 (round 3)"] = dict(D, dec_pv=1)
         variants["plan form 2 (runtime code)"] = dict(D, dec_pv=2)
         variants["plan form 3 paired segments"] = dict(D, dec_pv=4)
+        for w in (1, 2, 4, 8):
+            variants["plan rank-first window %d" % (64 * w)] = dict(D, dec_pv=5, dec_rwin=w)
         variants["padded rebuild slice (lpad)"] = dict(D, dec_lpad=1)
         variants["padded rebuild slice (lpad), wpc 3"] = dict(D, dec_lpad=1, dec_wpc=3)
         for ov in (2, 4, 8):

@@ -2,7 +2,7 @@
 """Diagnostics: run the multi-erasure recover of config_bench's mixes (RS(16,24) U{1..8},
 RS(20,30) U{1..10}) with one plan-sort window (knob dec_psort), for rocprofv3 --kernel-trace
 --stats to split the time between the sorted plan kernel and the rebuild.
-usage: plan_sort_probe.py K M MULTI PSORT [iters]"""
+usage: plan_sort_probe.py K M MULTI PSORT [iters] [knob=value ...]"""
 import importlib
 import os
 import sys
@@ -17,7 +17,7 @@ def main():
     fec = importlib.import_module("0xfec_amd")
     B, L, S, n = 1 << 19, 1202, 1216, k + m
     codec = fec.Codec(0).use_torch_stream()
-    codec.set_tuning(dec_psort=psort)
+    codec.set_tuning(dec_psort=psort, **{kv.split("=")[0]: int(kv.split("=")[1]) for kv in sys.argv[6:]})
     g = torch.Generator(device="cuda")
     g.manual_seed(0x0FEC)
     data = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device="cuda", generator=g)
