@@ -20,10 +20,12 @@ would reject in it:
     conditions are boolean.
 
 Types of the reference's own packages (internal/fec, internal/wire, internal/protocol, patched as
-go/patches/*.diff patch them) come from their declarations; packages that are not loaded (the
-standard library beyond a small table, cgo's runtime helpers) give an unknown type, which is
-never reported: the checker errs towards silence, and the tests pin its reach (how many selectors,
-calls and cgo arguments it typed) and its teeth (seeded errors it must report)."""
+go/patches/*.diff patch them) come from their declarations, with type aliases resolved; packages
+that are not loaded (the standard library beyond a small table, cgo's runtime helpers) and type
+parameters of generic code give an unknown type, which is never reported: the checker errs
+towards silence, and the tests pin its reach (how many selectors, calls and cgo arguments it
+typed), its teeth (seeded errors it must report) and its silence (the reference's own packages,
+Go that compiles, check clean)."""
 import os
 import re
 
@@ -192,7 +194,9 @@ class Universe:
         self.ctypes = set()  # C typedef names (opaque structs)
         self.bodies = []     # (ctx, FuncDecl) of the files to check
         self.import_errors = []
+        self.aliases = {}    # (pkg, name) -> the aliased type (type A = B)
         self.decl_sites = {}  # (pkg, name) -> [file:line]
+        self.final = False
 
     # -- C headers
     def load_c_header(self, text):
@@ -277,6 +281,37 @@ class Universe:
     def is_loaded(self, pkg):
         return pkg == "" or pkg in self.loaded
 
+    def canon(self, t, depth=0):
+        """t with every alias replaced by the type it names (type A = B: A and B are identical)."""
+        if depth > 20 or not isinstance(t, tuple) or not t:
+            return t
+        k = t[0]
+        if k == "named":
+            a = self.aliases.get((t[1], t[2]))
+            return self.canon(a, depth + 1) if a is not None else t
+        if k in ("ptr", "slice", "array", "chan", "typeval"):
+            return (k, self.canon(t[1], depth + 1))
+        if k == "map":
+            return (k, self.canon(t[1], depth + 1), self.canon(t[2], depth + 1))
+        if k == "func":
+            return (k, tuple(self.canon(x, depth + 1) for x in t[1]), tuple(self.canon(x, depth + 1) for x in t[2]), t[3])
+        if k == "struct":
+            return (k, tuple((n, self.canon(x, depth + 1), e) for n, x, e in t[1]))
+        if k == "iface":
+            return (k, {n: (self.canon(ft, depth + 1), p) for n, (ft, p) in t[1].items()},
+                    tuple(self.canon(e, depth + 1) for e in t[2]))
+        return t
+
+    def finalize(self):
+        """Resolve aliases through every stored declaration (they may be declared in any file)."""
+        self.types = {k: self.canon(v) for k, v in self.types.items()}
+        self.methods = {k: {n: (self.canon(ft), p) for n, (ft, p) in v.items()} for k, v in self.methods.items()}
+        self.funcs = {k: self.canon(v) for k, v in self.funcs.items()}
+        self.values = {k: (v if v[0] == "lazy" else self.canon(v)) for k, v in self.values.items()}
+        for k in list(self.aliases):
+            self.types[k] = self.canon(self.types[k])
+        self.final = True
+
 
 class FuncDecl:
     def __init__(self, name, recv, ftype, params, results, body, line, end):
@@ -339,7 +374,11 @@ class TypeParser:
     def __init__(self, uni, ctx):
         self.uni, self.ctx = uni, ctx
 
+    tparams = frozenset()
+
     def qualify(self, name):
+        if name in self.tparams:
+            return UNKNOWN   # a type parameter
         if name in BUILTIN_TYPES:
             return named("", name)
         return named(self.ctx.pkg, name)
@@ -400,7 +439,7 @@ class TypeParser:
             if c.at("[") and not c.at("]", 1):   # generic instantiation: not tracked
                 c.skip_balanced()
                 return UNKNOWN
-            return r
+            return self.uni.canon(r) if self.uni.final else r
         raise GoError("line %d: expected type, got %r" % (t.line, t.text))
 
     def parse_params(self, c):
@@ -580,9 +619,10 @@ class DeclParser(TypeParser):
                 c.skip_balanced()   # type parameters
             alias = c.accept("=")
             ty = self.parse_type(c)
+            if alias:
+                self.uni.aliases[(self.ctx.pkg, name)] = ty
             self.uni.types[(self.ctx.pkg, name)] = ty
             self._site(name, line)
-            del alias
             return None
         names = [c.ident()]
         while c.accept(","):
@@ -627,15 +667,29 @@ class DeclParser(TypeParser):
         line = c.next().line
         recv = None
         rparams = []
+        rtp = frozenset()
         if c.at("("):
+            s0 = c.i
+            c.skip_balanced()
+            rt = c.toks[s0:c.i]
+            c.i = s0
+            # type parameters of a generic receiver (m *T[K, V]): the names inside its brackets
+            if any(t.text == "[" for t in rt):
+                b0 = next(i for i, t in enumerate(rt) if t.text == "[")
+                rtp = frozenset(t.text for t in rt[b0:] if t.kind == "id")
             rparams, _ = self.parse_params(c)
             rt = rparams[0][1] if rparams else UNKNOWN
             ptr = rt[0] == "ptr"
             base = rt[1] if ptr else rt
             recv = (base, ptr)
         name = c.ident()
-        if c.at("["):
-            c.skip_balanced()   # type parameters
+        self.tparams = rtp
+        if c.at("["):   # type parameters: unknown types inside the signature and the body
+            s0 = c.i
+            c.skip_balanced()
+            tp = c.toks[s0:c.i]
+            self.tparams = rtp | frozenset(tp[i].text for i in range(1, len(tp) - 1)
+                                           if tp[i].kind == "id" and tp[i - 1].text in ("[", ","))
         ft, params, results = self.parse_signature(c)
         body = None
         if c.at("{"):
@@ -654,7 +708,9 @@ class DeclParser(TypeParser):
             if self.check is True or any(line <= ln <= end for ln in self.check):
                 fd = FuncDecl(name, (rparams[0] if rparams else None), ft, params, results,
                               Cursor(c.toks, body[0]), line, end)
+                fd.tparams = self.tparams
                 self.uni.bodies.append((self.ctx, fd))
+        self.tparams = frozenset()
 
 
 Universe.assertions = None  # set per instance in load_universe
@@ -663,8 +719,8 @@ Universe.assertions = None  # set per instance in load_universe
 # ----------------------------------------------------------------------------- checking
 
 STDLIB = {
-    ("fmt", "Errorf"): ("func", (named("", "string"),), (named("", "error"),), True),
-    ("fmt", "Sprintf"): ("func", (named("", "string"),), (named("", "string"),), True),
+    ("fmt", "Errorf"): ("func", (named("", "string"), ("slice", named("", "any"))), (named("", "error"),), True),
+    ("fmt", "Sprintf"): ("func", (named("", "string"), ("slice", named("", "any"))), (named("", "string"),), True),
     ("errors", "New"): ("func", (named("", "string"),), (named("", "error"),), False),
     ("os", "Getenv"): ("func", (named("", "string"),), (named("", "string"),), False),
     ("strconv", "Atoi"): ("func", (named("", "string"),), (named("", "int"), named("", "error")), False),
@@ -690,7 +746,10 @@ ASSIGN_OPS = {"=", "+=", "-=", "*=", "/=", "%=", "&=", "|=", "^=", "<<=", ">>=",
 
 class Checker:
     def __init__(self, uni):
+        if not uni.final:
+            uni.finalize()
         self.uni = uni
+        self.tparams = frozenset()
         self.errors = []
         self.stats = {"selectors": 0, "selectors_typed": 0, "calls": 0, "calls_typed": 0,
                       "c_args": 0, "c_args_typed": 0, "idents": 0, "assigns_typed": 0, "stmts": 0}
@@ -699,6 +758,11 @@ class Checker:
         self.results = []
         self.lhs_mode = False   # parsing the left side of an assignment: a bare name there is not a use
         self.breaks = []        # per enclosing for / switch / select: [saw a break]; None: a function boundary
+
+    def tp(self):
+        t = TypeParser(self.uni, self.ctx)
+        t.tparams = self.tparams
+        return t
 
     def err(self, line, msg):
         self.errors.append("%s:%d: %s" % (os.path.basename(self.ctx.path), line, msg))
@@ -753,6 +817,8 @@ class Checker:
     def identical(self, a, b):
         if a == UNKNOWN or b == UNKNOWN or a[0] == "?" or b[0] == "?":
             return True
+        if (a[0] == "named" and not self.known(a)) or (b[0] == "named" and not self.known(b)):
+            return True   # a type parameter, or a type of a package not loaded
         if a[0] != b[0]:
             return False
         k = a[0]
@@ -772,7 +838,9 @@ class Checker:
         """A type every part of which is loaded (so a mismatch is a real one)."""
         k = t[0]
         if k == "named":
-            return t[1] in ("", "C", "unsafe") or self.uni.is_loaded(t[1])
+            if t[1] in ("", "C", "unsafe"):
+                return True
+            return self.uni.is_loaded(t[1]) and (t[1], t[2]) in self.uni.types
         if k in ("ptr", "slice", "array", "chan"):
             return self.known(t[1])
         if k == "map":
@@ -834,6 +902,22 @@ class Checker:
                     eb = fty[1] if eptr else fty
                     self._collect_methods(eb, eptr or ptr, out, depth + 1)
 
+    def unknown_embed(self, base, depth):
+        """base (a struct, through embedded fields) embeds a type whose methods are not known."""
+        if depth > 5 or base[0] != "named":
+            return False
+        u = self.uni.underlying(base)
+        if u[0] == "iface":
+            return any(self.uni.underlying(e) == UNKNOWN for e in u[2])
+        if u[0] != "struct":
+            return False
+        for _, fty, emb in u[1]:
+            if emb:
+                eb = fty[1] if fty[0] == "ptr" else fty
+                if self.uni.underlying(eb) == UNKNOWN or self.unknown_embed(eb, depth + 1):
+                    return True
+        return False
+
     def iface_methods(self, u, depth=0):
         out = {name: ft for name, (ft, _) in u[1].items()}
         for e in u[2]:
@@ -854,6 +938,8 @@ class Checker:
         ms = self.method_set(v)
         for name, ft in self.iface_methods(self.uni.underlying(iface)).items():
             if name not in ms:
+                if self.unknown_embed(base, 0):
+                    return None   # maybe promoted from an embedded type of a package not loaded
                 return "%s does not implement %s (missing method %s)" % (fmt_type(v), fmt_type(iface), name)
             if not self.identical(ms[name], ft):
                 return "%s does not implement %s (method %s has type %s, want %s)" % (
@@ -995,9 +1081,9 @@ class Checker:
             return x
         if t.text in ("[", "map", "chan", "struct", "interface"):
             c.i -= 1
-            return ("typeval", TypeParser(self.uni, self.ctx).parse_type(c))
+            return ("typeval", self.tp().parse_type(c))
         if t.text == "func":
-            ft, params, results = TypeParser(self.uni, self.ctx).parse_signature(c)
+            ft, params, results = self.tp().parse_signature(c)
             if c.at("{"):
                 self.func_body(c, params, results, None)
                 return ft
@@ -1008,6 +1094,8 @@ class Checker:
         name = t.text
         if name == "_":
             return UNKNOWN
+        if name in self.tparams:
+            return ("typeval", UNKNOWN)
         loc = self.lookup_local(name)
         if loc is not None:
             if not (self.lhs_mode and c.peek().text in ASSIGN_OPS):
@@ -1015,7 +1103,7 @@ class Checker:
             return loc.t
         pkg = self.ctx.pkg
         if (pkg, name) in self.uni.types:
-            return ("typeval", named(pkg, name))
+            return ("typeval", self.uni.canon(named(pkg, name)))
         if (pkg, name) in self.uni.funcs:
             return self.uni.funcs[(pkg, name)]
         if (pkg, name) in self.uni.values:
@@ -1063,7 +1151,7 @@ class Checker:
         if not self.uni.is_loaded(pkg):
             return UNKNOWN
         if (pkg, sel) in self.uni.types:
-            return ("typeval", named(pkg, sel))
+            return ("typeval", self.uni.canon(named(pkg, sel)))
         if (pkg, sel) in self.uni.funcs:
             return self.uni.funcs[(pkg, sel)]
         if (pkg, sel) in self.uni.values:
@@ -1085,7 +1173,7 @@ class Checker:
                         c.expect(")")
                         x = UNKNOWN
                         continue
-                    ty = TypeParser(self.uni, self.ctx).parse_type(c)
+                    ty = self.tp().parse_type(c)
                     c.expect(")")
                     x = ("assert", ty)
                     continue
@@ -1140,7 +1228,7 @@ class Checker:
         if x == UNKNOWN or x[0] in ("?",):
             return UNKNOWN
         if x[0] == "typeval":
-            return UNKNOWN   # generic instantiation
+            return ("typeval", UNKNOWN)   # generic instantiation: a type, possibly of a composite literal
         u = self.uni.underlying(x)
         if u[0] == "map":
             if lo is not None and not self.assignable(lo, u[1]):
@@ -1237,7 +1325,7 @@ class Checker:
 
     def builtin(self, c, name, line):
         if name in ("make", "new"):
-            ty = TypeParser(self.uni, self.ctx).parse_type(c)
+            ty = self.tp().parse_type(c)
             while c.accept(","):
                 if c.at(")"):
                     break
@@ -1410,7 +1498,13 @@ class Checker:
             return
         if k == "const":
             c.next()
-            self.var_spec(c)
+            if c.accept("("):
+                while not c.accept(")"):
+                    if c.accept(";"):
+                        continue
+                    self.var_spec(c, const=True)
+            else:
+                self.var_spec(c, const=True)
             self._end(c)
             return
         if k == "if":
@@ -1462,13 +1556,13 @@ class Checker:
             out.append(self.expr(c, nocomp))
         return out
 
-    def var_spec(self, c):
+    def var_spec(self, c, const=False):
         names = [c.ident()]
         while c.accept(","):
             names.append(c.ident())
         ty = None
         if not (c.at("=") or c.at(";") or c.at(")") or c.at("}")):
-            ty = TypeParser(self.uni, self.ctx).parse_type(c)
+            ty = self.tp().parse_type(c)
         vals = []
         if c.accept("="):
             vals = self.expr_list(c)
@@ -1477,7 +1571,10 @@ class Checker:
             vt = types[i] if i < len(types) else UNKNOWN
             if ty is not None and vals and not self.assignable(vt, ty):
                 self.err(c.peek().line, "cannot use %s as %s in variable declaration" % (fmt_type(vt), fmt_type(ty)))
-            self.declare(n, ty if ty is not None else self.default_type(vt), local=True, line=c.peek().line)
+            if const:   # a constant keeps its untyped kind; an unused one is no error
+                self.declare(n, ty if ty is not None else vt)
+            else:
+                self.declare(n, ty if ty is not None else self.default_type(vt), local=True, line=c.peek().line)
 
     def default_type(self, t):
         if t[0] == "untyped":
@@ -1784,6 +1881,8 @@ class Checker:
                 self.err(line, "not enough return values: have 0, want %d" % len(want))
             return
         types = vals
+        if len(vals) == 1 and vals[0] == UNKNOWN and len(want) > 1:
+            return   # a call into an unloaded package
         if len(vals) == 1 and vals[0][0] == "tuple":
             types = list(vals[0][1])
         if len(types) != len(want):
@@ -1799,7 +1898,11 @@ class Checker:
         for ctx, fd in self.uni.bodies:
             self.ctx = ctx
             self.scopes = []
-            recv = fd.recv
+            self.tparams = getattr(fd, "tparams", frozenset())
+            cn = self.uni.canon
+            fd.params = [(n, cn(t)) for n, t in fd.params]
+            fd.results = [(n, cn(t)) for n, t in fd.results]
+            recv = fd.recv if fd.recv is None else (fd.recv[0], cn(fd.recv[1]))
             c = fd.body
             try:
                 self.func_body(c, fd.params, fd.results, recv)
@@ -1829,7 +1932,35 @@ def load_universe(headers, packages, check_files):
         uni.load_go(path, src, check=False)
     for path, src in check_files:
         uni.load_go(path, src, check=True)
+    uni.finalize()
     return uni
+
+
+GOOS_SUFFIXES = ("aix", "android", "darwin", "dragonfly", "freebsd", "illumos", "ios", "js", "linux", "netbsd",
+                 "openbsd", "plan9", "solaris", "wasip1", "windows")
+
+
+def build_ok(path, src, tags=("linux", "amd64", "unix", "cgo", "gc")):
+    """Whether a file is in the build for GOOS=linux GOARCH=amd64 (plus tags): its //go:build line
+    (&&, ||, !, parentheses) and its _GOOS / _GOARCH file-name suffixes."""
+    base = os.path.basename(path)[:-3]
+    parts = base.split("_")
+    for p_ in parts[1:]:
+        if p_ in GOOS_SUFFIXES and p_ != "linux":
+            return False
+    m = re.search(r"^//go:build (.+)$", src, re.M)
+    if not m:
+        return True
+    expr = m.group(1).strip()
+    toks = re.findall(r"&&|\|\||!|\(|\)|[\w.]+", expr)
+    py = []
+    for t in toks:
+        py.append({"&&": " and ", "||": " or ", "!": " not ", "(": "(", ")": ")"}.get(t) or
+                  (" True " if (t in tags or t.startswith("go1.")) else " False "))
+    try:
+        return bool(eval("".join(py), {"__builtins__": {}}))
+    except SyntaxError:
+        return True
 
 
 def duplicate_decls(uni, pkg, files):
