@@ -316,6 +316,9 @@ SEEDED = [
      'os.Getenv("FEC_HIP_DEVICE")); err == nil {\n\t\treturn v\n\t}\n}', "missing return"),
     ("packet_pool_hip.go", "\tif len(pp.free) == 0 {\n\t\treturn nil", "\tif len(pp.free) {\n\t\treturn nil",
      "non-boolean condition in if statement (int)"),
+    # the round-3 verdict's example: BatchSender.m of another integer type than maxFrames
+    ("batch_hip.go", "\tscheme  protocol.DecoderFECScheme\n\tk, m    int\n", "\tscheme  protocol.DecoderFECScheme\n\tk, m    C.int\n",
+     "mismatched types int and C.int (operator /)"),
 ]
 
 
