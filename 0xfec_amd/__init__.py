@@ -199,7 +199,7 @@ class Codec:
                    "dec_tier": 32, "dec_direct_big": 33, "dec_gate": 34, "dec_gate_pm": 35,
                    "host_gather": 36, "dec_win": 37, "dec_s64": 38, "dec_psort": 39,
                    "dec_pv": 40, "dec_povl": 41, "dec_lpad": 42, "bat_zc": 43,
-                   "enc_early": 44, "host_threads": 45, "host_pool": 46, "enc_x23": 47, "xor_fix2": 48, "dec_rwin": 49}
+                   "enc_early": 44, "host_threads": 45, "host_pool": 46, "enc_x23": 47, "xor_fix2": 48, "dec_rwin": 49, "dec_pdiag": 50}
 
     def set_tuning(self, **knobs):
         """Set kernel-selection knobs; returns the previous values (pass them back to restore)."""

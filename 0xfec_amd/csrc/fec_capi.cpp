@@ -1380,7 +1380,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
               : key == 43 ? &fk::g_tune.bat_zc
               : key == 44 ? &fk::g_tune.enc_early : key == 45 ? &fk::g_tune.host_threads
               : key == 46 ? &fk::g_tune.host_pool : key == 47 ? &fk::g_tune.enc_x23
-              : key == 48 ? &fk::g_tune.xor_fix2 : key == 49 ? &fk::g_tune.dec_rwin : nullptr;
+              : key == 48 ? &fk::g_tune.xor_fix2 : key == 49 ? &fk::g_tune.dec_rwin
+              : key == 50 ? &fk::g_tune.dec_pdiag : nullptr;
     if (!slot) return FEC_ERR_INVALID_ARG;
     const int old = *slot;
     *slot = value;

@@ -181,6 +181,8 @@ struct Tuning {
     int host_pool = 1;        // FEC_HOST copies on persistent workers (fec_capi.cpp CopyPool); 0: per call
     int dec_rwin = 4;         // plan form 5 (rank-first, dec_pv 5): sort window in units of 64 blocks (1..8).
                               // r04t: level with form 3 at 64-128 blocks, 0.8-2 % slower at 256-512 (not default)
+    int dec_pdiag = 0;        // plan form 3 diagnostics (timing only, wrong plans): bit 0 no coefficient rows,
+                              // bit 1 records copied out as their first 48 bytes (fec_plan.hip)
     int xor_fix2 = 0;         // XOR(2,1) reconstruct by its own one-item-per-lane kernel (fec_xor.hip). r04m,
                               // three interleaved rounds: 0.6443 vs 0.6395 ms for the generic kernel (-0.7 %):
                               // the gap to the XOR twin (0.955) is the in-place write, not the loop. Off

@@ -60,7 +60,7 @@ __host__ __device__ inline uint32_t sort_window(uint32_t groups, int psort) {
 // The window's nw record slots (first block base0) from LDS to their storage order in a.plans:
 // erasure count descending, then block order (stable). Workgroup-wide (barriers inside).
 __device__ __forceinline__ void sort_window_out(const PlanArgs& a, uint8_t* smem, const SortLds& L, uint32_t nw,
-                                                uint32_t base0) {
+                                                uint32_t base0, uint32_t copy16 = 0) {
     const PlanLayout lay = a.lay;
     uint32_t* s_pos = reinterpret_cast<uint32_t*>(smem + L.pos);
     __syncthreads();   // every record of the window written
@@ -102,12 +102,12 @@ __device__ __forceinline__ void sort_window_out(const PlanArgs& a, uint8_t* smem
         s_pos[t] += wc[(t >> 6) * U + v];
     }
     __syncthreads();
-    const uint32_t per = lay.stride / 16;
+    const uint32_t per = lay.stride / 16, cp = copy16 ? min(copy16, per) : per;
     const uint4* src = reinterpret_cast<const uint4*>(smem + L.recs);
     uint4* dst = reinterpret_cast<uint4*>(a.plans + (uint64_t)base0 * lay.stride);
-    for (uint32_t i = threadIdx.x; i < nvalid * per; i += kPlanSortThreads) {
-        const uint32_t r = i / per, q = i - r * per;
-        dst[(size_t)s_pos[r] * per + q] = src[i];
+    for (uint32_t i = threadIdx.x; i < nvalid * cp; i += kPlanSortThreads) {
+        const uint32_t r = i / cp, q = i - r * cp;
+        dst[(size_t)s_pos[r] * per + q] = src[(size_t)r * per + q];
     }
 }
 
@@ -361,8 +361,12 @@ constexpr uint32_t kV3S = 0, kV3X = 32, kV3O = 80, kV3N = 128, kV3D = 176, kGrou
 // H segments (knob dec_pv 4: H = 2) run interleaved in each wave: their fills, sums and coefficient
 // chunks are independent chains the wave issues back to back, so one segment's LDS round trips
 // overlap the other's VALU work (form 3 with H = 1 leaves the SIMD half idle on both pipes)
+// Diagnostics (knob dec_pdiag, timing only: the plans it makes are wrong): bit 0 skips the
+// coefficient rows, bit 1 copies only each record's first 48 bytes (its header and shard lists)
+// out, together what a record without coefficients would cost (tools/plan_sort_probe.py).
 template <uint32_t K, uint32_t M, uint32_t H, bool RF>
-__global__ __launch_bounds__(kPlanSortThreads) void rs_plan_code_kernel(PlanArgs a, uint32_t segs, uint32_t win) {
+__global__ __launch_bounds__(kPlanSortThreads) void rs_plan_code_kernel(PlanArgs a, uint32_t segs, uint32_t win_diag) {
+    const uint32_t win = win_diag & 0xFFFFu, diag = win_diag >> 16;
     constexpr uint32_t N = K + M, LPB = K <= 16 ? 16u : 32u, G = kPlanSortThreads / LPB, MAXE = M;
     static_assert(M < K && M <= 12 && K <= LPB && N <= 32, "complement-sum codes with the scratch above");
     static_assert(H == 1 || H == 2, "one or two segments at a time");
@@ -535,7 +539,7 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_code_kernel(PlanArgs
         for (uint32_t r0 = 0; r0 < MAXE; r0 += 4) {
 #pragma unroll
             for (uint32_t h = 0; h < H; ++h) {
-                if (r0 >= nw[h] || nw[h] < 2 || gl >= K) continue;   // wave-uniform but for gl
+                if (r0 >= nw[h] || nw[h] < 2 || gl >= K || (diag & 1u)) continue;   // wave-uniform but for gl
                 const uint32_t sb = nl_base + ((uint32_t)S[h][gl] ^ copy5), dn = Dn[h][gl];
                 uint32_t c[4];
 #pragma unroll
@@ -563,7 +567,7 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_code_kernel(PlanArgs
         }
         const bool last = sg + H >= segs || base + H * G >= a.nblocks;
         if (wl + H < win && !last) continue;   // workgroup-uniform
-        sort_window_out(a, smem, L, (wl + H) * G, base - wl * G);
+        sort_window_out(a, smem, L, (wl + H) * G, base - wl * G, (diag & 2u) ? 3u : 0u);
     }
 }
 
@@ -582,7 +586,9 @@ hipError_t code_launch(const PlanArgs& a, hipStream_t s) {
     segs = (segs + win - 1) / win * win;
     const uint32_t grid = (nseg + segs - 1) / segs;
     const size_t lds = sort_lds(M, K, G, a.lay.stride, win, true, H * kGroupScratch3, RF ? 1u : 0u).total;
-    hipLaunchKernelGGL((rs_plan_code_kernel<K, M, H, RF>), dim3(grid), dim3(kPlanSortThreads), lds, s, a, segs, win);
+    const uint32_t diag = (uint32_t)(g_tune.dec_pdiag & 3);
+    hipLaunchKernelGGL((rs_plan_code_kernel<K, M, H, RF>), dim3(grid), dim3(kPlanSortThreads), lds, s, a, segs,
+                       win | (diag << 16));
     return hipGetLastError();
 }
 
