@@ -266,10 +266,11 @@ def cpu_baseline(k, m, blocks, seed, budget_s=12.0):
             "scalar_sample": "%d reps, pure-Go mulTable form (oracle/fec_oracle.c)" % sreps}
 
 
-def host_resident(torch, fec, codec, k, m, blocks, seed, reps=3):
+def host_resident(torch, fec, codec, k, m, blocks, seed, reps=6):
     """The path as the reference runs it, from host packet buffers to host packet buffers:
     fec_rs_encode_batch + single-erasure fec_rs_reconstruct_batch on host memory, PCIe copies
-    included (pinned hipMemcpyAsync, two staging sets overlapping chunks). Two forms: buffers the
+    included (pinned hipMemcpyAsync on three streams, three staging sets overlapping chunks); the
+    best of `reps` steps, each ~50-60 ms (a shared host's CPU share comes and goes). Two forms: buffers the
     caller pinned (FEC_HOST_PINNED: direct 2D DMA) and pageable buffers (FEC_HOST: staged by the
     library). Packed host layout, stride = shard length. Reported beside the device-resident
     value, never as it."""
