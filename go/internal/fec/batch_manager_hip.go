@@ -110,6 +110,10 @@ type batchManager struct {
 	// (connection.go:1653), copying what it keeps (stream_frame.go:56-76).
 	rxHeld  map[protocol.BlockID][][]byte
 	release [][]byte
+	// receiver: the destination connection ID of the packet whose REPAIR frame is being handled
+	// (SetRepairDestConnID), and that of each staged block, handed out with its data
+	repairDest protocol.ConnectionID
+	dest       map[protocol.BlockID]protocol.ConnectionID
 }
 
 var (
@@ -134,6 +138,7 @@ func newBatchManager(id protocol.DecoderFECScheme, k, m int, send bool) (*batchM
 		}
 	} else {
 		bm.rx, err = NewBatchReceiver(id, k, m, hipBatchBlocks)
+		bm.dest = make(map[protocol.BlockID]protocol.ConnectionID)
 		if bm.pool = hipPacketPool(); bm.pool != nil {
 			bm.rxHeld = make(map[protocol.BlockID][][]byte)
 			hookWirePayloads(bm.pool)
@@ -327,6 +332,7 @@ func (m *batchManager) HandleRepairFrame(f *wire.RepairFrame) ([]byte, error) {
 		}
 		if staged {
 			m.pending++
+			m.dest[f.Metadata.BlockID] = m.repairDest
 			if pooled { // the device reads these when the batch is coded
 				m.rxHeld[f.Metadata.BlockID] = blockPayloads(bS.block)
 			}
@@ -340,10 +346,15 @@ func (m *batchManager) HandleRepairFrame(f *wire.RepairFrame) ([]byte, error) {
 	return nil, nil
 }
 
+// SetRepairDestConnID: the destination connection ID of the packet whose REPAIR frame the next
+// HandleRepairFrame handles (go/patches/connection.go.diff, before handleRepairFrame).
+func (m *batchManager) SetRepairDestConnID(id protocol.ConnectionID) { m.repairDest = id }
+
 // PollRecovered hands over the block data of finished recoveries in staging order (wait: every
-// staged block). Also starts decoding the staged blocks when no batch is in flight.
-func (m *batchManager) PollRecovered(wait bool) ([][]byte, error) {
-	var out [][]byte
+// staged block), each with the destination connection ID of the packet that staged it. Also
+// starts decoding the staged blocks when no batch is in flight.
+func (m *batchManager) PollRecovered(wait bool) ([]RecoveredBlock, error) {
+	var out []RecoveredBlock
 	if m.rxHeld != nil { // the receive burst that used these buffers has been handled
 		for _, p := range m.release {
 			m.pool.Put(p)
@@ -356,7 +367,9 @@ func (m *batchManager) PollRecovered(wait bool) ([][]byte, error) {
 			return out, err
 		}
 		for _, r := range rec {
-			out = append(out, r.Payloads) // a copy (BatchReceiver.Poll): the pool buffers can go back
+			// a copy (BatchReceiver.Poll): the pool buffers can go back
+			out = append(out, RecoveredBlock{Data: r.Payloads, DestConnID: m.dest[r.BlockID]})
+			delete(m.dest, r.BlockID)
 			if m.rxHeld != nil {
 				for _, p := range m.rxHeld[r.BlockID] {
 					m.pool.Put(p)
@@ -392,6 +405,7 @@ func (m *batchManager) Close() {
 	}
 	if m.rx != nil {
 		m.rx.Close()
+		clear(m.dest)
 	}
 	if m.pool == nil {
 		return

@@ -9,7 +9,10 @@ that bookkeeping statement for statement (line numbers below) over the reference
 sources + repairs >= k) and replays connections against it: lossless streams, losses, duplicates,
 blocks completed by sources after repairs, unrecoverable blocks, an exhausted pool (heap payloads),
 and close mid-stream. It checks that the pool ends full, that no buffer goes back twice, and that
-no buffer goes back while the device or the connection may still read it."""
+no buffer goes back while the device or the connection may still read it. It also replays the
+destination connection ID each staged block carries to the frames recovered from it
+(fec_poll.go RecoveredBlock, connection.go.diff handleRecoveredFEC) against the reference's
+RETIRE_CONNECTION_ID check (conn_id_generator.go:70-89, connection.go:1443-1444,1605-1606)."""
 import random
 
 import pytest
@@ -66,7 +69,7 @@ class Block:
     def recoverable(self):                    # block.go:88-90
         return len(self.src) + len(self.rep) >= self.k
 
-    def payloads(self):                       # batch_manager_hip.go:254-263 blockPayloads
+    def payloads(self):                       # batch_manager_hip.go:259-268 blockPayloads
         return list(self.src.values()) + list(self.rep.values())
 
 
@@ -104,11 +107,16 @@ class Receiver:
         self.pending = 0
         self.rx_held = {}
         self.release = []
+        self.repair_dest = None   # :115-116 repairDest, dest
+        self.dest = {}
 
     def _status(self, bid):
         return self.status.setdefault(bid, [Block(bid, self.k), False])
 
-    def handle_source(self, ssid, buf):   # :267-287 over manager.go:200-227
+    def set_repair_dest(self, cid):   # SetRepairDestConnID
+        self.repair_dest = cid
+
+    def handle_source(self, ssid, buf):   # :272-292 over manager.go:200-227
         bid = ssid // self.k
         prev = self.status[bid][0] if bid in self.status else None
         st = self._status(bid)
@@ -130,7 +138,7 @@ class Receiver:
             self.release.append(buf)
         return ret
 
-    def handle_repair(self, bid, pid, buf):   # :293-341
+    def handle_repair(self, bid, pid, buf):   # :298-347
         st = self._status(bid)
         if st[1]:
             self.release.append(buf)
@@ -143,20 +151,21 @@ class Receiver:
             if staged:
                 self.rx.submit(bid, st[0].payloads())
                 self.pending += 1
+                self.dest[bid] = self.repair_dest
                 self.rx_held[bid] = st[0].payloads()
             else:
                 self.release.extend(st[0].payloads())
             st[0], st[1] = None, True
 
-    def poll_recovered(self, wait):   # :345-373
-        out = 0
+    def poll_recovered(self, wait):   # :356-386: [(block, destConnID)] in staging order
+        out = []
         for b in self.release:
             self.pool.put(b)
         self.release = []
         while self.pending > 0:
             rec = self.rx.poll(wait)
             for bid in rec:
-                out += 1
+                out.append((bid, self.dest.pop(bid)))
                 for b in self.rx_held.pop(bid):
                     self.pool.put(b)
             self.pending -= len(rec)
@@ -164,11 +173,12 @@ class Receiver:
                 break
         return out
 
-    def recovery_pending(self):   # :378
+    def recovery_pending(self):   # :391
         return self.pending > 0 or len(self.release) > 0
 
-    def close(self):   # :389-420
+    def close(self):   # :402-438
         self.rx.close()
+        self.dest = {}
         for bufs in self.rx_held.values():
             for b in bufs:
                 self.pool.put(b)
@@ -190,7 +200,7 @@ class Sender:
         self.status = {}
         self.held = {}
 
-    def add_source(self, ssid, buf):   # :150-187
+    def add_source(self, ssid, buf):   # :155-192
         bid = ssid // self.k
         st = self.status.setdefault(bid, [Block(bid, self.k), False])
         if st[1]:
@@ -201,12 +211,12 @@ class Sender:
             self.held[bid] = list(st[0].src.values())
             st[0], st[1] = None, True
 
-    def poll_repair_frames(self, max_frames):   # :192-213
+    def poll_repair_frames(self, max_frames):   # :197-218
         for bid in self.tx.poll(False, max_frames // self.m if max_frames > 0 else 0):
             for b in self.held.pop(bid):
                 self.pool.put(b)
 
-    def close(self):   # :389-420
+    def close(self):   # :402-438
         self.tx.close()
         for bufs in self.held.values():
             for b in bufs:
@@ -219,7 +229,7 @@ class Sender:
 
 
 def _payload(pool):
-    """wire.FECPayloadBuffer (batch_manager_hip.go:230-245): a pool buffer, or the heap when the
+    """wire.FECPayloadBuffer (batch_manager_hip.go:235-250): a pool buffer, or the heap when the
     pool is exhausted."""
     return pool.get() or Buf(None)
 
@@ -282,3 +292,73 @@ def test_sender_returns_every_buffer(seed, k, m, pool_size):
             snd.poll_repair_frames(rng.choice([0, m, 3 * m, 64]))
     snd.close()
     assert not pool.out and len(pool.free) == pool.n
+
+
+class ProtocolViolation(Exception):
+    pass
+
+
+class ConnIDGenerator:
+    """conn_id_generator.go:70-89 Retire: retiring the connection ID the packet carrying the
+    frame was sent to is a PROTOCOL_VIOLATION; a sequence number no longer active is ignored."""
+
+    def __init__(self, active):
+        self.active = dict(active)   # seq -> connection ID
+        self.highest = max(active)
+
+    def retire(self, seq, sent_with):
+        if seq > self.highest:
+            raise ProtocolViolation("retired connection ID %d (highest issued: %d)" % (seq, self.highest))
+        cid = self.active.get(seq)
+        if cid is None:
+            return
+        if cid == sent_with:
+            raise ProtocolViolation("retired connection ID %d (%s), which was used as the Destination "
+                                    "Connection ID on this packet" % (seq, cid))
+        del self.active[seq]
+
+
+def _replay_retires(packets, per_block):
+    """Packets [(destConnID, block, retire_seq)], each carrying the REPAIR frame that makes its block
+    recoverable; the block's recovered frames hold RETIRE_CONNECTION_ID(retire_seq). The blocks
+    decode on the device and are handed over after every packet has been handled (one receive
+    burst, connection.go.diff run loop). per_block: each block's frames with the ID its block carries
+    (RecoveredBlock.DestConnID); else with one per-connection ID that every REPAIR frame overwrites
+    (the round-4 fecDestConnID)."""
+    k = 4
+    pool = Pool(256)
+    rcv = Receiver(k, pool, Device(pool, random.Random(1)))
+    gen = ConnIDGenerator({0: "A", 1: "B", 2: "C"})
+    last_dest = None
+    retire_of = {}
+    for dest, bid, seq in packets:
+        for j in range(1, k):                  # sources 1..k-1 arrive, source 0 is lost
+            rcv.handle_source(bid * k + j, _payload(pool))
+        rcv.set_repair_dest(dest)              # connection.go.diff, case *wire.RepairFrame
+        last_dest = dest
+        rcv.handle_repair(bid, 0, _payload(pool))
+        retire_of[bid] = seq
+    got = rcv.poll_recovered(True)
+    assert [b for b, _ in got] == [b for _, b, _ in packets]   # staging order
+    for bid, dest in got:
+        gen.retire(retire_of[bid], dest if per_block else last_dest)
+    rcv.close()
+    assert not pool.out
+    return gen
+
+
+def test_recovered_frames_carry_their_packets_dest_conn_id():
+    # block 0 staged by a packet sent to A retires B; block 1 staged by a packet sent to B retires C:
+    # both are legal in the reference, which handles each block's frames inside its own packet
+    gen = _replay_retires([("A", 0, 1), ("B", 1, 2)], per_block=True)
+    assert gen.active == {0: "A"}
+    # one per-connection ID overwritten by the last REPAIR frame (B) makes block 0's retire of B look
+    # like retiring the packet's own destination: a spurious PROTOCOL_VIOLATION
+    with pytest.raises(ProtocolViolation):
+        _replay_retires([("A", 0, 1), ("B", 1, 2)], per_block=False)
+
+
+def test_recovered_retire_of_own_dest_is_still_a_violation():
+    # the reference's check is kept: a block staged by a packet sent to B that retires B
+    with pytest.raises(ProtocolViolation):
+        _replay_retires([("A", 0, 2), ("B", 1, 1)], per_block=True)
