@@ -76,9 +76,10 @@ lib.fec_xor_reconstruct_batch.argtypes = [_vp, _i, _sz, _sz, _vp, _sz, _vp, _sz,
 _u64 = ctypes.c_uint64
 lib.fec_synth_data.argtypes = [_vp, _u64, _u64, _sz, _i, _sz, _vp, _sz, _sz]
 lib.fec_synth_single_erasures.argtypes = [_vp, _u64, _u64, _sz, _i, _i, _vp, _vp]
-lib.fec_probe_encode_traffic.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz]
-lib.fec_probe_recover_traffic.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _vp, _vp, _sz]
-lib.fec_probe_rebuild_traffic.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _vp, _vp, _sz]
+lib.fec_probe_encode_traffic.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _i]
+lib.fec_probe_recover_traffic.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _vp, _vp, _sz, _i]
+lib.fec_probe_rebuild_traffic.argtypes = [_vp, _i, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _vp, _vp, _sz, _i]
+lib.fec_probe_stream_traffic.argtypes = [_vp, _i, _sz, _sz, _vp, _sz, _vp, _sz, _sz, _i]
 lib.fec_probe_link.argtypes = [_vp, _sz, _i, ctypes.POINTER(ctypes.c_double)]
 
 
@@ -188,18 +189,12 @@ class Codec:
         """fec_sync's return code (FEC_ERR_TOO_FEW_SHARDS after a failed block) without raising."""
         return lib.fec_sync(self._h)
 
-    # Kernel-selection knobs (diagnostics and tests; defaults are the measured best). Keys of
-    # the library's internal fec__set_tuning(); the setting is process-wide.
-    TUNING_KEYS = {"enc_nt": 0, "dec_nt": 1, "grid_mult": 2, "dec_max_rounds": 3, "pad_zero": 4,
-                   "items_per_thread": 5, "tiles_per_wg": 6, "rotate": 7, "xcd_swz": 8, "enc_wpc": 9,
-                   "dec_wpc": 10, "enc_fixed": 11, "dec_swz": 12, "gen_wpc": 13, "enc_queue": 14,
-                   "enc_qwpc": 15, "enc_qdepth": 16, "dec_wave": 17, "enc_diag": 18, "dec_fused": 19, "dec_ipl": 20, "dec_diag": 21,
-                   "enc_dyadic": 22, "dec_direct": 23, "dec_sorted": 24, "dec_fixk": 25, "host_chunk": 26,
-                   "dir_wpc": 27, "dir_nt": 28, "dec_pseg": 29, "enc_bits": 30, "enc_bwpc": 31,
-                   "dec_tier": 32, "dec_direct_big": 33, "dec_gate": 34, "dec_gate_pm": 35,
-                   "host_gather": 36, "dec_win": 37, "dec_s64": 38, "dec_psort": 39,
-                   "dec_pv": 40, "dec_povl": 41, "dec_lpad": 42, "bat_zc": 43,
-                   "enc_early": 44, "host_threads": 45, "host_pool": 46, "enc_x23": 47, "xor_fix2": 48, "dec_rwin": 49, "dec_pdiag": 50}
+    # Tuning knobs (tests and tools; defaults are the measured best): residency of the shipped
+    # kernels, routing among shipped kernels, host-path sizes. Keys of the library's internal,
+    # test-only fec__set_tuning() in fk::Tuning's declaration order (fec_kernels.hpp); the setting
+    # is process-wide.
+    TUNING_KEYS = {"enc_wpc": 0, "gen_wpc": 1, "dec_wpc": 2, "dir_wpc": 3, "enc_bwpc": 4, "enc_fixed": 5,
+                   "dec_wave": 6, "dec_direct": 7, "host_chunk": 8, "host_threads": 9, "bat_zc": 10}
 
     def set_tuning(self, **knobs):
         """Set kernel-selection knobs; returns the previous values (pass them back to restore)."""
@@ -300,18 +295,25 @@ class Codec:
         return _check(lib.fec_synth_single_erasures(self._h, seed, first_block, nblocks, k, m, masks, erased),
                       "fec_synth_single_erasures")
 
-    # ---- traffic twins of the headline kernels (include/fec_probe.h; measurement only)
-    def probe_encode_traffic_raw(self, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss):
-        return _check(lib.fec_probe_encode_traffic(self._h, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss),
+    # ---- traffic twins of the headline kernels (include/fec_probe.h; measurement only). wpc:
+    # resident workgroups per CU (-1: the twinned kernel's own, 0: as many as fit)
+    def probe_encode_traffic_raw(self, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss, wpc=-1):
+        return _check(lib.fec_probe_encode_traffic(self._h, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss, wpc),
                       "fec_probe_encode_traffic")
 
-    def probe_recover_traffic_raw(self, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss, masks, out, out_bs):
+    def probe_recover_traffic_raw(self, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss, masks, out, out_bs,
+                                  wpc=-1):
         return _check(lib.fec_probe_recover_traffic(self._h, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss,
-                                                    masks, out, out_bs), "fec_probe_recover_traffic")
+                                                    masks, out, out_bs, wpc), "fec_probe_recover_traffic")
 
-    def probe_rebuild_traffic_raw(self, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss, masks, out, out_bs):
+    def probe_rebuild_traffic_raw(self, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss, masks, out, out_bs,
+                                  wpc=-1):
         return _check(lib.fec_probe_rebuild_traffic(self._h, k, m, shard_len, nblocks, data, dbs, parity, pbs, ss,
-                                                    masks, out, out_bs), "fec_probe_rebuild_traffic")
+                                                    masks, out, out_bs, wpc), "fec_probe_rebuild_traffic")
+
+    def probe_stream_traffic_raw(self, nin, shard_len, nblocks, data, in_bs, out, out_bs, ss, wpc=0):
+        return _check(lib.fec_probe_stream_traffic(self._h, nin, shard_len, nblocks, data, in_bs, out, out_bs, ss, wpc),
+                      "fec_probe_stream_traffic")
 
     def probe_link(self, nbytes=512 << 20, reps=3):
         """{h2d, d2h, duplex_each} GB/s of pinned hipMemcpyAsync on this ctx's device."""

@@ -381,7 +381,7 @@ Error BatchEncoder::flushImpl(size_t* delivered) {
     // a small set is coded straight from and into its pinned buffers: one launch (two when
     // gathered) and an event instead of a copy up, the launch, a copy down (knob bat_zc, as the
     // decoder's sets)
-    const bool zc = B * (size_t)k_ * s.slot <= (size_t)std::max(0, fk::g_tune.bat_zc);
+    const bool zc = B * (size_t)k_ * s.slot <= (size_t)std::max(0, (int)fk::g_tune.bat_zc);
     uint8_t* in = zc ? reinterpret_cast<uint8_t*>((uintptr_t)s.in_dev) : s.d_in;
     uint8_t* out = zc ? s.out_dev : s.d_out;
     if (s.gather) {   // referenced payloads: the device pulls every shard of the batch itself
@@ -827,7 +827,7 @@ Error BatchDecoder::flushImpl(size_t* delivered) {
     // buffers: one launch (two when gathered) and an event, where the copy form makes four copies
     // around the kernels, each a call of its own and a copy-engine round trip (knob bat_zc: input
     // bytes up to which; go_batch_bench burst)
-    const bool zc = B * n * S <= (size_t)std::max(0, fk::g_tune.bat_zc);
+    const bool zc = B * n * S <= (size_t)std::max(0, (int)fk::g_tune.bat_zc);
     uint8_t* in = zc ? reinterpret_cast<uint8_t*>((uintptr_t)s.in_dev) : s.d_in;
     uint8_t* out = zc ? s.out_dev : s.d_out;
     uint32_t* masks = zc ? s.masks_dev : s.d_masks;

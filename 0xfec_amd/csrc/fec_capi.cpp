@@ -77,8 +77,8 @@ constexpr uint64_t kMaxItems = uint64_t(1) << 31;
 
 }  // namespace
 
-// Device scratch of the kernels enqueued on one stream: decode plan records, the direct decode's
-// multi-erasure worklist and the queue kernels' ticket counters. Each stream the ctx launches on
+// Device scratch of the kernels enqueued on one stream: decode plan records and the direct decode's
+// multi-erasure worklist. Each stream the ctx launches on
 // (its own / the caller's, and one per host-path staging set) has its own, so launches that
 // overlap on different streams never share one (nor free one the other stream still reads).
 struct Work {
@@ -86,10 +86,8 @@ struct Work {
     size_t plans_cap = 0;
     uint32_t* d_hard = nullptr;   // fk::kHardList + waves words; count and done rewound by the kernel
     size_t hard_cap = 0;
-    uint32_t* d_ctr = nullptr;    // fk::kCtrWords ticket counters, self-rewinding
-    uint32_t* d_gate = nullptr;   // fk::kGateWords: the decode path rs_classify_kernel picked, its counters
     void release() {
-        for (void* q : {(void*)d_plans, (void*)d_hard, (void*)d_ctr, (void*)d_gate})
+        for (void* q : {(void*)d_plans, (void*)d_hard})
             if (q) (void)hipFree(q);
         *this = Work{};
     }
@@ -119,8 +117,8 @@ struct HostSet {
 // set's events alone. PCIe's two directions and the kernels of different chunks therefore overlap,
 // and the up direction (the larger one on every path) never waits for the host: the host blocks only
 // to reuse a set, on its chunk kHostSets back, and at the end of a call. Measured on one MI355X
-// (tools/pcie_duplex_probe.hip, profiles/r04/pcie_duplex_probe_r04a.log): H2D 57.5 GB/s, D2H 57.0,
-// both at once 48.9 each way; this shape with 64 MiB chunks moved 53.7 GB/s up and 26.8 down.
+// (tools/pcie_duplex_probe.hip, profiles/r04/pcie_duplex_probe_r04b.log): H2D 57.6 GB/s, D2H 57.0,
+// both at once 48.6 each way; this shape with 64 MiB chunks moved 53.8 GB/s up.
 constexpr int kHostSets = 3;
 struct HostPipe {
     hipStream_t up = nullptr, comp = nullptr, down = nullptr;
@@ -142,16 +140,9 @@ struct fec_ctx {
     uint32_t* d_masks = nullptr;
     int32_t* d_status = nullptr;
     size_t masks_cap = 0;
-    int grid_cache[3][6] = {};
     int ncu = 256;           // compute units of the device
     HostPipe pipe;           // host-resident path (FEC_HOST / FEC_HOST_PINNED)
     hipEvent_t handoff = nullptr;   // orders a newly set stream after the previous one
-    // multi-erasure decode with the plan kernels of later sub-batches beside the rebuild of earlier
-    // ones (knob dec_povl): the plans run on `side` (high priority), each sub-batch's rebuild waits
-    // for its plan's event; side_in orders the side stream after the calling stream
-    hipStream_t side = nullptr;
-    hipEvent_t side_in = nullptr;
-    hipEvent_t side_ev[8] = {};
 };
 
 #define HIP_TRY(expr)                      \
@@ -292,26 +283,6 @@ static int grow_hard(fec_ctx* ctx, size_t waves) {
     return FEC_OK;
 }
 
-// The queue kernels' ticket counters of the current stream's workspace (zeroed once; the kernels
-// rewind them).
-static int ensure_ctr(fec_ctx* ctx) {
-    Work& w = *ctx->work;
-    if (w.d_ctr) return FEC_OK;
-    HIP_TRY(hipMalloc(&w.d_ctr, fk::kCtrWords * sizeof(uint32_t)));
-    HIP_TRY(hipMemsetAsync(w.d_ctr, 0, fk::kCtrWords * sizeof(uint32_t), ctx->stream));
-    return FEC_OK;
-}
-
-// The classify kernel's gate words of the current stream's workspace (zeroed once; the kernel
-// rewinds its counters).
-static int ensure_gate(fec_ctx* ctx) {
-    Work& w = *ctx->work;
-    if (w.d_gate) return FEC_OK;
-    HIP_TRY(hipMalloc(&w.d_gate, fk::kGateWords * sizeof(uint32_t)));
-    HIP_TRY(hipMemsetAsync(w.d_gate, 0, fk::kGateWords * sizeof(uint32_t), ctx->stream));
-    return FEC_OK;
-}
-
 static int grow_stage(fec_ctx* ctx, size_t bytes) {
     if (bytes <= ctx->stage_cap) return FEC_OK;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -340,23 +311,11 @@ static int grow_masks(fec_ctx* ctx, size_t n) {
     return FEC_OK;
 }
 
-static int slot_of(uint32_t sel) { return sel <= 1 ? 0 : sel <= 2 ? 1 : sel <= 4 ? 2 : sel <= 8 ? 3 : 4; }
-
-static int grid_for(fec_ctx* ctx, int which, uint32_t sel, size_t lds) {
-    int& g = ctx->grid_cache[which][slot_of(sel)];
-    if (g == 0) g = fk::occupancy_grid(ctx->device, which, sel, lds) * std::max(1, fk::g_tune.grid_mult);
-    return g;
-}
-
 static size_t round16(size_t x) { return (x + 15) & ~size_t(15); }
 
-// Workgroups for a flat (block, chunk) item launch.
-static int flat_grid(int resident, uint32_t total) {
-    const uint64_t all = ((uint64_t)total + fk::kThreads - 1) / fk::kThreads;
-    uint64_t g = (uint64_t)resident;
-    if (fk::g_tune.items_per_thread > 0) g = (all + fk::g_tune.items_per_thread - 1) / fk::g_tune.items_per_thread;
-    g = std::min<uint64_t>(g, all);
-    return (int)std::max<uint64_t>(1, std::min<uint64_t>(g, 0x7FFFFFFF));
+// Workgroups for a flat (block, chunk) item launch: one item per lane (total < 2^31).
+static int flat_grid(uint32_t total) {
+    return (int)std::max<uint64_t>(1, ((uint64_t)total + fk::kThreads - 1) / fk::kThreads);
 }
 
 // ---------------------------------------------------------------- device-memory cores
@@ -383,36 +342,14 @@ static int rs_encode_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks
             a.total = (uint32_t)(nb * cps);
             a.div_cps = fk::make_fastdiv(cps);
             a.tabs = code->d_tabs + (size_t)r0 * k * 8;
-            a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
-            a.rot = fk::g_tune.rotate ? fk::line_rotation(ss, cps) : 0;
-            a.swz = (uint32_t)fk::g_tune.xcd_swz;
-            if (fk::fixed_encode_applies((uint32_t)k, (uint32_t)mr)) {
-                if (fk::g_tune.enc_queue) {
-                    const int rc = ensure_ctr(ctx);
-                    if (rc) return rc;
-                }
-                a.ctr = ctx->work->d_ctr;
-                a.dytabs = (r0 == 0 && mr == code->m) ? code->d_dytabs : nullptr;
-                HIP_TRY(fk::launch_rs_encode_fixed(a, ctx->ncu, ctx->stream));
+            a.dytabs = (r0 == 0 && mr == code->m) ? code->d_dytabs : nullptr;
+            if (fk::fixed_encode_applies((uint32_t)k, (uint32_t)mr, a.dytabs != nullptr)) {
+                HIP_TRY(fk::launch_rs_encode_fixed(a, ctx->stream));
                 continue;
             }
-            const size_t lds = (size_t)mr * k * sizeof(gf::PermTab);
-            int grid = grid_for(ctx, 0, (uint32_t)mr, fk::occupancy_lds(fk::g_tune.gen_wpc, lds <= 65536 ? lds : 0));
-            grid = flat_grid(grid, a.total);
-            if (grid < 1) grid = 1;
-            HIP_TRY(fk::launch_rs_encode(a, grid, ctx->stream));
+            HIP_TRY(fk::launch_rs_encode(a, flat_grid(a.total), ctx->stream));
         }
     }
-    return FEC_OK;
-}
-
-static int ensure_side(fec_ctx* ctx) {
-    if (ctx->side) return FEC_OK;
-    int least = 0, greatest = 0;
-    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    HIP_TRY(hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, greatest));
-    HIP_TRY(hipEventCreateWithFlags(&ctx->side_in, hipEventDisableTiming));
-    for (hipEvent_t& e : ctx->side_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     return FEC_OK;
 }
 
@@ -425,106 +362,28 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
     const uint32_t k = (uint32_t)code->k, m = (uint32_t)code->m;
     const uint32_t maxe = std::max<uint32_t>(1, std::min(k, m));
     const uint32_t cps = (uint32_t)((len + fk::kChunk - 1) / fk::kChunk);
-    const fk::PlanLayout lay0 = fk::plan_layout(k, maxe);
-    // direct form: no plan kernel (single-erasure tables of the code; multi-erasure waves plan
-    // in-wave), fec_recover.hip
-    // one output slot per block (recover into a buffer): the direct kernel alone is always right,
-    // for the big codes too (RS(20,30) single erasure +15 % over plan + rebuild, r03h)
+    const fk::PlanLayout lay_block = fk::plan_layout(k, maxe), lay_sorted = fk::plan_layout(k, maxe, true);
+    // Three forms:
+    //  * direct (fec_recover.hip): no plan kernel; single-erasure tables of the code, multi-erasure
+    //    waves planned in-wave from a worklist. Small codes (RS(2,3), RS(8,12)), and the big ones
+    //    when the caller gave one output slot per block (RS(20,30) single erasure +15 % over plan +
+    //    rebuild, r03h);
+    //  * shards of 32+ chunks: sorted plans (fec_plan.hip), then the wave-form rebuild
+    //    (fec_rebuild.hip for RS(16,24) / RS(20,30) with 64+ chunks, else fec_decode.hip);
+    //  * short shards: plans in block order, then the workgroup-tile rebuild.
     const bool single_slot = out && out_slots == 1;
-    const bool direct = code->d_single_coef && fk::direct_recon_applies(k, m, cps, lay0.stride, single_slot);
-    const bool sorted_ok = fk::g_tune.dec_sorted && !fk::g_tune.dec_fused && !fk::g_tune.dec_diag &&
-                           fk::wave_recon_applies(cps, k, maxe, fk::plan_layout(k, maxe, true).stride);
-    // both, gated on the device (RS(16,24), RS(20,30): their worklist path is slow, so a batch with
-    // more than dec_gate_pm per mille of multi-erasure blocks takes the plan path instead)
-    const bool gated = direct && !single_slot && sorted_ok && fk::g_tune.dec_gate &&
-                       (size_t)k * m * k * sizeof(gf::PermTab) > 16 * 1024;
-    // sorted parallel plans for the plan + wave path (fec_plan.hip)
-    const bool sorted = (gated || !direct) && sorted_ok;
-    const fk::PlanLayout lay = sorted ? fk::plan_layout(k, maxe, true) : lay0;
-    size_t per_launch =
-        std::min<size_t>(direct && !gated ? nblocks : kPlanBytes / lay.stride, (size_t)(kMaxItems / cps));
+    const bool direct = code->d_single_coef && fk::direct_recon_applies(k, m, cps, lay_block.stride, single_slot);
+    const bool wave = !direct && fk::wave_recon_applies(cps, k, maxe, lay_sorted.stride);
+    const fk::PlanLayout lay = wave ? lay_sorted : lay_block;
+    size_t per_launch = std::min<size_t>(direct ? nblocks : kPlanBytes / lay.stride, (size_t)(kMaxItems / cps));
     per_launch = std::max<size_t>(1, std::min(per_launch, nblocks));
     {
-        int rc = direct ? grow_hard(ctx, (per_launch * cps + 63) / 64) : FEC_OK;
-        if (!rc && (!direct || gated)) rc = grow_plans(ctx, per_launch * lay.stride);
-        if (!rc && gated) rc = ensure_gate(ctx);
+        const int rc = direct ? grow_hard(ctx, (per_launch * cps + 63) / 64) : grow_plans(ctx, per_launch * lay.stride);
         if (rc) return rc;
     }
     const uint32_t G = fk::pick_tile_blocks(cps, k, maxe, lay);
-    const size_t lds = fk::recon_lds_bytes(G, k, maxe, lay);
-    const bool wave = fk::wave_recon_applies(cps, k, maxe, lay.stride);
-    const bool fused = wave && fk::g_tune.dec_fused;
-    // two-tier rebuild (fec_decode.hip): waves needing many rows go through the worklist
-    const bool tiered = wave && sorted && !fused && fk::tier_recon_applies(k, maxe, cps);
-    if (tiered) {
-        const int rc = grow_hard(ctx, (per_launch * cps + 63) / 64);
-        if (rc) return rc;
-    }
-    // plans of sub-batch j + 1 beside the rebuild of sub-batch j (knob dec_povl = sub-batches per
-    // launch, each a multiple of 64 blocks, the plan sort window)
-    const int povl = std::min(fk::g_tune.dec_povl, 8);
-    const bool overlap = povl > 1 && sorted && wave && !fused && !tiered && !direct && !gated &&
-                         fk::rebuild_k_applies(k, maxe, cps) && nblocks >= (size_t)povl * 1024;
-    if (overlap) {
-        const int rc = ensure_side(ctx);
-        if (rc) return rc;
-    }
     for (size_t b0 = 0; b0 < nblocks; b0 += per_launch) {
         const size_t nb = std::min(per_launch, nblocks - b0);
-        if (overlap) {
-            HIP_TRY(hipEventRecord(ctx->side_in, ctx->stream));
-            HIP_TRY(hipStreamWaitEvent(ctx->side, ctx->side_in, 0));
-            const size_t sub = (nb + povl - 1) / povl + 63 & ~(size_t)63;
-            int j = 0;
-            for (size_t s0 = 0; s0 < nb; s0 += sub, ++j) {   // every plan first, on the side stream
-                const size_t snb = std::min(sub, nb - s0);
-                fk::PlanArgs p{};
-                p.masks = masks + b0 + s0;
-                p.plans = ctx->work->d_plans + s0 * lay.stride;
-                p.status = status ? status + b0 + s0 : nullptr;
-                p.err = err;
-                p.prows = code->d_prows;
-                p.k = k;
-                p.m = m;
-                p.nblocks = (uint32_t)snb;
-                p.maxe = maxe;
-                p.lay = lay;
-                p.max_out = out ? out_slots : 0;
-                p.dall = code->d_dall;
-                HIP_TRY(fk::launch_rs_plan_sorted(p, ctx->side));
-                HIP_TRY(hipEventRecord(ctx->side_ev[j], ctx->side));
-            }
-            j = 0;
-            for (size_t s0 = 0; s0 < nb; s0 += sub, ++j) {   // each rebuild after its plan
-                const size_t snb = std::min(sub, nb - s0);
-                HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->side_ev[j], 0));
-                fk::ReconArgs a{};
-                a.data = data + (b0 + s0) * dbs;
-                a.parity = parity + (b0 + s0) * pbs;
-                a.dbs = dbs;
-                a.pbs = pbs;
-                a.ss = ss;
-                a.pss = pss;
-                a.plans = ctx->work->d_plans + s0 * lay.stride;
-                a.k = k;
-                a.len = (uint32_t)len;
-                a.cps = cps;
-                a.nblocks = (uint32_t)snb;
-                a.maxe = maxe;
-                a.lay = lay;
-                a.g = G;
-                a.ntiles = (uint32_t)((snb + G - 1) / G);
-                a.div_cps = fk::make_fastdiv(cps);
-                a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
-                a.rot = fk::g_tune.rotate ? fk::line_rotation(ss, cps) : 0;
-                a.swz = (uint32_t)fk::g_tune.dec_swz;
-                a.sorted = 1u;
-                a.out = out ? out + (b0 + s0) * out_bs : nullptr;
-                a.out_bs = out_bs;
-                HIP_TRY(fk::launch_rs_rebuild_k(a, ctx->stream));
-            }
-            continue;
-        }
         fk::PlanArgs p{};
         p.masks = masks + b0;
         p.plans = ctx->work->d_plans;
@@ -538,14 +397,6 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         p.lay = lay;
         p.max_out = out ? out_slots : 0;
         p.dall = code->d_dall;
-        if (gated) {
-            HIP_TRY(fk::launch_rs_classify(p.masks, (uint32_t)nb, k, m, p.max_out, ctx->work->d_gate,
-                                           (uint32_t)fk::g_tune.dec_gate_pm, ctx->ncu, ctx->stream));
-            p.gate = ctx->work->d_gate;
-            p.gate_want = 2;
-        }
-        if (sorted) HIP_TRY(fk::launch_rs_plan_sorted(p, ctx->stream));
-        else if (!fused && !direct) HIP_TRY(fk::launch_rs_plan(p, ctx->stream));
         fk::ReconArgs a{};
         a.data = data + b0 * dbs;
         a.parity = parity + b0 * pbs;
@@ -563,14 +414,9 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         a.g = G;
         a.ntiles = (uint32_t)((nb + G - 1) / G);
         a.div_cps = fk::make_fastdiv(cps);
-        a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
-        a.rot = fk::g_tune.rotate ? fk::line_rotation(ss, cps) : 0;
-        a.swz = (uint32_t)fk::g_tune.dec_swz;
-        a.diag = (uint32_t)fk::g_tune.dec_diag;
-        a.sorted = sorted ? 1u : 0u;
+        a.sorted = wave ? 1u : 0u;
         a.out = out ? out + b0 * out_bs : nullptr;
         a.out_bs = out_bs;
-        a.persist_ncu = gated ? (uint32_t)ctx->ncu : 0u;   // both paths persistent: the loser exits in one round
         if (direct) {
             a.masks = p.masks;
             a.status = p.status;
@@ -583,42 +429,15 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
             a.single_coef_host = code->single_coef.data();
             a.hard = ctx->work->d_hard;
             a.hard_cap = (uint32_t)(ctx->work->hard_cap - fk::kHardList);
-            a.gate = gated ? ctx->work->d_gate : nullptr;
-            a.gate_want = 1;
             HIP_TRY(fk::launch_rs_recover_direct(a, ctx->ncu, ctx->stream));
-            if (!gated) continue;
-            a.gate_want = 2;   // and the plan path, which runs only if the classify kernel picked it
-        }
-        if (fused) {
-            a.masks = p.masks;
-            a.status = p.status;
-            a.err = p.err;
-            a.prows = p.prows;
-            a.m = m;
-            a.max_out = p.max_out;
-            HIP_TRY(fk::launch_rs_recover_fused(a, ctx->stream));
-            continue;
-        }
-        if (tiered) {
-            a.err = err;
-            a.hard = ctx->work->d_hard;
-            a.hard_cap = (uint32_t)(ctx->work->hard_cap - fk::kHardList);
-            a.list_grid = (uint32_t)ctx->ncu * 4;
-            HIP_TRY(fk::launch_rs_reconstruct_tiered(a, ctx->stream));
-            continue;
-        }
-        if (wave) {
+        } else if (wave) {
+            HIP_TRY(fk::launch_rs_plan_sorted(p, ctx->stream));
             if (fk::rebuild_k_applies(k, maxe, cps)) HIP_TRY(fk::launch_rs_rebuild_k(a, ctx->stream));
             else HIP_TRY(fk::launch_rs_reconstruct_wave(a, ctx->stream));
-            continue;
+        } else {
+            HIP_TRY(fk::launch_rs_plan(p, ctx->stream));
+            HIP_TRY(fk::launch_rs_reconstruct(a, (int)std::max<uint32_t>(1, a.ntiles), ctx->stream));
         }
-        int grid;
-        if (fk::g_tune.tiles_per_wg > 0)
-            grid = (int)((a.ntiles + fk::g_tune.tiles_per_wg - 1) / fk::g_tune.tiles_per_wg);
-        else
-            grid = grid_for(ctx, 1, maxe, fk::occupancy_lds(fk::g_tune.dec_wpc, lds));
-        grid = std::max(1, std::min<int>(grid, (int)a.ntiles));
-        HIP_TRY(fk::launch_rs_reconstruct(a, grid, ctx->stream));
     }
     return FEC_OK;
 }
@@ -640,13 +459,7 @@ static int xor_encode_device(fec_ctx* ctx, int k, size_t len, size_t nblocks, co
         a.cps = cps;
         a.total = (uint32_t)(nb * cps);
         a.div_cps = fk::make_fastdiv(cps);
-        a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
-        a.rot = fk::g_tune.rotate ? fk::line_rotation(ss, cps) : 0;
-        a.swz = (uint32_t)fk::g_tune.xcd_swz;
-        int grid = grid_for(ctx, 2, 1, fk::occupancy_lds(fk::g_tune.gen_wpc, 0));
-        grid = flat_grid(grid, a.total);
-        if (grid < 1) grid = 1;
-        HIP_TRY(fk::launch_xor_encode(a, grid, ctx->stream));
+        HIP_TRY(fk::launch_xor_encode(a, flat_grid(a.total), ctx->stream));
     }
     return FEC_OK;
 }
@@ -674,13 +487,7 @@ static int xor_reconstruct_device(fec_ctx* ctx, int k, size_t len, size_t nblock
         a.cps = cps;
         a.total = (uint32_t)(nb * cps);
         a.div_cps = fk::make_fastdiv(cps);
-        a.pad_zero = (uint32_t)fk::g_tune.pad_zero;
-        a.rot = fk::g_tune.rotate ? fk::line_rotation(ss, cps) : 0;
-        a.swz = (uint32_t)fk::g_tune.dec_swz;
-        int grid = grid_for(ctx, 2, 1, fk::occupancy_lds(fk::g_tune.dec_wpc, 0));
-        grid = flat_grid(grid, a.total);
-        if (grid < 1) grid = 1;
-        HIP_TRY(fk::launch_xor_reconstruct(a, grid, ctx->stream));
+        HIP_TRY(fk::launch_xor_reconstruct(a, flat_grid(a.total), ctx->stream));
     }
     return FEC_OK;
 }
@@ -779,17 +586,18 @@ class CopyPool {
 };
 
 // fn(lo, hi) over [0, n) on up to host_threads threads (knob, 8): the staging and scatter copies
-// of FEC_HOST (one core copies ~10 GB/s, a fifth of PCIe). Knob host_pool (1): on CopyPool's
-// persistent workers; 0: threads made per call (round 4 before r04j).
+// of FEC_HOST (one core copies ~10 GB/s, a fifth of PCIe), on CopyPool's persistent workers (r04j:
+// +0.7 to +1.6 GiB/s pageable over threads made per call); a caller that finds them busy makes
+// its own.
 template <class F>
 static void parallel_for(size_t n, F fn) {
-    const unsigned T = std::min<unsigned>((unsigned)std::max(1, fk::g_tune.host_threads),
+    const unsigned T = std::min<unsigned>((unsigned)std::max(1, (int)fk::g_tune.host_threads),
                                           std::max(1u, std::thread::hardware_concurrency()));
     if (n < 512 || T == 1) {
         fn((size_t)0, n);
         return;
     }
-    if (fk::g_tune.host_pool && CopyPool::get().run(T, n, std::function<void(size_t, size_t)>(fn))) return;
+    if (CopyPool::get().run(T, n, std::function<void(size_t, size_t)>(fn))) return;
     std::vector<std::thread> th;
     const size_t per = (n + T - 1) / T;
     for (size_t lo = 0; lo < n; lo += per) th.emplace_back(fn, lo, std::min(n, lo + per));
@@ -1057,6 +865,9 @@ static int host_reconstruct_rs(fec_ctx* ctx, Code* code, int k, int m, size_t le
     if (pinned)
         for (HostSet& s : p.set)
             if ((rc = grow_dev(&s.d_raw_in, &s.raw_in_cap, span_bytes(chunk, k, dbs, ss, len) + 16))) return rc;
+    // the sticky device word of the host path: statuses report every per-block failure, but a plan
+    // kernel that cannot run (fec_plan.hip form 3's LDS-alignment guard, bit 4) writes no statuses
+    HIP_TRY(hipMemsetAsync(ctx->d_err + 1, 0, sizeof(int), p.comp));
     bool failed = false;
     auto up = [&](HostSet& s, HostChunk& ch) -> int {
         const size_t nb = ch.nb, b0 = ch.b0;
@@ -1085,12 +896,12 @@ static int host_reconstruct_rs(fec_ctx* ctx, Code* code, int k, int m, size_t le
             // the device reads sparse planes straight out of the caller's pinned buffer (needs a
             // device mapping of it; otherwise every plane goes by DMA)
             const uint8_t* dpar = nullptr;
-            const bool mapped = ch.planes && fk::g_tune.host_gather &&
+            const bool mapped = ch.planes &&
                                 hipHostGetDevicePointer((void**)&dpar, (void*)(parity + b0 * pbs), 0) == hipSuccess &&
                                 dpar;
             if (ch.planes && !mapped) (void)hipGetLastError();
             for (size_t r = 0; r < ch.planes; ++r) {
-                const bool sparse = fk::g_tune.host_gather == 2 || needers[r] * 4 < nb * 3;
+                const bool sparse = needers[r] * 4 < nb * 3;
                 if (mapped && sparse) {
                     ch.gather |= 1u << r;
                     continue;
@@ -1156,7 +967,10 @@ static int host_reconstruct_rs(fec_ctx* ctx, Code* code, int k, int m, size_t le
         return FEC_OK;
     };
     if ((rc = host_pipeline(ctx, nblocks, chunk, up, kern, down, finish))) return rc;
-    // the sticky device word of the host path is not used: statuses say it all
+    int err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, ctx->d_err + 1, sizeof(int), hipMemcpyDeviceToHost, p.comp));
+    HIP_TRY(hipStreamSynchronize(p.comp));
+    if (err & 4) return FEC_ERR_HIP;
     return failed ? FEC_ERR_TOO_FEW_SHARDS : FEC_OK;
 }
 
@@ -1256,8 +1070,6 @@ int fec_ctx_create(int device, fec_ctx** out) {
     ctx->device = device;
     if (hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&ctx->d_err, 2 * sizeof(int)) != hipSuccess ||
-        hipMalloc(&ctx->main.d_ctr, fk::kCtrWords * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(ctx->main.d_ctr, 0, fk::kCtrWords * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(ctx->d_err, 0, 2 * sizeof(int)) != hipSuccess ||
         hipDeviceSynchronize() != hipSuccess) {   // null-stream memsets done before any ctx stream runs
         (void)hipGetLastError();
@@ -1315,20 +1127,13 @@ void fec_ctx_destroy(fec_ctx* ctx) {
     for (hipStream_t q : {p.up, p.comp, p.down})
         if (q) (void)hipStreamDestroy(q);
     if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
-    if (ctx->side) {
-        (void)hipStreamSynchronize(ctx->side);
-        (void)hipStreamDestroy(ctx->side);
-    }
-    for (hipEvent_t e : ctx->side_ev)
-        if (e) (void)hipEventDestroy(e);
-    if (ctx->side_in) (void)hipEventDestroy(ctx->side_in);
     if (ctx->own) (void)hipStreamDestroy(ctx->own);
     (void)hipGetLastError();
     delete ctx;
 }
 
 // Switch the ctx to `next`. The ctx's own / caller's stream share one workspace (`main`: plan
-// records, the self-rewinding worklist, ticket counters), so work already queued on the old
+// records, the self-rewinding worklist), so work already queued on the old
 // stream must finish before anything on the new one touches it: the new stream waits on an
 // event recorded on the old one (no host wait). grow_* then sync only the current stream,
 // which by this wait covers the old one's kernels too.
@@ -1348,79 +1153,50 @@ int fec_ctx_set_stream(fec_ctx* ctx, void* hip_stream) {
     return switch_stream(ctx, (hipStream_t)hip_stream);
 }
 
-// Internal tuning knob (not part of the public ABI; process-wide): kernel variants and grid
-// sizing, A/B-tested by tools/kbench.py. Keys: 0 encode/XOR nt, 1 decode nt, 2 persistent grid
-// multiplier, 3 decode max rounds per tile, 4 zero-padded tail stores, 5 items per thread
-// (flat kernels, 0 = persistent), 6 tiles per workgroup (decode, 0 = persistent).
-// Returns the previous value.
+// Internal, test-only tuning entry point (not part of the public ABI): knob `key` of fk::Tuning
+// (fec_kernels.hpp, keys 0..kTuningKeys-1 in declaration order) set to `value`, process-wide, for
+// every ctx. Tests and tools set knobs while no other thread submits work. Returns the previous
+// value, or FEC_ERR_INVALID_ARG for an unknown key.
 int fec__set_tuning(fec_ctx* ctx, int key, int value) {
     if (!ctx) return FEC_ERR_INVALID_ARG;
-    int* slot = key == 0 ? &fk::g_tune.enc_nt : key == 1 ? &fk::g_tune.dec_nt
-              : key == 2 ? &fk::g_tune.grid_mult : key == 3 ? &fk::g_tune.dec_max_rounds
-              : key == 4 ? &fk::g_tune.pad_zero : key == 5 ? &fk::g_tune.items_per_thread
-              : key == 6 ? &fk::g_tune.tiles_per_wg : key == 7 ? &fk::g_tune.rotate
-              : key == 8 ? &fk::g_tune.xcd_swz : key == 9 ? &fk::g_tune.enc_wpc
-              : key == 10 ? &fk::g_tune.dec_wpc : key == 11 ? &fk::g_tune.enc_fixed
-              : key == 12 ? &fk::g_tune.dec_swz : key == 13 ? &fk::g_tune.gen_wpc
-              : key == 14 ? &fk::g_tune.enc_queue : key == 15 ? &fk::g_tune.enc_qwpc
-              : key == 16 ? &fk::g_tune.enc_qdepth : key == 17 ? &fk::g_tune.dec_wave
-              : key == 18 ? &fk::g_tune.enc_diag : key == 19 ? &fk::g_tune.dec_fused
-              : key == 20 ? &fk::g_tune.dec_ipl : key == 21 ? &fk::g_tune.dec_diag
-              : key == 22 ? &fk::g_tune.enc_dyadic : key == 23 ? &fk::g_tune.dec_direct
-              : key == 24 ? &fk::g_tune.dec_sorted : key == 25 ? &fk::g_tune.dec_fixk
-              : key == 26 ? &fk::g_tune.host_chunk : key == 27 ? &fk::g_tune.dir_wpc
-              : key == 28 ? &fk::g_tune.dir_nt : key == 29 ? &fk::g_tune.dec_pseg
-              : key == 30 ? &fk::g_tune.enc_bits : key == 31 ? &fk::g_tune.enc_bwpc
-              : key == 32 ? &fk::g_tune.dec_tier : key == 33 ? &fk::g_tune.dec_direct_big
-              : key == 34 ? &fk::g_tune.dec_gate : key == 35 ? &fk::g_tune.dec_gate_pm
-              : key == 36 ? &fk::g_tune.host_gather : key == 37 ? &fk::g_tune.dec_win
-              : key == 38 ? &fk::g_tune.dec_s64
-              : key == 39 ? &fk::g_tune.dec_psort : key == 40 ? &fk::g_tune.dec_pv
-              : key == 41 ? &fk::g_tune.dec_povl : key == 42 ? &fk::g_tune.dec_lpad
-              : key == 43 ? &fk::g_tune.bat_zc
-              : key == 44 ? &fk::g_tune.enc_early : key == 45 ? &fk::g_tune.host_threads
-              : key == 46 ? &fk::g_tune.host_pool : key == 47 ? &fk::g_tune.enc_x23
-              : key == 48 ? &fk::g_tune.xor_fix2 : key == 49 ? &fk::g_tune.dec_rwin
-              : key == 50 ? &fk::g_tune.dec_pdiag : nullptr;
-    if (!slot) return FEC_ERR_INVALID_ARG;
-    const int old = *slot;
-    *slot = value;
-    memset(ctx->grid_cache, 0, sizeof(ctx->grid_cache));
-    return old;
+    fk::Tuning& t = fk::g_tune;
+    std::atomic<int>* slots[fk::kTuningKeys] = {&t.enc_wpc,   &t.gen_wpc,    &t.dec_wpc,      &t.dir_wpc,
+                                                &t.enc_bwpc,  &t.enc_fixed,  &t.dec_wave,     &t.dec_direct,
+                                                &t.host_chunk, &t.host_threads, &t.bat_zc};
+    if (key < 0 || key >= fk::kTuningKeys) return FEC_ERR_INVALID_ARG;
+    return slots[key]->exchange(value);
 }
 
 // Internal self-test (not part of the public ABI, no device needed): parallel_for covers [0, n)
-// exactly once on the persistent copy workers and on threads made per call, for sizes around
-// the part boundaries and part counts 2..16, with four threads calling at once (one holds the
-// workers, the others find them busy and make their own). 0 on success, else the failing case.
+// exactly once, for sizes around the part boundaries and part counts 2..16, with four threads
+// calling at once (one holds the persistent copy workers, the others find them busy and make
+// their own threads). 0 on success, else the failing case.
 extern "C" int fec__selftest_copypool(void) {
-    const fk::Tuning saved = fk::g_tune;
+    const int saved = fk::g_tune.host_threads;
     int fail = 0;
     const size_t sizes[] = {511, 512, 513, 1000, 4097, 65536, 100003};
-    for (int pool = 0; pool <= 1 && !fail; ++pool)
-        for (int T : {2, 3, 8, 16}) {
-            fk::g_tune.host_pool = pool;
-            fk::g_tune.host_threads = T;
-            std::vector<std::thread> callers;
-            std::vector<int> bad(4, 0);
-            for (int t = 0; t < 4; ++t)
-                callers.emplace_back([&, t] {
-                    for (size_t n : sizes) {
-                        std::unique_ptr<std::atomic<uint32_t>[]> hits(new std::atomic<uint32_t>[n]);
-                        for (size_t i = 0; i < n; ++i) hits[i].store(0);
-                        parallel_for(n, [&](size_t lo, size_t hi) {
-                            for (size_t i = lo; i < hi; ++i) hits[i].fetch_add(1);
-                        });
-                        for (size_t i = 0; i < n; ++i)
-                            if (hits[i].load() != 1) bad[t] = 1;
-                    }
-                });
-            for (auto& th : callers) th.join();
-            for (int b : bad)
-                if (b) fail = 1 + pool * 100 + T;
-            if (fail) break;
-        }
-    fk::g_tune = saved;
+    for (int T : {2, 3, 8, 16}) {
+        fk::g_tune.host_threads = T;
+        std::vector<std::thread> callers;
+        std::vector<int> bad(4, 0);
+        for (int t = 0; t < 4; ++t)
+            callers.emplace_back([&, t] {
+                for (size_t n : sizes) {
+                    std::unique_ptr<std::atomic<uint32_t>[]> hits(new std::atomic<uint32_t>[n]);
+                    for (size_t i = 0; i < n; ++i) hits[i].store(0);
+                    parallel_for(n, [&](size_t lo, size_t hi) {
+                        for (size_t i = lo; i < hi; ++i) hits[i].fetch_add(1);
+                    });
+                    for (size_t i = 0; i < n; ++i)
+                        if (hits[i].load() != 1) bad[t] = 1;
+                }
+            });
+        for (auto& th : callers) th.join();
+        for (int b : bad)
+            if (b) fail = 100 + T;
+        if (fail) break;
+    }
+    fk::g_tune.host_threads = saved;
     return fail;
 }
 

@@ -17,33 +17,17 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
     return (uint32_t)(((uint64_t)t + n) >> f.shift);
 }
 
-// Item order inside a block: the first `rot` items take the last `rot` chunks of the shard,
-// so a shard's tail and the next shard's head — which share a 128-byte line when the shard
-// stride is an odd multiple of 64 (1216 = 9.5 lines) — are loaded by neighbouring lanes of
-// one wave on consecutive instructions, and the line is fetched from HBM once.
-__device__ __forceinline__ uint32_t rotate_chunk(uint32_t c, uint32_t cps, uint32_t rot) {
-    return c < rot ? c + (cps - rot) : c - rot;
-}
-
 // Workgroup index in XCD-contiguous order. Dispatch deals workgroups round-robin over the 8
-// XCDs (MI355X_MICROARCH.md, workgroup dispatch); with swz the workgroups one XCD receives take
-// one contiguous eighth of the grid, so each XCD streams its own contiguous address range
-// (speed only: any bijection is correct). Workgroups past the last multiple of 8 keep their index.
-__device__ __forceinline__ uint32_t xcd_order_of(uint32_t wg, uint32_t G, uint32_t swz) {
-    if (!swz) return wg;
+// XCDs (MI355X_MICROARCH.md, workgroup dispatch); here the workgroups one XCD receives take one
+// contiguous eighth of the grid, so each XCD streams its own contiguous address range (speed
+// only: any bijection is correct; DESIGN.md 3: +5-9 % encode, +2-3.5 % decode). Workgroups past
+// the last multiple of 8 keep their index.
+__device__ __forceinline__ uint32_t xcd_order_of(uint32_t wg, uint32_t G) {
     const uint32_t full = G & ~7u;
     if (wg >= full) return wg;
     return (wg & 7u) * (full >> 3) + (wg >> 3);
 }
-__device__ __forceinline__ uint32_t xcd_order(uint32_t swz) { return xcd_order_of(blockIdx.x, gridDim.x, swz); }
-
-// Workgroup wg of a virtual grid of G (a persistent grid walks wg = blockIdx.x, + gridDim.x, ...;
-// gridDim.x a multiple of 8 keeps every virtual workgroup on its physical one's XCD).
-template <class Body>
-__device__ __forceinline__ void for_virtual_blocks(uint32_t vgrid, Body body) {
-    const uint32_t G = vgrid ? vgrid : gridDim.x;
-    for (uint32_t wg = blockIdx.x; wg < G; wg += gridDim.x) body(wg, G);
-}
+__device__ __forceinline__ uint32_t xcd_order() { return xcd_order_of(blockIdx.x, gridDim.x); }
 
 struct Idx {
     uint32_t a, b, c;
@@ -86,21 +70,6 @@ __device__ __forceinline__ uint32_t word_of(const uint4& v, int d) {
     return d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
 }
 
-// Store the first nb (< 16) bytes of v, byte-exact.
-__device__ __forceinline__ void st_partial(uint8_t* p, const uint4& v, uint32_t nb) {
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        const uint32_t w = word_of(v, d);
-        if (4u * d + 4u <= nb) {
-            *reinterpret_cast<uint32_t*>(p + 4 * d) = w;
-        } else if (4u * d < nb) {
-            const uint32_t rem = nb - 4u * d;
-            if (rem >= 2) *reinterpret_cast<uint16_t*>(p + 4 * d) = (uint16_t)w;
-            if (rem & 1) p[4 * d + (rem & 2)] = (uint8_t)(w >> (8 * (rem & 2)));
-        }
-    }
-}
-
 // Keep only the first nb bytes of v (zero the rest).
 __device__ __forceinline__ uint4 keep_bytes(const uint4& v, uint32_t nb) {
     auto m = [nb](int d) -> uint32_t {
@@ -110,18 +79,13 @@ __device__ __forceinline__ uint4 keep_bytes(const uint4& v, uint32_t nb) {
     return make_uint4(v.x & m(0), v.y & m(1), v.z & m(2), v.w & m(3));
 }
 
-// Store one output chunk holding nb valid bytes. A partial tail chunk is either one full
-// 16-byte store with the bytes past nb zeroed (pad_zero: the slot padding up to the 16-byte
-// boundary is written as zeros, which avoids partially written cache lines) or a byte-exact
-// partial store.
+// Store one output chunk holding nb valid bytes. A partial tail chunk is one full 16-byte store
+// with the bytes past nb zeroed: the slot padding up to the 16-byte boundary is written as zeros
+// ("Whole-chunk outputs"), which avoids partially written cache lines (+3-4 %
+// encode, +1 % decode against byte-exact partial stores).
 template <bool NT>
-__device__ __forceinline__ void store_chunk(uint8_t* p, const uint4& v, uint32_t nb, uint32_t pad_zero) {
-    if (nb >= 16)
-        st16<NT>(p, v);
-    else if (pad_zero)
-        st16<NT>(p, keep_bytes(v, nb));
-    else
-        st_partial(p, v, nb);
+__device__ __forceinline__ void store_chunk(uint8_t* p, const uint4& v, uint32_t nb) {
+    st16<NT>(p, nb >= 16 ? v : keep_bytes(v, nb));
 }
 
 // a ^ b ^ c in one VALU op. gfx950 has no v_xor3_b32; v_bitop3_b32 with truth table 0x96 is

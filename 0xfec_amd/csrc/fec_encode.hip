@@ -1,6 +1,6 @@
-// fec_encode.hip — RS encode kernels for gfx950 (reed_solomon.go:51 Encode): generic (k, m),
-// fixed compile-time shapes (RS(2,3), RS(8,12), RS(16,24)) with the dyadic split-recursive body,
-// and the persistent ticket-queue form (knob enc_queue). See fec_kernels.hip for the overview.
+// fec_encode.hip — RS encode kernels for gfx950 (reed_solomon.go:51 Encode): generic (k, m), RS(8,12)
+// by the dyadic split-recursive body, RS(16,24) / RS(20,30) by the bit-sliced XOR network (RS(2,3):
+// fec_encode23.hip). See fec_kernels.hip for the overview.
 #include "fec_device.hpp"
 
 namespace fk {
@@ -8,11 +8,11 @@ namespace fk {
 // ------------------------------------------------------------------ RS encode
 // One lane = one 16-byte column chunk of one block; all m parities accumulate in VGPRs.
 // Inputs are loaded 8 shards at a time (clamped, so loads are never predicated), then
-// each input updates every parity accumulator with its LDS-broadcast PermTab.
-// POL: bit 0 non-temporal loads, bit 1 non-temporal stores.
-template <int MAXM, bool LDS_TABS, int POL>
+// each input updates every parity accumulator with its LDS-broadcast PermTab. Non-temporal loads
+// and stores (+2-5 %).
+template <int MAXM, bool LDS_TABS>
 __global__ __launch_bounds__(kThreads) void rs_encode_kernel(EncodeArgs a) {
-    constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
+    constexpr bool NTL = true, NTS = true;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const gf::PermTab* tabs;
     if constexpr (LDS_TABS) {
@@ -26,9 +26,9 @@ __global__ __launch_bounds__(kThreads) void rs_encode_kernel(EncodeArgs a) {
     }
     const uint32_t k = a.k, m = a.m;
     const uint32_t stride = gridDim.x * kThreads;
-    for (uint32_t item = xcd_order(a.swz) * kThreads + threadIdx.x; item < a.total; item += stride) {
+    for (uint32_t item = xcd_order() * kThreads + threadIdx.x; item < a.total; item += stride) {
         const uint32_t b = fdiv(item, a.div_cps);
-        const uint32_t c = rotate_chunk(item - b * a.cps, a.cps, a.rot);
+        const uint32_t c = item - b * a.cps;
         const uint8_t* src = a.in + (uint64_t)b * a.in_bs + (uint64_t)c * kChunk;
         uint32_t acc[MAXM][4];
 #pragma unroll
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(kThreads) void rs_encode_kernel(EncodeArgs a) {
         const uint32_t nb = a.len - c * kChunk;
 #pragma unroll
         for (int r = 0; r < MAXM; ++r)
-            if (r < (int)m) store_chunk<NTS>(dst + (uint64_t)r * a.ss, as_uint4(acc[r]), nb, a.pad_zero);
+            if (r < (int)m) store_chunk<NTS>(dst + (uint64_t)r * a.ss, as_uint4(acc[r]), nb);
     }
 }
 
@@ -130,241 +130,62 @@ __device__ __forceinline__ void dy_conv(const Idx (*D)[NC], const gf::PermTab* T
 }
 
 // ------------------------------------------------------------------ RS encode, fixed shape
-// The code shapes the reference benchmarks, with K and M compile-time: one lane = one 16-byte
-// column chunk, the K loads issued back to back, inputs folded in pairs (mac2), no runtime
-// guards. Tail chunks are stored whole with the pad bytes zeroed.
-template <int K, int M, int POL>
-struct FixedEncode {
-    static constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
-    const EncodeArgs& a;
-    const gf::PermTab* T;
-
-    __device__ __forceinline__ void load(uint4 (&x)[K], uint32_t it) const {
-        const uint32_t b = fdiv(it, a.div_cps);
-        const uint32_t c = it - b * a.cps;
-        const uint8_t* src = a.in + (uint64_t)b * a.in_bs + (uint64_t)c * kChunk;
-#pragma unroll
-        for (int j = 0; j < K; ++j) x[j] = ld16<NTL>(src + (uint64_t)j * a.ss);
-    }
-
-    __device__ __forceinline__ void compute_store(const uint4 (&x)[K], uint32_t it) const {
-        // opaque zero: keeps the table reads next to their use (hoisted out of a loop they
-        // would hold 5*M*K VGPRs)
-        uint32_t toff = 0;
-        asm volatile("" : "+s"(toff));
-        const gf::PermTab* t = T + toff;
-        uint32_t acc[M][4];
-#pragma unroll
-        for (int r = 0; r < M; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0;
-        if constexpr ((POL & 4) != 0) {   // diagnostics (knob enc_diag): traffic only, no field math
-#pragma unroll
-            for (int j = 0; j < K; ++j)
-#pragma unroll
-                for (int d = 0; d < 4; ++d) acc[j % M][d] ^= word_of(x[j], d);
-        } else if constexpr ((POL & 8) != 0) {   // dyadic code: T holds the leaf tables
-            constexpr int B = M == 1 ? 0 : M == 2 ? 1 : M == 4 ? 2 : M == 8 ? 3 : 4;
-            constexpr int L = Pow3<B>::v;
-            constexpr int NC = K >= 16 ? 1 : 4;   // dword columns per pass (registers)
-#pragma unroll
-            for (int c0 = 0; c0 < 4; c0 += NC) {
-                // opaque zero per pass: the table reads stay in their pass (shared across
-                // passes they would be hoisted and held: 5 VGPRs per leaf)
-                uint32_t poff = 0;
-                asm volatile("" : "+s"(poff));
-                const gf::PermTab* tp = t + poff;
-#pragma unroll
-                for (int h = 0; h < K / M; ++h) {
-                    Idx D[M][NC];
-#pragma unroll
-                    for (int v = 0; v < M; ++v)
-#pragma unroll
-                        for (int c = 0; c < NC; ++c) D[v][c] = split(word_of(x[h * M + v], c0 + c));
-                    uint32_t Y[M][NC];
-                    dy_conv<B, NC>(D, tp + h * L, Y);
-#pragma unroll
-                    for (int i = 0; i < M; ++i)
-#pragma unroll
-                        for (int c = 0; c < NC; ++c) acc[i][c0 + c] = h ? acc[i][c0 + c] ^ Y[i][c] : Y[i][c];
-                }
-            }
-        } else
-#pragma unroll
-        for (int j = 0; j < K; j += 2) {
-            Idx ia[4], ib[4];
-            split4(ia, x[j]);
-            if (j + 1 < K) split4(ib, x[j + 1 < K ? j + 1 : j]);
-#pragma unroll
-            for (int r = 0; r < M; ++r) {
-                if (j + 1 < K) mac2(acc[r], ia, ib, t + r * K + j, t + r * K + j + 1);
-                else mac1(acc[r], ia, t + r * K + j);
-            }
-        }
-        const uint32_t b = fdiv(it, a.div_cps);
-        const uint32_t c = it - b * a.cps;
-        uint8_t* dst = a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk;
-        const uint32_t nb = min(a.len - c * kChunk, (uint32_t)kChunk);
-#pragma unroll
-        for (int r = 0; r < M; ++r) st16<NTS>(dst + (uint64_t)r * a.ss, keep_bytes(as_uint4(acc[r]), nb));
-    }
-};
-
+// RS(8,12), the headline code, with K and M compile-time and the dyadic body: one lane = one
+// 16-byte column chunk, the K loads issued back to back, no runtime guards; the workgroup stages
+// the leaf tables (dyadic_leaves(), fec_capi.cpp) in LDS. Non-temporal loads and stores. Tail
+// chunks are stored whole with the pad bytes zeroed.
 template <int K, int M>
-__device__ __forceinline__ const gf::PermTab* stage_tabs(uint8_t* smem, const uint32_t* tabs) {
-    uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
-    for (uint32_t i = threadIdx.x; i < (uint32_t)(M * K * 8); i += kThreads) dst[i] = tabs[i];
-    __syncthreads();
-    return reinterpret_cast<const gf::PermTab*>(smem);
-}
-
-// Flat launch: one item per lane, XCD-contiguous workgroup order. POL bit 4 (knob enc_early): the
-// table words' loads go out first, then the item's K shard loads, and the tables reach LDS behind an
-// LDS-only barrier, so the shard loads are in flight while the tables stage (without it the
-// workgroup's __syncthreads waits for the table loads before any shard load is issued: one memory
-// round trip per workgroup, which a 40-us RS(2,3) launch of ~20 000 workgroups feels).
-template <int K, int M, int POL>
 __global__ __launch_bounds__(kThreads) void rs_encode_fixed_kernel(EncodeArgs a) {
+    static_assert((K & (K - 1)) == 0 && (M & (M - 1)) == 0 && M <= K, "dyadic codes: powers of two, m <= k");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t it = xcd_order(a.swz) * kThreads + threadIdx.x;
-    if constexpr ((POL & 16) != 0) {
-        constexpr uint32_t W = M * K * 8, R = (W + kThreads - 1) / kThreads;   // table dwords, per lane
-        uint32_t tw[R];
-#pragma unroll
-        for (uint32_t q = 0; q < R; ++q) {
-            const uint32_t i = threadIdx.x + q * kThreads;
-            tw[q] = i < W ? a.tabs[i] : 0u;
-        }
-        const FixedEncode<K, M, POL> f{a, reinterpret_cast<const gf::PermTab*>(smem)};
-        uint4 x[K];
-        if (it < a.total) f.load(x, it);
-#pragma unroll
-        for (uint32_t q = 0; q < R; ++q) {
-            const uint32_t i = threadIdx.x + q * kThreads;
-            if (i < W) reinterpret_cast<uint32_t*>(smem)[i] = tw[q];
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (it >= a.total) return;
-        f.compute_store(x, it);
-    } else {
-        const FixedEncode<K, M, POL> f{a, stage_tabs<K, M>(smem, a.tabs)};
-        if (it >= a.total) return;
-        uint4 x[K];
-        f.load(x, it);
-        f.compute_store(x, it);
+    {
+        uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
+        for (uint32_t i = threadIdx.x; i < (uint32_t)(M * K * 8); i += kThreads) dst[i] = a.dytabs[i];
+        __syncthreads();
     }
-}
-
-// Persistent ticket-queue launch (the default for the fixed shapes). The items are split into
-// 8 contiguous ranges; the workgroups with blockIdx % 8 == x own range x (the grid is a multiple
-// of 8, so every range has owners: correctness never depends on placement) and draw 256-item
-// chunks of it in order from ticket counter x. Round-robin dispatch puts those workgroups on one
-// XCD, so each XCD streams one compact window of addresses: measured as fast as a flat grid for
-// pure traffic, where a static persistent sweep lets the windows drift apart and loses ~20 %
-// (tools/mix_probe.py persist). Each lane loads its next chunk's K inputs and draws the ticket
-// after it before it computes and stores the current chunk (ping-pong register sets), so two
-// resident workgroups per CU keep HBM busy while the field arithmetic runs.
-template <int K, int M, int POL, int D>
-__global__ __launch_bounds__(kThreads) void rs_encode_queue_kernel(EncodeArgs a) {
-    static_assert(D == 1 || D == 2, "prefetch depth");
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    // tk[2..2+D]: the first D+1 tickets (never rewritten); tk[t & 1]: the ticket drawn in stage
-    // t, read after that stage's barrier and rewritten two stages later, after a barrier every
-    // reader has passed
-    __shared__ uint32_t tk[2 + D + 1];
-    uint32_t* ctr = a.ctr + (blockIdx.x & 7u) * kCtrStride;
-    if (threadIdx.x == 0)
-        for (int i = 0; i <= D; ++i) tk[2 + i] = atomicAdd(ctr, 1u);
-    const FixedEncode<K, M, POL> f{a, stage_tabs<K, M>(smem, a.tabs)};   // barrier inside
-    const uint32_t lo = (blockIdx.x & 7u) * a.per_xcd;
-    const uint32_t hi = min(a.total, lo + a.per_xcd);
-    // chunk bases in flight (uniform over the workgroup): q[0] is computed, q[D] is loaded next
-    uint32_t q[D + 1];
+    const uint32_t it = xcd_order() * kThreads + threadIdx.x;
+    if (it >= a.total) return;
+    const uint32_t b = fdiv(it, a.div_cps);
+    const uint32_t c = it - b * a.cps;
+    const uint8_t* src = a.in + (uint64_t)b * a.in_bs + (uint64_t)c * kChunk;
+    uint4 x[K];
 #pragma unroll
-    for (int i = 0; i <= D; ++i) q[i] = lo + tk[2 + i] * kThreads;
-    const uint32_t last = hi - 1;           // loads clamp to the range's last item
-    const uint32_t lane = threadIdx.x;
-    uint4 xs[D + 1][K];
-    // one stage: draw the ticket D+1 chunks ahead, issue the loads of chunk q[D], compute and
-    // store chunk q[0], publish the ticket. The barrier waits for LDS only (HIP's __syncthreads
-    // would also drain vmcnt, i.e. wait for the prefetched loads).
-    auto stage = [&](uint4 (&now)[K], uint4 (&fill)[K], uint32_t slot) {
-        uint32_t drawn = 0;
-        if (lane == 0) drawn = atomicAdd(ctr, 1u);
-        f.load(fill, min(q[D] + lane, last));   // clamped: unconditional, no merge of old values
-        if (q[0] + lane < hi) f.compute_store(now, q[0] + lane);
-        if (lane == 0) tk[slot] = drawn;
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    for (int j = 0; j < K; ++j) x[j] = ld16<true>(src + (uint64_t)j * a.ss);
+    // opaque zero: keeps the table reads next to their use (hoisted out of a loop they would hold
+    // 5*M*K VGPRs)
+    uint32_t toff = 0;
+    asm volatile("" : "+s"(toff));
+    const gf::PermTab* t = reinterpret_cast<const gf::PermTab*>(smem) + toff;
+    uint32_t acc[M][4];
+    constexpr int B = M == 1 ? 0 : M == 2 ? 1 : M == 4 ? 2 : M == 8 ? 3 : 4;
+    constexpr int L = Pow3<B>::v;
+    constexpr int NC = K >= 16 ? 1 : 4;   // dword columns per pass (registers)
 #pragma unroll
-        for (int i = 0; i < D; ++i) q[i] = q[i + 1];
-        q[D] = lo + tk[slot] * kThreads;
-    };
-    if (q[0] < hi) {
+    for (int c0 = 0; c0 < 4; c0 += NC) {
+        // opaque zero per pass: the table reads stay in their pass (shared across passes they
+        // would be hoisted and held: 5 VGPRs per leaf)
+        uint32_t poff = 0;
+        asm volatile("" : "+s"(poff));
+        const gf::PermTab* tp = t + poff;
 #pragma unroll
-        for (int i = 0; i < D; ++i) f.load(xs[i], min(q[i] + lane, last));
-        if constexpr (D == 1) {
-            while (q[0] < hi) {
-                stage(xs[0], xs[1], 0);
-                if (q[0] >= hi) break;
-                stage(xs[1], xs[0], 1);
-            }
-        } else {
-            while (q[0] < hi) {
-                stage(xs[0], xs[2], 0);
-                if (q[0] >= hi) break;
-                stage(xs[1], xs[0], 1);
-                if (q[0] >= hi) break;
-                stage(xs[2], xs[1], 0);
-                if (q[0] >= hi) break;
-                stage(xs[0], xs[2], 1);
-                if (q[0] >= hi) break;
-                stage(xs[1], xs[0], 0);
-                if (q[0] >= hi) break;
-                stage(xs[2], xs[1], 1);
-            }
+        for (int h = 0; h < K / M; ++h) {
+            Idx D[M][NC];
+#pragma unroll
+            for (int v = 0; v < M; ++v)
+#pragma unroll
+                for (int cc = 0; cc < NC; ++cc) D[v][cc] = split(word_of(x[h * M + v], c0 + cc));
+            uint32_t Y[M][NC];
+            dy_conv<B, NC>(D, tp + h * L, Y);
+#pragma unroll
+            for (int i = 0; i < M; ++i)
+#pragma unroll
+                for (int cc = 0; cc < NC; ++cc) acc[i][c0 + cc] = h ? acc[i][c0 + cc] ^ Y[i][cc] : Y[i][cc];
         }
     }
-    // The last workgroup to finish rewinds the counters for the next launch on this stream
-    // (every workgroup's draws precede its arrival, released by the fence).
-    if (threadIdx.x == 0) {
-        __threadfence();
-        uint32_t* done = a.ctr + 8 * kCtrStride;
-        if (atomicAdd(done, 1u) == gridDim.x - 1) {
-            for (int x = 0; x < 8; ++x) atomicExch(a.ctr + x * kCtrStride, 0u);
-            atomicExch(done, 0u);
-        }
-    }
-}
-
-// Ticket queue without prefetch (prefetch depth 0): draw, barrier, load, compute, store.
-// DRAIN: the barrier is HIP's __syncthreads, which also waits for the workgroup's stores.
-template <int K, int M, int POL, bool DRAIN>
-__global__ __launch_bounds__(kThreads) void rs_encode_queue0_kernel(EncodeArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ uint32_t tk[2];
-    uint32_t* ctr = a.ctr + (blockIdx.x & 7u) * kCtrStride;
-    const FixedEncode<K, M, POL> f{a, stage_tabs<K, M>(smem, a.tabs)};
-    const uint32_t lo = (blockIdx.x & 7u) * a.per_xcd;
-    const uint32_t hi = min(a.total, lo + a.per_xcd);
-    for (uint32_t t = 0;; ++t) {
-        if (threadIdx.x == 0) tk[t & 1] = atomicAdd(ctr, 1u);
-        if constexpr (DRAIN) __syncthreads();
-        else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        const uint32_t base = lo + tk[t & 1] * kThreads;
-        if (base >= hi) break;
-        const uint32_t it = base + threadIdx.x;
-        if (it < hi) {
-            uint4 x[K];
-            f.load(x, it);
-            f.compute_store(x, it);
-        }
-    }
-    if (threadIdx.x == 0) {
-        __threadfence();
-        uint32_t* done = a.ctr + 8 * kCtrStride;
-        if (atomicAdd(done, 1u) == gridDim.x - 1) {
-            for (int x = 0; x < 8; ++x) atomicExch(a.ctr + x * kCtrStride, 0u);
-            atomicExch(done, 0u);
-        }
-    }
+    uint8_t* dst = a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk;
+    const uint32_t nb = min(a.len - c * kChunk, (uint32_t)kChunk);
+#pragma unroll
+    for (int r = 0; r < M; ++r) st16<true>(dst + (uint64_t)r * a.ss, keep_bytes(as_uint4(acc[r]), nb));
 }
 
 // ------------------------------------------------------------------ RS encode, bit-sliced
@@ -406,25 +227,14 @@ __device__ __forceinline__ void bit_transpose8(uint32_t (&w)[8]) {
     delta_swap8<1>(w);
 }
 
-// Group GI of the network: transpose the group's raw chunks into planes, fold them into y.
-// STREAM: the next group's loads are issued first, behind an opaque dependence on the previous
-// group's last output, so only two groups of inputs are ever held (fewer VGPRs, more waves) and
-// every wave keeps loads in flight while it computes.
-template <int K, int M, int POL, bool STREAM, int GI>
+// Group GI of the network: transpose the group's raw chunks into planes, fold them into y, then
+// load the next group (streaming the next group's loads ahead of this one's network measured -0.2 %,
+// r02).
+template <int K, int M, int GI>
 __device__ __forceinline__ void bs_stream(const uint8_t* s0, const uint8_t* s1, uint64_t ss,
                                           uint4 (&cur)[BsShape<K, M>::G][2], uint32_t (&y)[M][8]) {
     constexpr int G = BsShape<K, M>::G, NG = K / G;
-    constexpr bool NTL = POL & 1;
     uint4 nxt[G][2];
-    if constexpr (STREAM && GI + 1 < NG) {
-        uint64_t off = (uint64_t)(GI + 1) * G * ss;
-        if constexpr (GI > 0) asm volatile("" : "+v"(off) : "v"(y[M - 1][7]));
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-            nxt[j][0] = ld16<NTL>(s0 + off + (uint64_t)j * ss);
-            nxt[j][1] = ld16<NTL>(s1 + off + (uint64_t)j * ss);
-        }
-    }
     uint32_t x[G][8];
 #pragma unroll
     for (int j = 0; j < G; ++j) {
@@ -434,26 +244,24 @@ __device__ __forceinline__ void bs_stream(const uint8_t* s0, const uint8_t* s1, 
     }
     bs_grp<K, M, GI>(x, y);
     if constexpr (GI + 1 < NG) {
-        if constexpr (!STREAM) {
 #pragma unroll
-            for (int j = 0; j < G; ++j) {
-                nxt[j][0] = ld16<NTL>(s0 + (uint64_t)((GI + 1) * G + j) * ss);
-                nxt[j][1] = ld16<NTL>(s1 + (uint64_t)((GI + 1) * G + j) * ss);
-            }
+        for (int j = 0; j < G; ++j) {
+            nxt[j][0] = ld16<true>(s0 + (uint64_t)((GI + 1) * G + j) * ss);
+            nxt[j][1] = ld16<true>(s1 + (uint64_t)((GI + 1) * G + j) * ss);
         }
-        bs_stream<K, M, POL, STREAM, GI + 1>(s0, s1, ss, nxt, y);
+        bs_stream<K, M, GI + 1>(s0, s1, ss, nxt, y);
     }
 }
 
-template <int K, int M, int POL>
+template <int K, int M>
 __global__ __launch_bounds__(kThreads) void rs_encode_bits_kernel(EncodeArgs a) {
-    constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
+    constexpr bool NTL = true, NTS = true;
     // A wave takes 128 consecutive (block, chunk) items: lane l items w*128 + l and w*128 + 64 + l,
     // so each load and store instruction covers 64 consecutive chunks, as in the one-chunk
     // kernels. The two chunks of a lane may belong to different blocks: the network treats every
     // byte column alike.
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t f0 = (xcd_order(a.swz) * kThreads + (threadIdx.x & ~63u)) * 2u + lane;
+    const uint32_t f0 = (xcd_order() * kThreads + (threadIdx.x & ~63u)) * 2u + lane;
     if (f0 >= a.total) return;
     const uint32_t f1 = f0 + 64u;
     const bool two = f1 < a.total;
@@ -470,7 +278,7 @@ __global__ __launch_bounds__(kThreads) void rs_encode_bits_kernel(EncodeArgs a) 
         g0[j][1] = ld16<NTL>(s1 + (uint64_t)j * a.ss);
     }
     uint32_t y[M][8];
-    bs_stream<K, M, POL, (POL & 16) != 0, 0>(s0, s1, a.ss, g0, y);
+    bs_stream<K, M, 0>(s0, s1, a.ss, g0, y);
     uint8_t* d0 = a.out + (uint64_t)b0 * a.out_bs + (uint64_t)c0 * kChunk;
     uint8_t* d1 = a.out + (uint64_t)b1 * a.out_bs + (uint64_t)c1 * kChunk;
     const uint32_t nb0 = min(a.len - c0 * kChunk, (uint32_t)kChunk);
@@ -487,33 +295,23 @@ template <int K, int M>
 static hipError_t enc_bits_dispatch(const EncodeArgs& a, hipStream_t s) {
     const int grid = (int)((a.total + 2 * kThreads - 1) / (2 * kThreads));
     if (grid == 0) return hipSuccess;
-    const size_t lds = occupancy_lds(g_tune.enc_bwpc, 0);
-    const bool nt = g_tune.enc_nt & 1, stream = g_tune.enc_bits & 4;
-    if (stream && nt) hipLaunchKernelGGL((rs_encode_bits_kernel<K, M, 19>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (stream) hipLaunchKernelGGL((rs_encode_bits_kernel<K, M, 18>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (nt) hipLaunchKernelGGL((rs_encode_bits_kernel<K, M, 3>), dim3(grid), dim3(kThreads), lds, s, a);
-    else hipLaunchKernelGGL((rs_encode_bits_kernel<K, M, 2>), dim3(grid), dim3(kThreads), lds, s, a);
+    hipLaunchKernelGGL((rs_encode_bits_kernel<K, M>), dim3(grid), dim3(kThreads), occupancy_lds(g_tune.enc_bwpc, 0), s,
+                       a);
     return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ launchers
-template <int MAXM, int POL>
-static hipError_t enc_dispatch2(const EncodeArgs& a, int grid, hipStream_t s) {
+template <int MAXM>
+static hipError_t enc_dispatch(const EncodeArgs& a, int grid, hipStream_t s) {
     const bool lds_tabs = a.m * a.k <= (uint32_t)kMaxLdsTabs;
     if (lds_tabs) {
         const size_t lds = occupancy_lds(g_tune.gen_wpc, (size_t)a.m * a.k * sizeof(gf::PermTab));
-        hipLaunchKernelGGL((rs_encode_kernel<MAXM, true, POL>), dim3(grid), dim3(kThreads), lds, s, a);
+        hipLaunchKernelGGL((rs_encode_kernel<MAXM, true>), dim3(grid), dim3(kThreads), lds, s, a);
     } else {
         const size_t lds = occupancy_lds(g_tune.gen_wpc, 0);
-        hipLaunchKernelGGL((rs_encode_kernel<MAXM, false, POL>), dim3(grid), dim3(kThreads), lds, s, a);
+        hipLaunchKernelGGL((rs_encode_kernel<MAXM, false>), dim3(grid), dim3(kThreads), lds, s, a);
     }
     return hipGetLastError();
-}
-
-template <int MAXM>
-static hipError_t enc_dispatch(const EncodeArgs& a, int grid, hipStream_t s) {
-    // cache policy: plain, or non-temporal loads and stores (the mixed forms measured no better)
-    return (g_tune.enc_nt & 3) ? enc_dispatch2<MAXM, 3>(a, grid, s) : enc_dispatch2<MAXM, 0>(a, grid, s);
 }
 
 hipError_t launch_rs_encode(const EncodeArgs& a, int grid, hipStream_t s) {
@@ -524,87 +322,27 @@ hipError_t launch_rs_encode(const EncodeArgs& a, int grid, hipStream_t s) {
     return enc_dispatch<16>(a, grid, s);   // caller splits m > 16
 }
 
-// (k, m) shapes with a fixed-shape encode instance: the reference's benchmark codes RS(2,3),
-// RS(8,12), RS(16,24), and (bit-sliced) its sender's RS(20,30). Any other shape runs the
-// generic kernel.
-bool fixed_encode_applies(uint32_t k, uint32_t m) {
+// (k, m) shapes with an encode of their own: the reference's benchmark codes RS(2,3) (its parity
+// row, fec_encode23.hip), RS(8,12) (dyadic), RS(16,24) and its sender's RS(20,30) (bit-sliced).
+// Any other shape runs the generic kernel.
+bool fixed_encode_applies(uint32_t k, uint32_t m, bool dyadic) {
     if (!g_tune.enc_fixed) return false;
-    return (k == 2 && m == 1) || (k == 8 && m == 4) || (k == 16 && m == 8) ||
-           (k == 20 && m == 10 && (g_tune.enc_bits & 8));   // bit-sliced only
+    return rs_encode23_applies(k, m) || (k == 8 && m == 4 && dyadic) || (k == 16 && m == 8) || (k == 20 && m == 10);
 }
 
-template <int K, int M>
-static hipError_t enc_fixed_dispatch(const EncodeArgs& a, int grid, size_t lds, bool queue, hipStream_t s) {
-    if (queue) {
-        if (g_tune.enc_qdepth == 0 && g_tune.enc_diag)
-            hipLaunchKernelGGL((rs_encode_queue0_kernel<K, M, 7, true>), dim3(grid), dim3(kThreads), lds, s, a);
-        else if (g_tune.enc_qdepth == 0)
-            hipLaunchKernelGGL((rs_encode_queue0_kernel<K, M, 3, true>), dim3(grid), dim3(kThreads), lds, s, a);
-        else if (g_tune.enc_qdepth < 0)
-            hipLaunchKernelGGL((rs_encode_queue0_kernel<K, M, 3, false>), dim3(grid), dim3(kThreads), lds, s, a);
-        else if (g_tune.enc_diag)
-            hipLaunchKernelGGL((rs_encode_queue_kernel<K, M, 7, 1>), dim3(grid), dim3(kThreads), lds, s, a);
-        else if (g_tune.enc_qdepth >= 2 && K <= 8)   // K = 16 at depth 2 exceeds the register file
-            hipLaunchKernelGGL((rs_encode_queue_kernel<K, M, 3, (K <= 8 ? 2 : 1)>), dim3(grid), dim3(kThreads), lds, s, a);
-        else
-            hipLaunchKernelGGL((rs_encode_queue_kernel<K, M, 3, 1>), dim3(grid), dim3(kThreads), lds, s, a);
-    } else if (g_tune.enc_dyadic && a.dytabs && K >= 4) {
-        EncodeArgs d = a;
-        d.tabs = a.dytabs;
-        if ((g_tune.enc_early == 1 || (g_tune.enc_early == 2 && K == 2)) && (g_tune.enc_nt & 1))
-            hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 27>), dim3(grid), dim3(kThreads), lds, s, d);
-        else if (g_tune.enc_nt & 1)
-            hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 11>), dim3(grid), dim3(kThreads), lds, s, d);
-        else
-            hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 10>), dim3(grid), dim3(kThreads), lds, s, d);
-    } else {
-        if ((g_tune.enc_early == 1 || (g_tune.enc_early == 2 && K == 2)) && (g_tune.enc_nt & 1))
-            hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 19>), dim3(grid), dim3(kThreads), lds, s, a);
-        else if (g_tune.enc_nt & 1)
-            hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 3>), dim3(grid), dim3(kThreads), lds, s, a);
-        else
-            hipLaunchKernelGGL((rs_encode_fixed_kernel<K, M, 2>), dim3(grid), dim3(kThreads), lds, s, a);
+hipError_t launch_rs_encode_fixed(const EncodeArgs& a, hipStream_t s) {
+    if (a.total == 0) return hipSuccess;
+    if (rs_encode23_applies(a.k, a.m)) return launch_rs_encode23(a, s);
+    if (a.k == 16 && a.m == 8) return enc_bits_dispatch<16, 8>(a, s);
+    if (a.k == 20 && a.m == 10) return enc_bits_dispatch<20, 10>(a, s);
+    if (a.k == 8 && a.m == 4 && a.dytabs) {
+        // 3 workgroups per CU (knob enc_wpc; DESIGN.md 3: the flat grid at 3 beats 2, 4 and uncapped)
+        const int grid = (int)((a.total + kThreads - 1) / kThreads);
+        const size_t lds = occupancy_lds(g_tune.enc_wpc, (size_t)a.m * a.k * sizeof(gf::PermTab));
+        hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4>), dim3(grid), dim3(kThreads), lds, s, a);
+        return hipGetLastError();
     }
-    return hipGetLastError();
-}
-
-hipError_t launch_rs_encode_fixed(EncodeArgs a, int ncu, hipStream_t s) {
-    const uint32_t chunks = (a.total + kThreads - 1) / kThreads;
-    if (chunks == 0) return hipSuccess;
-    // bit-sliced network (knob enc_bits: bit 0 RS(16,24), bit 1 RS(8,12), bit 2 streamed loads,
-    // bit 3 RS(20,30), the reference's own sender code, manager.go:80)
-    if (a.k == 16 && a.m == 8 && (g_tune.enc_bits & 1)) return enc_bits_dispatch<16, 8>(a, s);
-    if (a.k == 8 && a.m == 4 && (g_tune.enc_bits & 2)) return enc_bits_dispatch<8, 4>(a, s);
-    if (a.k == 20 && a.m == 10 && (g_tune.enc_bits & 8)) return enc_bits_dispatch<20, 10>(a, s);
-    // Per shape (measured): RS(8,12) and RS(16,24) run the flat grid at
-    // g_tune.enc_wpc (3) workgroups per CU; RS(2,3) (2 loads per lane: little in flight per
-    // wave) at full residency. The ticket-queue form stays selectable (enc_queue).
-    const bool queue = g_tune.enc_queue && a.ctr != nullptr && a.k == 8;
-    int grid = (int)chunks;
-    int wpc = a.k == 2 ? 0 : g_tune.enc_wpc;
-    if (queue) {
-        wpc = g_tune.enc_qwpc > 0 ? g_tune.enc_qwpc : 2;
-        grid = ncu * wpc;
-        // no more owners per range than the range has chunks; a multiple of 8 (every range owned)
-        const int per_range = (int)((chunks + 7) / 8);
-        grid = std::min(grid / 8, per_range) * 8;
-        if (grid < 8) grid = 8;
-        a.per_xcd = ((a.total + 7) / 8 + kThreads - 1) / kThreads * kThreads;
-    }
-    const size_t lds = occupancy_lds(wpc, (size_t)a.m * a.k * sizeof(gf::PermTab));
-    if (!queue && rs_encode23_applies(a.k, a.m)) return launch_rs_encode23(a, s);
-    if (a.k == 2 && a.m == 1) return enc_fixed_dispatch<2, 1>(a, grid, lds, queue, s);
-    if (a.k == 8 && a.m == 4) return enc_fixed_dispatch<8, 4>(a, grid, lds, queue, s);
-    if (a.k == 16 && a.m == 8) return enc_fixed_dispatch<16, 8>(a, grid, lds, queue, s);
     return hipErrorInvalidValue;
-}
-
-const void* encode_occupancy_kernel(uint32_t sel) {
-    if (sel <= 1) return (const void*)rs_encode_kernel<1, true, 3>;
-    if (sel <= 2) return (const void*)rs_encode_kernel<2, true, 3>;
-    if (sel <= 4) return (const void*)rs_encode_kernel<4, true, 3>;
-    if (sel <= 8) return (const void*)rs_encode_kernel<8, true, 3>;
-    return (const void*)rs_encode_kernel<16, true, 3>;
 }
 
 }  // namespace fk

@@ -12,11 +12,12 @@
 //   * decode solves only the e x e system of the erased data shards per block
 //     (rs_plan_kernel), which is the same linear solution klauspost computes from the
 //     full k x k inverse of the first k present rows.
-// Grid shapes, non-temporal access and tail-store form were chosen by measurement
-// (tools/kbench.py; DESIGN.md "Kernel tuning").
+// Grid shapes, non-temporal access and tail-store form were chosen by measurement (DESIGN.md
+// "Kernel tuning").
 //
-// The kernels live in fec_encode.hip, fec_decode.hip and fec_xor.hip (compiled as separate
-// translation units, in parallel); this file holds the process-wide tuning and the host helpers.
+// The kernels live in fec_encode*.hip, fec_decode.hip, fec_plan.hip, fec_rebuild.hip,
+// fec_recover.hip and fec_xor.hip (separate translation units, compiled in parallel); this file
+// holds the process-wide tuning and the host helpers.
 #include <hip/hip_runtime.h>
 
 #include <map>
@@ -62,29 +63,6 @@ int resident_per_cu(const void* kernel, size_t lds) {
     }
     cache[{kernel, lds}] = per;
     return per;
-}
-
-int flat_or_persistent(ReconArgs* a, const void* kernel, size_t lds, int flat) {
-    a->vgrid = 0;
-    if (!a->persist_ncu || flat <= 8) return flat;
-    int g = resident_per_cu(kernel, lds) * (int)a->persist_ncu;
-    g = std::max(8, g & ~7);
-    if (g >= flat) return flat;
-    a->vgrid = (uint32_t)flat;
-    return g;
-}
-
-int occupancy_grid(int device, int which, uint32_t sel, size_t lds) {
-    int ncu = 0;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0)
-        ncu = 256;
-    int per = 0;
-    const void* fn = which == 0 ? encode_occupancy_kernel(sel) : which == 1 ? recon_occupancy_kernel(sel)
-                                                                : xor_occupancy_kernel();
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kThreads, lds) != hipSuccess || per <= 0)
-        per = 4;
-    if (per > 8) per = 8;
-    return ncu * per;
 }
 
 }  // namespace fk

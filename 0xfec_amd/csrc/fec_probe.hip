@@ -13,6 +13,10 @@
 //                 per block the first k present shards and one store per erased data shard, in
 //                 block order (the rebuild walks the same blocks in plan order within 64-block
 //                 windows), at the rebuild's residency; no plan kernel
+//   stream        shape-independent reference: nin consecutive shards of each block read, one
+//                 store per block, no masks (the simplest mixed read/write stream of the layout)
+// Every twin takes a residency (workgroups per CU; -1: the twinned kernel's own), so a caller can
+// take each twin's best over residency as the box's ceiling for its access shape.
 #include <string.h>
 
 #include <algorithm>
@@ -28,7 +32,7 @@ namespace {
 template <int K, int M>
 __global__ __launch_bounds__(kThreads) void probe_encode_kernel(EncodeArgs a) {
     extern __shared__ uint8_t smem[];   // residency only, as the encode's staged tables
-    const uint32_t it = xcd_order(a.swz) * kThreads + threadIdx.x;
+    const uint32_t it = xcd_order() * kThreads + threadIdx.x;
     if (it >= a.total) return;
     const uint32_t b = fdiv(it, a.div_cps);
     const uint32_t c = it - b * a.cps;
@@ -50,7 +54,7 @@ __global__ __launch_bounds__(kThreads) void probe_encode_kernel(EncodeArgs a) {
     const uint32_t nb = min(a.len - c * kChunk, (uint32_t)kChunk);
 #pragma unroll
     for (int r = 0; r < M; ++r) st16<true>(dst + (uint64_t)r * a.ss, keep_bytes(acc[r], nb));
-    if (a.pad_zero == 0x5A5A5A5Au) smem[0] = 1;   // never: keeps the LDS allocation
+    if (a.k == 0x5A5A5A5Au) smem[0] = 1;   // never: keeps the LDS allocation
 }
 
 struct RecoverProbeArgs {
@@ -59,7 +63,7 @@ struct RecoverProbeArgs {
     uint8_t* out;
     const uint32_t* masks;
     uint64_t dbs, pbs, ss, out_bs;
-    uint32_t len, cps, total, nblocks, swz;
+    uint32_t len, cps, total, nblocks, nin;
     FastDiv div_cps;
 };
 
@@ -67,20 +71,21 @@ template <int K>
 __global__ __launch_bounds__(kThreads) void probe_recover_kernel(RecoverProbeArgs a, uint32_t m) {
     extern __shared__ uint8_t smem[];   // residency only, as the decode's wave slices
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t i0 = xcd_order(a.swz) * kThreads + (wave << 6);
+    const uint32_t i0 = xcd_order() * kThreads + (wave << 6);
     if (i0 >= a.total) return;
-    // the wave's <= 3 block masks in one load, as the direct kernel
+    // the wave's <= 3 block masks by scalar loads, as the direct kernel
     const uint32_t bfirst = fdiv(i0, a.div_cps);
-    const uint32_t nbw = fdiv(min(i0 + 63u, a.total - 1u), a.div_cps) - bfirst + 1;
-    const uint32_t mine = lane < nbw ? a.masks[bfirst + lane] : 0u;
+    typedef __attribute__((address_space(4))) const uint32_t ConstU32;
+    ConstU32* cm = (ConstU32*)a.masks;
+    const uint32_t bf = (uint32_t)__builtin_amdgcn_readfirstlane((int)bfirst), last = a.nblocks - 1;
+    const uint32_t m0 = cm[bf];
+    const uint32_t m1 = cm[(uint32_t)__builtin_amdgcn_readfirstlane((int)min(bf + 1, last))];
+    const uint32_t m2 = cm[(uint32_t)__builtin_amdgcn_readfirstlane((int)min(bf + 2, last))];
     const uint32_t item = i0 + lane;
     if (item >= a.total) return;
     const uint32_t blk = fdiv(item, a.div_cps);
     const uint32_t g = blk - bfirst;
     const uint32_t c = item - blk * a.cps;
-    const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 0);
-    const uint32_t m1 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 1);
-    const uint32_t m2 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 2);
     const uint32_t mask = (g == 0 ? m0 : g == 1 ? m1 : m2) & low_mask(K + m);
     const uint32_t E0 = __ffs(~mask & low_mask(K)) - 1;
     const uint32_t R0 = __ffs(mask >> K) - 1;
@@ -100,13 +105,13 @@ __global__ __launch_bounds__(kThreads) void probe_recover_kernel(RecoverProbeArg
     }
     const uint32_t nb = min(a.len - c * kChunk, (uint32_t)kChunk);
     st16<true>(a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk, keep_bytes(acc, nb));
-    if (a.swz == 0x5A5A5A5Au) smem[0] = 1;   // never: keeps the LDS allocation
+    if (a.nin == 0x5A5A5A5Au) smem[0] = 1;   // never: keeps the LDS allocation
 }
 
 template <int K, int R>
 __global__ __launch_bounds__(kThreads) void probe_rebuild_kernel(RecoverProbeArgs a, uint32_t m) {
     extern __shared__ uint8_t smem[];   // residency only, as the rebuild's table and wave slices
-    const uint32_t item = xcd_order(a.swz) * kThreads + threadIdx.x;
+    const uint32_t item = xcd_order() * kThreads + threadIdx.x;
     if (item >= a.total) return;
     const uint32_t blk = fdiv(item, a.div_cps);
     const uint32_t c = item - blk * a.cps;
@@ -132,7 +137,33 @@ __global__ __launch_bounds__(kThreads) void probe_rebuild_kernel(RecoverProbeArg
 #pragma unroll
     for (int r = 0; r < R; ++r)
         if ((uint32_t)r < e) st16<true>(o + (uint64_t)r * a.ss, keep_bytes(acc, nb));
-    if (a.swz == 0x5A5A5A5Au) smem[0] = 1;   // never: keeps the LDS allocation
+    if (a.nin == 0x5A5A5A5Au) smem[0] = 1;   // never: keeps the LDS allocation
+}
+
+// NIN consecutive shards of the block read (data at stride ss inside the block), their XOR stored
+// once per chunk: the simplest mixed read / write stream of the bench layout.
+template <int NIN>
+__global__ __launch_bounds__(kThreads) void probe_stream_kernel(RecoverProbeArgs a) {
+    extern __shared__ uint8_t smem[];   // residency only
+    const uint32_t item = xcd_order() * kThreads + threadIdx.x;
+    if (item >= a.total) return;
+    const uint32_t blk = fdiv(item, a.div_cps);
+    const uint32_t c = item - blk * a.cps;
+    const uint8_t* d0 = a.data + (uint64_t)blk * a.dbs + (uint64_t)c * kChunk;
+    uint4 x[NIN];
+#pragma unroll
+    for (int j = 0; j < NIN; ++j) x[j] = ld16<true>(d0 + (uint64_t)j * a.ss);
+    uint4 acc = x[0];
+#pragma unroll
+    for (int j = 1; j < NIN; ++j) {
+        acc.x ^= x[j].x;
+        acc.y ^= x[j].y;
+        acc.z ^= x[j].z;
+        acc.w ^= x[j].w;
+    }
+    const uint32_t nb = min(a.len - c * kChunk, (uint32_t)kChunk);
+    st16<true>(a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk, keep_bytes(acc, nb));
+    if (a.nin == 0x5A5A5A5Au) smem[0] = 1;   // never: keeps the LDS allocation
 }
 
 int stream_of(fec_ctx* ctx, hipStream_t* s) {
@@ -154,7 +185,7 @@ bool layout_ok(const void* p, size_t bs, size_t ss, size_t len) {
 }  // namespace fk
 
 extern "C" int fec_probe_encode_traffic(fec_ctx* ctx, int k, int m, size_t shard_len, size_t nblocks,
-                                        const void* data, size_t dbs, void* parity, size_t pbs, size_t ss) {
+                                        const void* data, size_t dbs, void* parity, size_t pbs, size_t ss, int wpc) {
     using namespace fk;
     hipStream_t s;
     int rc = stream_of(ctx, &s);
@@ -178,13 +209,12 @@ extern "C" int fec_probe_encode_traffic(fec_ctx* ctx, int k, int m, size_t shard
     a.cps = cps;
     a.total = (uint32_t)(nblocks * cps);
     a.div_cps = make_fastdiv(cps);
-    a.swz = (uint32_t)g_tune.xcd_swz;
     const int grid = (int)((a.total + kThreads - 1) / kThreads);
-    // the fixed encode's residency: g_tune.enc_wpc workgroups per CU, RS(2,3) uncapped; RS(16,24) and
-    // RS(20,30) as the bit-sliced encode, uncapped (g_tune.enc_bwpc; the bit-sliced kernel takes two
-    // chunks a lane, the twin one)
-    const size_t lds = k >= 16 ? occupancy_lds(g_tune.enc_bwpc, 0)
-                               : occupancy_lds(k == 2 ? 0 : g_tune.enc_wpc, (size_t)m * k * 32);
+    // the encode's own residency (wpc -1): RS(8,12) g_tune.enc_wpc workgroups per CU, RS(2,3)
+    // uncapped (no LDS); RS(16,24) and RS(20,30) as the bit-sliced encode (g_tune.enc_bwpc; the
+    // bit-sliced kernel takes two chunks a lane, the twin one)
+    if (wpc < 0) wpc = k >= 16 ? (int)g_tune.enc_bwpc : k == 2 ? 0 : (int)g_tune.enc_wpc;
+    const size_t lds = occupancy_lds(wpc, k == 8 ? (size_t)m * k * 32 : 0);
     if (k == 2) hipLaunchKernelGGL((probe_encode_kernel<2, 1>), dim3(grid), dim3(kThreads), lds, s, a);
     else if (k == 8) hipLaunchKernelGGL((probe_encode_kernel<8, 4>), dim3(grid), dim3(kThreads), lds, s, a);
     else if (k == 16) hipLaunchKernelGGL((probe_encode_kernel<16, 8>), dim3(grid), dim3(kThreads), lds, s, a);
@@ -194,7 +224,7 @@ extern "C" int fec_probe_encode_traffic(fec_ctx* ctx, int k, int m, size_t shard
 
 extern "C" int fec_probe_recover_traffic(fec_ctx* ctx, int k, int m, size_t shard_len, size_t nblocks,
                                          const void* data, size_t dbs, const void* parity, size_t pbs, size_t ss,
-                                         const uint32_t* masks, void* out, size_t out_bs) {
+                                         const uint32_t* masks, void* out, size_t out_bs, int wpc) {
     using namespace fk;
     hipStream_t s;
     int rc = stream_of(ctx, &s);
@@ -220,12 +250,11 @@ extern "C" int fec_probe_recover_traffic(fec_ctx* ctx, int k, int m, size_t shar
     a.cps = cps;
     a.total = (uint32_t)(nblocks * cps);
     a.nblocks = (uint32_t)nblocks;
-    a.swz = (uint32_t)g_tune.dec_swz;
     a.div_cps = make_fastdiv(cps);
     const int grid = (int)((a.total + kThreads - 1) / kThreads);
-    // the direct decode's residency (fec_recover.hip direct_launch): 4 workgroups per CU at k = 8,
-    // 3 at k >= 16, small codes uncapped; LDS as its four wave slices of 3 blocks' PermTab rows
-    const int wpc = g_tune.dir_wpc >= 0 ? g_tune.dir_wpc : (k >= 16 ? 3 : k >= 8 ? 4 : 0);
+    // the direct decode's residency (wpc -1; fec_recover.hip direct_launch): 3 workgroups per CU for
+    // k >= 8, small codes uncapped; LDS as its four wave slices of 3 blocks' PermTab rows
+    if (wpc < 0) wpc = g_tune.dir_wpc >= 0 ? (int)g_tune.dir_wpc : (k >= 8 ? 3 : 0);
     const size_t lds = occupancy_lds(wpc, (size_t)4 * 3 * k * 32);
     const uint32_t um = (uint32_t)m;
     if (k == 2) hipLaunchKernelGGL((probe_recover_kernel<2>), dim3(grid), dim3(kThreads), lds, s, a, um);
@@ -237,7 +266,7 @@ extern "C" int fec_probe_recover_traffic(fec_ctx* ctx, int k, int m, size_t shar
 
 extern "C" int fec_probe_rebuild_traffic(fec_ctx* ctx, int k, int m, size_t shard_len, size_t nblocks,
                                          const void* data, size_t dbs, const void* parity, size_t pbs, size_t ss,
-                                         const uint32_t* masks, void* out, size_t out_bs) {
+                                         const uint32_t* masks, void* out, size_t out_bs, int wpc) {
     using namespace fk;
     hipStream_t s;
     int rc = stream_of(ctx, &s);
@@ -263,14 +292,47 @@ extern "C" int fec_probe_rebuild_traffic(fec_ctx* ctx, int k, int m, size_t shar
     a.cps = cps;
     a.total = (uint32_t)(nblocks * cps);
     a.nblocks = (uint32_t)nblocks;
-    a.swz = (uint32_t)g_tune.dec_swz;
     a.div_cps = make_fastdiv(cps);
     const int grid = (int)((a.total + kThreads - 1) / kThreads);
-    // the rebuild's residency: its VGPRs allow 4 workgroups per CU (fec_rebuild.hip, uncapped)
-    const size_t lds = occupancy_lds(4, 0);
+    // the rebuild's residency (wpc -1): its VGPRs allow 4 workgroups per CU (fec_rebuild.hip, uncapped)
+    const size_t lds = occupancy_lds(wpc < 0 ? 4 : wpc, 0);
     const uint32_t um = (uint32_t)m;
     if (k == 16) hipLaunchKernelGGL((probe_rebuild_kernel<16, 8>), dim3(grid), dim3(kThreads), lds, s, a, um);
     else hipLaunchKernelGGL((probe_rebuild_kernel<20, 10>), dim3(grid), dim3(kThreads), lds, s, a, um);
+    return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
+}
+
+extern "C" int fec_probe_stream_traffic(fec_ctx* ctx, int nin, size_t shard_len, size_t nblocks, const void* in,
+                                        size_t in_bs, void* out, size_t out_bs, size_t ss, int wpc) {
+    using namespace fk;
+    hipStream_t s;
+    int rc = stream_of(ctx, &s);
+    if (rc) return rc;
+    if (nin != 2 && nin != 8 && nin != 16 && nin != 20) return FEC_ERR_INVALID_ARG;
+    if (!layout_ok(in, in_bs, ss, shard_len) || !layout_ok(out, out_bs, 16, 0) || shard_len == 0 ||
+        out_bs < ((shard_len + 15) & ~size_t(15)) || in_bs < (size_t)(nin - 1) * ss + shard_len)
+        return FEC_ERR_ALIGNMENT;
+    const uint32_t cps = (uint32_t)((shard_len + kChunk - 1) / kChunk);
+    if ((uint64_t)nblocks * cps >= (uint64_t(1) << 31)) return FEC_ERR_INVALID_ARG;
+    if (nblocks == 0) return FEC_OK;
+    RecoverProbeArgs a{};
+    a.data = (const uint8_t*)in;
+    a.out = (uint8_t*)out;
+    a.dbs = in_bs;
+    a.ss = ss;
+    a.out_bs = out_bs;
+    a.len = (uint32_t)shard_len;
+    a.cps = cps;
+    a.total = (uint32_t)(nblocks * cps);
+    a.nblocks = (uint32_t)nblocks;
+    a.nin = (uint32_t)nin;
+    a.div_cps = make_fastdiv(cps);
+    const int grid = (int)((a.total + kThreads - 1) / kThreads);
+    const size_t lds = occupancy_lds(wpc < 0 ? 0 : wpc, 0);
+    if (nin == 2) hipLaunchKernelGGL((probe_stream_kernel<2>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (nin == 8) hipLaunchKernelGGL((probe_stream_kernel<8>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (nin == 16) hipLaunchKernelGGL((probe_stream_kernel<16>), dim3(grid), dim3(kThreads), lds, s, a);
+    else hipLaunchKernelGGL((probe_stream_kernel<20>), dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
 }
 

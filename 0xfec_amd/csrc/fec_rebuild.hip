@@ -71,17 +71,14 @@ static_assert(kSplitCheck.t01[0xFF][0] == 0x1CE3FF00u && kSplitCheck.t01[0xFF][3
 constexpr uint32_t kTabLds = 256 * 16 + 256 * 4;   // the workgroup's copy of kPermTabSplit
 
 // A wave's LDS slice: PermTab words of R rows x K inputs for each of its WB blocks, the blocks'
-// input offsets, their plan records. PAD: each block's table words start 128 bytes past a 256-byte
-// row from the other block's, so the two blocks' rows of one read sit 32 banks apart. Unpadded,
-// RS(16,24)'s 2048-byte T0|T1 and 512-byte T2 block strides are whole 256-byte rows: every table
-// read of a wave spanning two blocks meets itself on the same banks (SQ_LDS_BANK_CONFLICT 24 % of
-// the LDS cycles, r04b; RS(20,30)'s 3200-byte stride is 128 off already: 9 %).
-__host__ __device__ constexpr uint32_t half_row_off(uint32_t x) { return x + (128u + 256u - x % 256u) % 256u; }
-template <int K, int R, bool PAD = false>
+// input offsets, their plan records. (RS(16,24)'s 2048-byte T0|T1 and 512-byte T2 block strides put
+// the two blocks' rows on the same banks, 24 % of its LDS cycles in conflicts; padding them 32 banks
+// apart measured +0.1 % for RS(16,24) and -1.2 % for RS(20,30), r04c: not on the critical path.)
+template <int K, int R>
 struct Slice {
     static constexpr uint32_t WB = 2;
-    static constexpr uint32_t bs01 = PAD ? half_row_off(R * K * 16) : R * K * 16;   // bytes per block
-    static constexpr uint32_t bs2 = PAD ? half_row_off(R * K * 4) : R * K * 4;
+    static constexpr uint32_t bs01 = R * K * 16;   // bytes per block
+    static constexpr uint32_t bs2 = R * K * 4;
     static constexpr uint32_t t01 = 0;                        // uint4    [WB][R][K], blocks bs01 apart
     static constexpr uint32_t t2 = t01 + WB * bs01;           // uint32_t [WB][R][K], blocks bs2 apart
     static constexpr uint32_t offs = t2 + WB * bs2;           // uint64_t [WB][K]
@@ -89,24 +86,6 @@ struct Slice {
     static_assert(bs01 % 16 == 0 && t2 % 16 == 0 && offs % 16 == 0 && plans % 16 == 0, "16-byte aligned parts");
     __host__ __device__ static size_t bytes(uint32_t stride) { return plans + (size_t)WB * stride; }
 };
-
-// split4 with the two shifted forms of a dword pair made by one 64-bit shift each: (hi:lo) >> 3
-// moves three bits of hi into the top of lo, which the 0x07070707 mask clears again (and >> 6
-// likewise under 0x03030303), so 4 dwords take 4 instead of 8 shifts.
-__device__ __forceinline__ void split4w(Idx (&ix)[4], const uint4& x) {
-    const uint64_t w0 = ((uint64_t)x.y << 32) | x.x, w1 = ((uint64_t)x.w << 32) | x.z;
-    // as asm: left to itself the compiler sees that only masked bits are used and splits each
-    // 64-bit shift back into two 32-bit ones
-    uint64_t a3, b3, a6, b6;
-    asm("v_lshrrev_b64 %0, 3, %1" : "=v"(a3) : "v"(w0));
-    asm("v_lshrrev_b64 %0, 3, %1" : "=v"(b3) : "v"(w1));
-    asm("v_lshrrev_b64 %0, 6, %1" : "=v"(a6) : "v"(w0));
-    asm("v_lshrrev_b64 %0, 6, %1" : "=v"(b6) : "v"(w1));
-    ix[0] = {x.x & 0x07070707u, (uint32_t)a3 & 0x07070707u, (uint32_t)a6 & 0x03030303u};
-    ix[1] = {x.y & 0x07070707u, (uint32_t)(a3 >> 32) & 0x07070707u, (uint32_t)(a6 >> 32) & 0x03030303u};
-    ix[2] = {x.z & 0x07070707u, (uint32_t)b3 & 0x07070707u, (uint32_t)b6 & 0x03030303u};
-    ix[3] = {x.w & 0x07070707u, (uint32_t)(b3 >> 32) & 0x07070707u, (uint32_t)(b6 >> 32) & 0x03030303u};
-}
 
 // acc ^= c_a x_a ^ c_b x_b (one 16-byte chunk), c by its split PermTab words.
 __device__ __forceinline__ void mac2s(uint32_t (&acc)[4], const Idx (&ia)[4], const Idx (&ib)[4], const uint4& la,
@@ -156,7 +135,7 @@ __device__ __forceinline__ void pair_rows(uint32_t (&acc)[ROWS][4], const Idx (&
 
 // One item's ROWS rebuilt chunks: the K inputs at dbase + offs[j] through a rolling window of W
 // loads (each folded pair's registers take the loads of the pair W inputs ahead).
-template <int K, int ROWS, int W, bool NTL, bool NTS, bool RP, bool S64>
+template <int K, int ROWS, int W, bool RP>
 __device__ __forceinline__ void rebuild_rows(const ReconArgs& a, const uint8_t* out_idx, const uint4* T01,
                                              const uint32_t* T2, const uint64_t* offs, uint8_t* dbase,
                                              uint8_t* obase, uint32_t c, uint32_t nout) {
@@ -167,8 +146,8 @@ __device__ __forceinline__ void rebuild_rows(const ReconArgs& a, const uint8_t* 
     // two inputs' offsets per 16-byte read (immediate LDS offsets)
     auto load2 = [&](int j, uint4& xa, uint4& xb) {
         const ulonglong2 o = *reinterpret_cast<const ulonglong2*>(offs + j);
-        xa = ld16<NTL>(dbase + o.x);
-        xb = ld16<NTL>(dbase + o.y);
+        xa = ld16<kNT>(dbase + o.x);
+        xb = ld16<kNT>(dbase + o.y);
     };
     uint4 x[K];
 #pragma unroll
@@ -185,14 +164,10 @@ __device__ __forceinline__ void rebuild_rows(const ReconArgs& a, const uint8_t* 
         const uint32_t* t2 = T2 + toff;
         const uint4 xa = x[j], xb = x[j + 1];
         __builtin_amdgcn_sched_barrier(0);
+        // (splits by 64-bit shifts, 64 fewer VALU per body, measured +0.2 %, r03m)
         Idx ia[4], ib[4];
-        if constexpr (S64) {
-            split4w(ia, xa);
-            split4w(ib, xb);
-        } else {
-            split4(ia, xa);
-            split4(ib, xb);
-        }
+        split4(ia, xa);
+        split4(ib, xb);
         if (j + W < K) load2(j + W, x[j + W], x[j + W + 1]);
         pair_rows<K, ROWS, RP>(acc, ia, ib, t01, t2, j);
     }
@@ -200,18 +175,16 @@ __device__ __forceinline__ void rebuild_rows(const ReconArgs& a, const uint8_t* 
 #pragma unroll
     for (int r = 0; r < ROWS; ++r)
         if (r < (int)nout)
-            store_chunk<NTS>(obase ? obase + (uint64_t)r * a.ss : dbase + (uint64_t)out_idx[r] * a.ss, as_uint4(acc[r]),
-                             nb, a.pad_zero);
+            store_chunk<kNT>(obase ? obase + (uint64_t)r * a.ss : dbase + (uint64_t)out_idx[r] * a.ss, as_uint4(acc[r]),
+                             nb);
 }
 
 // Flat grid, one wave per 64 consecutive items of the (sorted) plan order; R: the code's largest
-// rebuilt row count (min(k, m)).
-template <int K, int R, int W, int POL, bool RP, bool S64, bool PAD>
+// rebuilt row count (min(k, m)); W: loads in flight per lane; RP: row-pipelined table reads.
+template <int K, int R, int W, bool RP>
 __global__ __launch_bounds__(kThreads) void rs_rebuild_k_kernel(ReconArgs a) {
-    constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
-    using S = Slice<K, R, PAD>;
+    using S = Slice<K, R>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    if (a.gate && *a.gate != a.gate_want) return;   // the classify kernel picked the direct path
     uint4* g01 = reinterpret_cast<uint4*>(smem);
     uint32_t* g2 = reinterpret_cast<uint32_t*>(smem + 256 * 16);
     // the workgroup's PermTab table: one coefficient per thread (kThreads == 256)
@@ -224,7 +197,7 @@ __global__ __launch_bounds__(kThreads) void rs_rebuild_k_kernel(ReconArgs a) {
     uint64_t* offs = reinterpret_cast<uint64_t*>(slice + S::offs);
     uint8_t* plans = slice + S::plans;
     const uint32_t total = a.nblocks * a.cps;
-    const uint32_t i0 = xcd_order(a.swz) * kThreads + (wave << 6);
+    const uint32_t i0 = xcd_order() * kThreads + (wave << 6);
     const bool live = i0 < total;   // wave-uniform
     uint32_t bfirst = 0, nb = 0;
     if (live) {
@@ -283,7 +256,7 @@ __global__ __launch_bounds__(kThreads) void rs_rebuild_k_kernel(ReconArgs a) {
     const uint64_t* O = offs + g * K;
     const uint8_t* oi = P + lay.out_off;
     static_assert(R <= 10, "row bodies 1..10");
-#define FEC_RB_ROWS(N) rebuild_rows<K, N, W, NTL, NTS, RP, S64>(a, oi, T01, T2, O, dbase, obase, c, nout)
+#define FEC_RB_ROWS(N) rebuild_rows<K, N, W, RP>(a, oi, T01, T2, O, dbase, obase, c, nout)
     switch (rows) {   // wave-uniform
         case 1: FEC_RB_ROWS(1); break;
         case 2: if constexpr (R >= 2) FEC_RB_ROWS(2); break;
@@ -299,45 +272,27 @@ __global__ __launch_bounds__(kThreads) void rs_rebuild_k_kernel(ReconArgs a) {
 #undef FEC_RB_ROWS
 }
 
-// W: loads in flight per lane (knob dec_win; 0: by code); DW: the code's default window, the one
-// built with the padded slice too (knob dec_lpad)
-template <int K, int R, bool RP, int DW>
-hipError_t rebuild_launch(const ReconArgs& a, int w, hipStream_t s) {
+template <int K, int R, int W, bool RP>
+hipError_t rebuild_launch(const ReconArgs& a, hipStream_t s) {
     const uint64_t total = (uint64_t)a.nblocks * a.cps;
     const int grid = (int)((total + kThreads - 1) / kThreads);
     if (grid == 0) return hipSuccess;
-    const bool s64 = g_tune.dec_s64 != 0;
-    if (g_tune.dec_lpad && w == DW && !s64) {
-        const size_t lds = occupancy_lds(g_tune.dec_wpc, kTabLds + 4 * Slice<K, R, true>::bytes(a.lay.stride));
-        hipLaunchKernelGGL((rs_rebuild_k_kernel<K, R, DW, 3, RP, false, true>), dim3(grid), dim3(kThreads), lds, s, a);
-        return hipGetLastError();
-    }
     const size_t lds = occupancy_lds(g_tune.dec_wpc, kTabLds + 4 * Slice<K, R>::bytes(a.lay.stride));
-#define FEC_RB_LAUNCH(WW, S) \
-    hipLaunchKernelGGL((rs_rebuild_k_kernel<K, R, WW, 3, RP, S, false>), dim3(grid), dim3(kThreads), lds, s, a)
-    if (w == 4 && s64) FEC_RB_LAUNCH(4, true);
-    else if (w == 4) FEC_RB_LAUNCH(4, false);
-    else if (w == 6 && s64) FEC_RB_LAUNCH(6, true);
-    else if (w == 6) FEC_RB_LAUNCH(6, false);
-    else if (s64) FEC_RB_LAUNCH(8, true);
-    else FEC_RB_LAUNCH(8, false);
-#undef FEC_RB_LAUNCH
+    hipLaunchKernelGGL((rs_rebuild_k_kernel<K, R, W, RP>), dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 
 }  // namespace
 
 bool rebuild_k_applies(uint32_t k, uint32_t maxe, uint32_t cps) {
-    return g_tune.dec_fixk == 4 && (g_tune.dec_nt & 3) == 3 && !g_tune.dec_diag && cps >= 64 &&
-           ((k == 16 && maxe == 8) || (k == 20 && maxe == 10));
+    return cps >= 64 && ((k == 16 && maxe == 8) || (k == 20 && maxe == 10));
 }
 
 hipError_t launch_rs_rebuild_k(const ReconArgs& a, hipStream_t s) {
-    // windows by interleaved A/B (dec_select.py, r03k): RS(16,24) 8 -> 4 +0.3 %; RS(20,30) 8 -> 6 +6.7 %
-    // (137 -> 125 VGPRs: 4 instead of 3 waves per SIMD)
-    const int w = g_tune.dec_win;
-    if (a.k == 16) return rebuild_launch<16, 8, false, 4>(a, w ? w : 4, s);
-    return rebuild_launch<20, 10, true, 6>(a, w ? w : 6, s);
+    // windows by interleaved A/B (r03k): RS(16,24) 8 -> 4 +0.3 % (4 / 6 / 8 within 0.7 %); RS(20,30)
+    // 8 -> 6 +6.7 % (137 -> 125 VGPRs: 4 instead of 3 waves per SIMD)
+    if (a.k == 16) return rebuild_launch<16, 8, 4, false>(a, s);
+    return rebuild_launch<20, 10, 6, true>(a, s);
 }
 
 }  // namespace fk

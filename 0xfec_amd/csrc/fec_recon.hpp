@@ -1,6 +1,6 @@
 // fec_recon.hpp — device pieces shared by the reconstruct kernels (fec_decode.hip: plan + wave /
-// tile rebuild; fec_recover.hip: direct single-erasure rebuild): the per-item rebuild, the wave
-// slice layout and the in-wave plan construction.
+// tile rebuild; fec_recover.hip: direct single-erasure rebuild and its multi-erasure worklist;
+// fec_rebuild.hip): the per-item rebuild, the wave slice layout and the in-wave plan construction.
 #pragma once
 
 #include "fec_device.hpp"
@@ -24,7 +24,10 @@ __device__ __forceinline__ const uint8_t* parity_base(const uint8_t* pblk, uint3
 // One (block, chunk) item: load the k input shards named by the plan record P, fold them with
 // the block's PermTabs T (row r = erased shard r), store the rebuilt chunks. `rows` is
 // wave-uniform (the wave's largest erasure count), so the loop bounds never diverge.
-template <int MAXE, bool NTL, bool NTS>
+// Non-temporal loads and stores throughout the reconstruct kernels.
+constexpr bool kNT = true;
+
+template <int MAXE>
 __device__ __forceinline__ void recon_item(const ReconArgs& a, const uint8_t* P, const gf::PermTab* T,
                                            uint32_t blk, uint32_t c, uint32_t rows, uint32_t nout) {
     const uint32_t k = a.k;
@@ -44,7 +47,7 @@ __device__ __forceinline__ void recon_item(const ReconArgs& a, const uint8_t* P,
             const uint32_t w = jj < 4 ? sl.x : sl.y;
             const uint32_t slot = (w >> (8 * (jj & 3))) & 0xFFu;
             x[jj] = j0 + jj < k   // uniform predicate: no loads past input k-1
-                        ? ld16<NTL>(slot_addr(dblk, pbase, slot, k, (uint32_t)a.ss, (uint32_t)a.pss))
+                        ? ld16<kNT>(slot_addr(dblk, pbase, slot, k, (uint32_t)a.ss, (uint32_t)a.pss))
                         : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
@@ -72,8 +75,8 @@ __device__ __forceinline__ void recon_item(const ReconArgs& a, const uint8_t* P,
 #pragma unroll
     for (int r = 0; r < MAXE; ++r)
         if (r < (int)nout)
-            store_chunk<NTS>(oblk ? oblk + (uint64_t)r * a.ss : dblk + (uint64_t)out_idx[r] * a.ss, as_uint4(acc[r]),
-                             nb, a.pad_zero);
+            store_chunk<kNT>(oblk ? oblk + (uint64_t)r * a.ss : dblk + (uint64_t)out_idx[r] * a.ss, as_uint4(acc[r]),
+                             nb);
 }
 
 // recon_item with the data shard count K known at compile time: all K input loads are issued
@@ -81,7 +84,7 @@ __device__ __forceinline__ void recon_item(const ReconArgs& a, const uint8_t* P,
 // loads wait for the first group's arithmetic), and the wave-uniform row count selects a
 // straight-line body per count (per-row branches inside the fold make the compiler copy the
 // accumulators through every branch).
-template <int K, int ROWS, bool NTS>
+template <int K, int ROWS>
 __device__ __forceinline__ void recon_rows_k(const ReconArgs& a, const uint8_t* P, const gf::PermTab* T,
                                              const uint4 (&x)[K], uint8_t* dblk, uint8_t* oblk, uint32_t c,
                                              uint32_t nout) {
@@ -110,11 +113,11 @@ __device__ __forceinline__ void recon_rows_k(const ReconArgs& a, const uint8_t* 
 #pragma unroll
     for (int r = 0; r < ROWS; ++r)
         if (r < (int)nout)
-            store_chunk<NTS>(oblk ? oblk + (uint64_t)r * a.ss : dblk + (uint64_t)out_idx[r] * a.ss, as_uint4(acc[r]),
-                             nb, a.pad_zero);
+            store_chunk<kNT>(oblk ? oblk + (uint64_t)r * a.ss : dblk + (uint64_t)out_idx[r] * a.ss, as_uint4(acc[r]),
+                             nb);
 }
 
-template <int K, int MAXE, bool NTL, bool NTS>
+template <int K, int MAXE>
 __device__ __forceinline__ void recon_item_k(const ReconArgs& a, const uint8_t* P, const gf::PermTab* T,
                                              uint32_t blk, uint32_t c, uint32_t rows, uint32_t nout) {
     static_assert(K % 2 == 0, "inputs are folded in pairs");
@@ -130,7 +133,7 @@ __device__ __forceinline__ void recon_item_k(const ReconArgs& a, const uint8_t* 
         for (int jj = 0; jj < 8; ++jj) {
             if (j0 + jj >= K) break;   // compile-time: the slot area is rounded up to 8 bytes
             const uint32_t slot = ((jj < 4 ? sl.x : sl.y) >> (8 * (jj & 3))) & 0xFFu;
-            x[j0 + jj] = ld16<NTL>(slot_addr(dblk, pbase, slot, K, (uint32_t)a.ss, (uint32_t)a.pss));
+            x[j0 + jj] = ld16<kNT>(slot_addr(dblk, pbase, slot, K, (uint32_t)a.ss, (uint32_t)a.pss));
         }
     }
     uint8_t* oblk = a.out ? a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk : nullptr;
@@ -138,135 +141,17 @@ __device__ __forceinline__ void recon_item_k(const ReconArgs& a, const uint8_t* 
     constexpr int R = MAXE < K ? (MAXE <= 8 ? MAXE : 10) : K;
     static_assert(R <= 10, "row bodies 1..10");
     switch (rows) {   // wave-uniform
-        case 1: recon_rows_k<K, 1, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
-        case 2: if constexpr (R >= 2) recon_rows_k<K, 2, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
-        case 3: if constexpr (R >= 3) recon_rows_k<K, 3, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
-        case 4: if constexpr (R >= 4) recon_rows_k<K, 4, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
-        case 5: if constexpr (R >= 5) recon_rows_k<K, 5, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
-        case 6: if constexpr (R >= 6) recon_rows_k<K, 6, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
-        case 7: if constexpr (R >= 7) recon_rows_k<K, 7, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
-        case 8: if constexpr (R >= 8) recon_rows_k<K, 8, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
-        case 9: if constexpr (R >= 9) recon_rows_k<K, 9, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
-        default: if constexpr (R >= 10) recon_rows_k<K, 10, NTS>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 1: recon_rows_k<K, 1>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 2: if constexpr (R >= 2) recon_rows_k<K, 2>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 3: if constexpr (R >= 3) recon_rows_k<K, 3>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 4: if constexpr (R >= 4) recon_rows_k<K, 4>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 5: if constexpr (R >= 5) recon_rows_k<K, 5>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 6: if constexpr (R >= 6) recon_rows_k<K, 6>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 7: if constexpr (R >= 7) recon_rows_k<K, 7>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 8: if constexpr (R >= 8) recon_rows_k<K, 8>(a, P, T, x, dblk, oblk, c, nout); break;
+        case 9: if constexpr (R >= 9) recon_rows_k<K, 9>(a, P, T, x, dblk, oblk, c, nout); break;
+        default: if constexpr (R >= 10) recon_rows_k<K, 10>(a, P, T, x, dblk, oblk, c, nout); break;
     }
-}
-
-// acc[r] ^= T[r][j] x_a ^ T[r][j+1] x_b for the ROWS rows, with each row's PermTab words read from
-// LDS one row ahead of their use (scheduling barriers keep the reads of row r + 2 behind row r's
-// products). Left to itself the compiler issues every row's table reads of the pair at once to
-// hide LDS latency: 10 words per row, 100 VGPRs at 10 rows (RS(20,30)), which is what held the
-// K = 20 rebuild at 2 waves per SIMD; here 20 are live, and other waves hide the latency.
-template <int K, int ROWS>
-__device__ __forceinline__ void mac2_rows_pipe(uint32_t (&acc)[ROWS][4], const Idx (&ia)[4], const Idx (&ib)[4],
-                                               const gf::PermTab* t, int j) {
-    uint4 la = *reinterpret_cast<const uint4*>(t + j), lb = *reinterpret_cast<const uint4*>(t + j + 1);
-    uint32_t a2 = t[j].t2, b2 = t[j + 1].t2;
-#pragma unroll
-    for (int r = 0; r < ROWS; ++r) {
-        uint4 na = la, nb = lb;
-        uint32_t na2 = a2, nb2 = b2;
-        if (r + 1 < ROWS) {
-            const gf::PermTab* tn = t + (r + 1) * K + j;
-            na = *reinterpret_cast<const uint4*>(tn);
-            nb = *reinterpret_cast<const uint4*>(tn + 1);
-            na2 = tn[0].t2;
-            nb2 = tn[1].t2;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            const Prod3 p = gprod(ia[d], la, a2);
-            const Prod3 q = gprod(ib[d], lb, b2);
-            acc[r][d] = xor3(xor3(xor3(acc[r][d], p.p0, p.p1), p.p2, q.p0), q.p1, q.p2);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        la = na, lb = nb, a2 = na2, b2 = nb2;
-    }
-}
-
-// recon_rows_k with a rolling load window (dec_fixk = 2): W inputs are loaded up front, and each
-// folded pair's registers take the loads of the pair W inputs ahead, so at most W inputs are
-// live instead of K (K = 16: 64 -> 32 data VGPRs), for more resident waves per SIMD. RP: the
-// rows' table reads pipelined one row ahead (mac2_rows_pipe, dec_fixk = 3).
-template <int K, int ROWS, int W, bool NTL, bool NTS, bool RP = false>
-__device__ __forceinline__ void recon_rows_roll(const ReconArgs& a, const uint8_t* P, const gf::PermTab* T,
-                                                uint8_t* dblk, const uint8_t* pbase, uint8_t* oblk, uint32_t c,
-                                                uint32_t nout) {
-    static_assert(K % 2 == 0 && W % 2 == 0 && W <= K, "inputs are folded and loaded in pairs");
-    // A body that starts like no other: the row bodies of recon_item_roll's switch share their
-    // opening (the window's loads, the first pair's splits, row 0's products), and the compiler
-    // hoists an identical opening into the block before the switch, where it is live across
-    // every body at once (RS(20,30): ~96 VGPRs of split indices, 193 in all).
-    if constexpr (RP) asm volatile("; rows %0" ::"n"(ROWS));
-    constexpr int NS = (K + 7) / 8;   // the slot area is rounded up to 8 bytes
-    uint2 sl[NS];
-#pragma unroll
-    for (int g = 0; g < NS; ++g) sl[g] = *reinterpret_cast<const uint2*>(P + a.lay.in_off + 8 * g);
-    auto load = [&](int j) {
-        const uint32_t w = (j & 7) < 4 ? sl[j >> 3].x : sl[j >> 3].y;
-        const uint32_t slot = (w >> (8 * (j & 3))) & 0xFFu;
-        return ld16<NTL>(slot_addr(dblk, pbase, slot, K, (uint32_t)a.ss, (uint32_t)a.pss));
-    };
-    uint4 x[K];
-#pragma unroll
-    for (int j = 0; j < W; ++j) x[j] = load(j);
-    uint32_t acc[ROWS][4];
-#pragma unroll
-    for (int r = 0; r < ROWS; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0;
-#pragma unroll
-    for (int j = 0; j < K; j += 2) {
-        uint32_t toff = 0;
-        asm volatile("" : "+s"(toff));
-        const gf::PermTab* t = T + toff;
-        const uint4 xa = x[j], xb = x[j + 1];
-        __builtin_amdgcn_sched_barrier(0);
-        Idx ia[4], ib[4];
-        split4(ia, xa);
-        split4(ib, xb);
-        // the pair W inputs ahead goes out once this pair's inputs are split
-        if (j + W < K) {
-            x[j + W] = load(j + W);
-            x[j + W + 1] = load(j + W + 1);
-        }
-        if constexpr (RP) {
-            mac2_rows_pipe<K, ROWS>(acc, ia, ib, t, j);
-        } else {
-#pragma unroll
-            for (int r = 0; r < ROWS; ++r) mac2(acc[r], ia, ib, t + r * K + j, t + r * K + j + 1);
-        }
-    }
-    const uint32_t nb = a.len - c * kChunk;
-    const uint8_t* out_idx = P + a.lay.out_off;
-#pragma unroll
-    for (int r = 0; r < ROWS; ++r)
-        if (r < (int)nout)
-            store_chunk<NTS>(oblk ? oblk + (uint64_t)r * a.ss : dblk + (uint64_t)out_idx[r] * a.ss, as_uint4(acc[r]),
-                             nb, a.pad_zero);
-}
-
-template <int K, int MAXE, int W, bool NTL, bool NTS, bool RP = false>
-__device__ __forceinline__ void recon_item_roll(const ReconArgs& a, const uint8_t* P, const gf::PermTab* T,
-                                                uint32_t blk, uint32_t c, uint32_t rows, uint32_t nout) {
-    uint8_t* dblk = a.data + (uint64_t)blk * a.dbs + (uint64_t)c * kChunk;
-    const uint8_t* pblk = a.parity + (uint64_t)blk * a.pbs + (uint64_t)c * kChunk;
-    const uint8_t* pbase = parity_base(pblk, K, a.pss);
-    uint8_t* oblk = a.out ? a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk : nullptr;
-    constexpr int R = MAXE < K ? (MAXE <= 8 ? MAXE : 10) : K;
-    static_assert(R <= 10, "row bodies 1..10");
-#define FEC_ROLL_ROWS(N) recon_rows_roll<K, N, W, NTL, NTS, RP>(a, P, T, dblk, pbase, oblk, c, nout)
-    switch (rows) {   // wave-uniform
-        case 1: FEC_ROLL_ROWS(1); break;
-        case 2: if constexpr (R >= 2) FEC_ROLL_ROWS(2); break;
-        case 3: if constexpr (R >= 3) FEC_ROLL_ROWS(3); break;
-        case 4: if constexpr (R >= 4) FEC_ROLL_ROWS(4); break;
-        case 5: if constexpr (R >= 5) FEC_ROLL_ROWS(5); break;
-        case 6: if constexpr (R >= 6) FEC_ROLL_ROWS(6); break;
-        case 7: if constexpr (R >= 7) FEC_ROLL_ROWS(7); break;
-        case 8: if constexpr (R >= 8) FEC_ROLL_ROWS(8); break;
-        case 9: if constexpr (R >= 9) FEC_ROLL_ROWS(9); break;
-        default: if constexpr (R >= 10) FEC_ROLL_ROWS(10); break;
-    }
-#undef FEC_ROLL_ROWS
 }
 
 template <int MAXE>
@@ -289,23 +174,10 @@ __host__ __device__ inline size_t wave_slice_bytes(uint32_t k, uint32_t maxe, ui
     return (size_t)nblk * maxe * k * 32 + (size_t)nblk * stride;
 }
 
-// Fused form: the wave also builds its blocks' plan records (the work of rs_plan_kernel) from
-// the present masks, lanes in parallel: slots and erased indices by prefix popcounts, one
-// erasure by the single-parity-row solution, several by the Lagrange coefficients (see
-// rs_plan_kernel) with the k^2 + e*k lookups spread over the 64 lanes. No plan kernel, no plan
-// buffer round trip through HBM.
-struct FusedLds {
-    size_t prows, slices, slice;   // offsets: exp [0,512), log [512,768), prows, wave slices
-};
+// A wave slice that also holds the scratch of build_wave_plans (below): the direct decode's
+// multi-erasure worklist kernel builds its blocks' plans in-wave (fec_recover.hip).
 __host__ __device__ inline size_t fused_slice_bytes(uint32_t k, uint32_t maxe, uint32_t stride) {
     return (wave_slice_bytes(k, maxe, stride) + (size_t)k + maxe + 15) & ~(size_t)15;
-}
-__host__ __device__ inline FusedLds fused_lds(uint32_t m, uint32_t k, uint32_t maxe, uint32_t stride) {
-    FusedLds l;
-    l.prows = 768;
-    l.slices = (l.prows + (size_t)m * k + 15) & ~(size_t)15;
-    l.slice = fused_slice_bytes(k, maxe, stride);
-    return l;
 }
 
 __device__ __forceinline__ void wave_sync() {

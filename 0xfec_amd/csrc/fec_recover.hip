@@ -57,15 +57,12 @@ struct CoefWords {
 // read from the code's coefficient table in device memory (a.single_coef, through the constant
 // address space: scalar loads), for codes whose rows do not fit the argument (RS(20,30): 1000
 // dwords).
-template <int K, int POL, int TAB, bool PERSIST = false>
+template <int K, int POL, int TAB>
 __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a, CoefWords cwords) {
     constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    if (a.gate && *a.gate != a.gate_want) return;   // the classify kernel picked the plan path
-    // one flat workgroup, or (PERSIST: gated launches) the flat grid's workgroups walked by a
-    // persistent grid, so the losing path exits after one round (a separate instance: the loop
-    // costs the flat bodies registers, RS(8,12) 67 -> 76 VGPRs)
-    auto body = [&](uint32_t vb, uint32_t G) {
+    {
+        const uint32_t vb = blockIdx.x;
         const uint32_t k = K ? (uint32_t)K : a.k, m = a.m;
         const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
         uint8_t* slice = smem + (size_t)wave * direct_wave_bytes(k);
@@ -98,17 +95,32 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
                 if (lane == 0 && (f1 || f2)) atomicOr(a.err, (f1 ? 1 : 0) | (f2 ? 2 : 0));
             }
         }
-        const uint32_t i0 = xcd_order_of(vb, G, a.swz) * kThreads + (wave << 6);
+        const uint32_t i0 = xcd_order() * kThreads + (wave << 6);
         if (i0 >= total) return;
         const uint32_t bfirst = fdiv(i0, a.div_cps);
         const uint32_t nb = fdiv(min(i0 + 63u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
-        const uint32_t mine = lane < nb ? a.masks[bfirst + lane] : 0u;   // the wave's masks in one load
+        // The wave's <= 3 masks by scalar loads (wave-uniform addresses, the constant cache), which
+        // the scalar unit turns into shard addresses while the vector memory path is free: a
+        // vector load of the masks put a dependent vector round trip in front of every wave's
+        // shard loads (decode twin at 4 workgroups/CU: 5.73 TB/s with a vector mask load, 5.84
+        // with scalar ones, 5.85 with no mask at all; with the field arithmetic 5.70 / 5.83 /
+        // 5.87; profiles/r05/dec_twin_r05b.log)
+        uint32_t m0, m1, m2;
+        {
+            typedef __attribute__((address_space(4))) const uint32_t ConstU32;
+            ConstU32* cm = (ConstU32*)a.masks;
+            const uint32_t bf = (uint32_t)__builtin_amdgcn_readfirstlane((int)bfirst), last = a.nblocks - 1;
+            m0 = cm[bf];
+            m1 = cm[(uint32_t)__builtin_amdgcn_readfirstlane((int)min(bf + 1, last))];
+            m2 = cm[(uint32_t)__builtin_amdgcn_readfirstlane((int)min(bf + 2, last))];
+        }
+        auto mask_of = [&](uint32_t g) { return g == 0 ? m0 : g == 1 ? m1 : m2; };   // g < nb
 
         // A block with two or more erasures (and enough shards) sends the whole wave to the
         // worklist of rs_recover_hard_kernel.
         bool hard = false;
         for (uint32_t g = 0; g < nb; ++g) {
-            const uint32_t mask = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)g) & all;
+            const uint32_t mask = mask_of(g) & all;
             const uint32_t e = k - __popc(mask & kmask);
             if (e >= 2 && (uint32_t)__popc(mask) >= k && !(a.max_out && e > a.max_out)) hard = true;
         }
@@ -125,7 +137,7 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
     #pragma unroll
         for (uint32_t g = 0; g < kWaveBlocks; ++g) {
             if (g >= nb) break;
-            const uint32_t mask = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)g) & all;
+            const uint32_t mask = mask_of(g) & all;
             const uint32_t e = k - __popc(mask & kmask);
             if (e == 1 && (uint32_t)__popc(mask) >= k && !(a.max_out && e > a.max_out))
                 row[g] = (__ffs(~mask & kmask) - 1) * m + (__ffs(mask >> k) - 1);   // m >= 1 here: k < 32
@@ -186,10 +198,7 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
         const uint32_t blk = inr ? fdiv(item, a.div_cps) : bfirst;
         const uint32_t g = blk - bfirst;
         const uint32_t c = item - blk * a.cps;
-        const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 0);
-        const uint32_t m1 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 1);
-        const uint32_t m2 = (uint32_t)__builtin_amdgcn_readlane((int)mine, 2);
-        const uint32_t mask = (g == 0 ? m0 : g == 1 ? m1 : m2) & all;
+        const uint32_t mask = mask_of(g) & all;
         const bool work = inr && k - __popc(mask & kmask) == 1 && (uint32_t)__popc(mask) >= k;
         const uint32_t E0 = __ffs(~mask & kmask) - 1;
         const uint32_t R0 = work ? __ffs(mask >> k) - 1 : 0;
@@ -253,10 +262,8 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
         }
         uint8_t* dst = a.out ? a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk
                              : const_cast<uint8_t*>(dblk) + (uint64_t)E0 * a.ss;
-        store_chunk<NTS>(dst, as_uint4(acc), a.len - c * kChunk, a.pad_zero);
-    };
-    if constexpr (PERSIST) for_virtual_blocks(a.vgrid, body);
-    else body(blockIdx.x, gridDim.x);
+        store_chunk<NTS>(dst, as_uint4(acc), a.len - c * kChunk);
+    }
 }
 
 // Waves the direct kernel found holding a multi-erasure block (worklist a.hard: [0] count,
@@ -264,9 +271,8 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
 // in turn, builds the plans of each wave's blocks in-wave (build_wave_plans, the fused form of
 // fec_decode.hip) and rebuilds them through the general per-item path. With an empty list every
 // wave exits at once. The last workgroup to finish rewinds the worklist for the next launch.
-template <int MAXE, int POL>
+template <int MAXE>
 __global__ __launch_bounds__(kThreads) void rs_recover_hard_kernel(ReconArgs a) {
-    constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t k = a.k, m = a.m, maxe = a.maxe;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -307,7 +313,7 @@ __global__ __launch_bounds__(kThreads) void rs_recover_hard_kernel(ReconArgs a) 
             const uint8_t* P = plans + g * a.lay.stride;
             const uint32_t nout = inr ? P[a.lay.nout_off] : 0;
             const uint32_t rows = wave_rows<MAXE>(nout);
-            if (nout) recon_item<MAXE, NTL, NTS>(a, P, wt + g * maxe * k, blk, c, rows, nout);
+            if (nout) recon_item<MAXE>(a, P, wt + g * maxe * k, blk, c, rows, nout);
         }
     }
     __syncthreads();
@@ -325,12 +331,13 @@ size_t direct_table_words(uint32_t k, uint32_t m) { return (size_t)k * m * k * 8
 bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t stride, bool single_slot) {
     if (!g_tune.dec_direct || m == 0 || k + m > 32 || cps < 32) return false;
     // small codes (their PermTab table fits), or RS(20,30) / RS(16,24) with their rows read from
-    // device memory: when the caller gave one output slot per block (no block can need the
-    // multi-erasure worklist: two or more erasures are an error the kernel reports itself), or
-    // by the knob (gated or not)
+    // device memory when the caller gave one output slot per block (no block can need the
+    // multi-erasure worklist: two or more erasures are an error the kernel reports itself). For
+    // mixed batches of the big codes the plan path is level with the direct one on single
+    // erasures and faster on mixed ones (r04p: a device-side classify picking per batch cost 3-7 %).
     const bool small = (size_t)k * m * k * sizeof(gf::PermTab) <= kDirectTableBytes;
     const bool big = (k == 20 && m == 10) || (k == 16 && m == 8);
-    if (!small && !(big && (single_slot || g_tune.dec_direct_big))) return false;
+    if (!small && !(big && single_slot)) return false;
     const uint32_t maxe = std::max<uint32_t>(1, std::min(k, m));
     return 4 * hard_wave_bytes(m, k, maxe, stride) <= g_max_lds;
 }
@@ -340,101 +347,54 @@ static hipError_t direct_launch(const ReconArgs& a0, const CoefWords& cw, hipStr
     const uint64_t total = (uint64_t)a0.nblocks * a0.cps;
     const int flat = (int)((total + kThreads - 1) / kThreads);
     if (flat == 0) return hipSuccess;
-    // residency by shape: RS(8,12) 4 workgroups/CU (+3.6 %), RS(16,24) / RS(20,30) 3 (+1 %, r03i),
+    // residency by shape: 3 workgroups/CU for k >= 8 (RS(8,12) with the masks by scalar loads,
+    // profiles/r05/dec_twin_r05c.log: 5.88 TB/s at 3 against 5.82 at 4, 5.76 at 5, 5.37 at 2; with
+    // a vector mask load 4 had been best, +3.6 % over uncapped; RS(16,24) / RS(20,30) 3, +1 %, r03i),
     // small codes uncapped
-    const int wpc = g_tune.dir_wpc >= 0 ? g_tune.dir_wpc : (a0.k >= 16 ? 3 : a0.k >= 8 ? 4 : 0);
+    const int wpc = g_tune.dir_wpc >= 0 ? (int)g_tune.dir_wpc : (a0.k >= 8 ? 3 : 0);
     const size_t lds = occupancy_lds(wpc, 4 * direct_wave_bytes(a0.k));
-    if constexpr (TAB == 2) {   // the gated big codes: the persistent instance when asked
-        if (a0.persist_ncu) {
-            ReconArgs a = a0;
-            const int grid = flat_or_persistent(&a, (const void*)rs_recover_direct_kernel<K, POL, TAB, true>, lds, flat);
-            hipLaunchKernelGGL((rs_recover_direct_kernel<K, POL, TAB, true>), dim3(grid), dim3(kThreads), lds, s, a, cw);
-            return hipGetLastError();
-        }
-    }
     hipLaunchKernelGGL((rs_recover_direct_kernel<K, POL, TAB>), dim3(flat), dim3(kThreads), lds, s, a0, cw);
     return hipGetLastError();
 }
 
-template <int MAXE, int POL>
+template <int MAXE>
 static hipError_t hard_launch(const ReconArgs& a, int ncu, hipStream_t s) {
     const size_t lds = 4 * hard_wave_bytes(a.m, a.k, a.maxe, a.lay.stride);
     // a persistent grid of exactly the workgroups that are resident at once: more would wait
     // for a second round behind the first
-    const int grid = ncu * resident_per_cu((const void*)rs_recover_hard_kernel<MAXE, POL>, lds);
-    hipLaunchKernelGGL((rs_recover_hard_kernel<MAXE, POL>), dim3(grid), dim3(kThreads), lds, s, a);
+    const int grid = ncu * resident_per_cu((const void*)rs_recover_hard_kernel<MAXE>, lds);
+    hipLaunchKernelGGL((rs_recover_hard_kernel<MAXE>), dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 
-template <int POL>
-static hipError_t direct_dispatch(const ReconArgs& a, int ncu, hipStream_t s) {
-    // the reference's benchmark shapes at compile time, the rest by runtime k
+hipError_t launch_rs_recover_direct(const ReconArgs& a, int ncu, hipStream_t s) {
+    // the reference's benchmark shapes at compile time, the rest by runtime k. Cache policy by
+    // shape: non-temporal loads and stores (POL 3); for k <= 4 plain loads and non-temporal stores
+    // (POL 2: RS(2,3) +8 %, r02; at k = 8 plain loads cost 4 %)
     hipError_t e;
     CoefWords cw{};
     const size_t kw = (a.k + 3) / 4, words = (size_t)a.k * a.m * kw;
     const bool by_arg = g_tune.dec_direct != 2 && a.single_coef_host && words <= kCoefWords;
     if (by_arg) memcpy(cw.w, a.single_coef_host, words * 4);
     if (a.k == 20)   // RS(20,30), RS(16,24): rows from the device coefficient table
-        e = direct_launch<20, POL, 2>(a, cw, s);
+        e = direct_launch<20, 3, 2>(a, cw, s);
     else if (a.k == 16)
-        e = direct_launch<16, POL, 2>(a, cw, s);
-    else if (!by_arg)
-        e = a.k == 2 ? direct_launch<2, POL, 0>(a, cw, s) : a.k == 8 ? direct_launch<8, POL, 0>(a, cw, s)
-                                                                     : direct_launch<0, POL, 0>(a, cw, s);
+        e = direct_launch<16, 3, 2>(a, cw, s);
+    else if (a.k == 8)
+        e = by_arg ? direct_launch<8, 3, 1>(a, cw, s) : direct_launch<8, 3, 0>(a, cw, s);
+    else if (a.k == 2)
+        e = by_arg ? direct_launch<2, 2, 1>(a, cw, s) : direct_launch<2, 2, 0>(a, cw, s);
+    else if (a.k <= 4)
+        e = by_arg ? direct_launch<0, 2, 1>(a, cw, s) : direct_launch<0, 2, 0>(a, cw, s);
     else
-        e = a.k == 2 ? direct_launch<2, POL, 1>(a, cw, s) : a.k == 8 ? direct_launch<8, POL, 1>(a, cw, s)
-                                                                     : direct_launch<0, POL, 1>(a, cw, s);
+        e = by_arg ? direct_launch<0, 3, 1>(a, cw, s) : direct_launch<0, 3, 0>(a, cw, s);
     // m = 1: two erasures always leave too few shards; one output slot: a block with two or more
     // erasures is an error the direct kernel reports itself (nothing goes to the worklist)
     if (e != hipSuccess || a.m < 2 || a.max_out == 1) return e;
-    if (a.maxe <= 2) return hard_launch<2, POL>(a, ncu, s);
-    if (a.maxe <= 4) return hard_launch<4, POL>(a, ncu, s);
-    if (a.maxe <= 8) return hard_launch<8, POL>(a, ncu, s);
-    return hard_launch<16, POL>(a, ncu, s);
-}
-
-// One lane per block (grid-stride): count the blocks the direct decode would send to the
-// worklist (two or more erased data shards, recoverable, within the output slots); the last
-// workgroup to finish turns the count into the batch's path and rewinds the counters.
-__global__ __launch_bounds__(kThreads) void rs_classify_kernel(const uint32_t* masks, uint32_t nblocks, uint32_t k,
-                                                               uint32_t m, uint32_t max_out, uint32_t* gate,
-                                                               uint32_t thr_pm) {
-    const uint32_t all = low_mask(k + m), kmask = low_mask(k);
-    uint32_t multi = 0;
-    for (uint32_t b = blockIdx.x * kThreads + threadIdx.x; b < nblocks; b += gridDim.x * kThreads) {
-        const uint32_t mask = masks[b] & all;
-        const uint32_t e = k - __popc(mask & kmask);
-        multi += e >= 2 && (uint32_t)__popc(mask) >= k && !(max_out && e > max_out);
-    }
-    // wave sum, then one atomic per wave
-    for (int o = 32; o > 0; o >>= 1) multi += __shfl_xor(multi, o);
-    if ((threadIdx.x & 63) == 0 && multi) atomicAdd(gate + kGateCount, multi);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (atomicAdd(gate + kGateDone, 1u) == gridDim.x - 1) {
-            const uint32_t n = atomicAdd(gate + kGateCount, 0u);
-            atomicExch(gate, (uint64_t)n * 1000u > (uint64_t)nblocks * thr_pm ? 2u : 1u);
-            atomicExch(gate + kGateCount, 0u);
-            atomicExch(gate + kGateDone, 0u);
-        }
-    }
-}
-
-hipError_t launch_rs_classify(const uint32_t* masks, uint32_t nblocks, uint32_t k, uint32_t m, uint32_t max_out,
-                              uint32_t* gate, uint32_t thr_pm, int ncu, hipStream_t s) {
-    const uint32_t need = (nblocks + kThreads - 1) / kThreads;
-    const int grid = (int)std::max<uint32_t>(1, std::min<uint32_t>(need, (uint32_t)ncu * 4));
-    hipLaunchKernelGGL(rs_classify_kernel, dim3(grid), dim3(kThreads), 0, s, masks, nblocks, k, m, max_out, gate,
-                       thr_pm);
-    return hipGetLastError();
-}
-
-hipError_t launch_rs_recover_direct(const ReconArgs& a, int ncu, hipStream_t s) {
-    // cache policy: 3 non-temporal loads and stores (default), 2 plain loads + non-temporal
-    // stores, else plain
-    const int nt = g_tune.dir_nt >= 0 ? (g_tune.dir_nt & 3) : (a.k <= 4 ? 2 : 3);
-    return nt == 3 ? direct_dispatch<3>(a, ncu, s) : nt == 2 ? direct_dispatch<2>(a, ncu, s) : direct_dispatch<0>(a, ncu, s);
+    if (a.maxe <= 2) return hard_launch<2>(a, ncu, s);
+    if (a.maxe <= 4) return hard_launch<4>(a, ncu, s);
+    if (a.maxe <= 8) return hard_launch<8>(a, ncu, s);
+    return hard_launch<16>(a, ncu, s);
 }
 
 }  // namespace fk

@@ -37,6 +37,12 @@ PAYLOAD = 1200
 SHARD_LEN = PAYLOAD + 2          # + big-endian uint16 length trailer
 SHARD_STRIDE = 1216              # 16-byte aligned device slot per shard
 HBM_PEAK = 8.0e12                # MI355X HBM3E spec, bytes/s (MI355X_MICROARCH.md)
+# traffic-twin ceiling search (best_twin): resident workgroups per CU (0: as many as fit) and
+# offsets of the twin's output from its buffer's start (the output buffers carry TWIN_SLACK spare
+# bytes for them; the codec kernels always write at offset 0)
+TWIN_WPC = (1, 2, 3, 4, 5, 0)
+TWIN_OFFSETS = (0, 4160, 65600)
+TWIN_SLACK = 1 << 17
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of this bench (separate passes, tools/pmc_traffic.py,
 # gfx950 FETCH_SIZE x2 correction): HBM bytes per launch of each codec kernel, with the hash of
 # the kernel's machine code at profiling time (tools/gpu_round.sh pmc refreshes it)
@@ -104,6 +110,15 @@ def parse():
     return p.parse_args()
 
 
+def padded(torch, shape, dev):
+    """A zeroed device tensor of `shape` at the start of a buffer TWIN_SLACK bytes longer (room for
+    the traffic twins' output offsets, best_twin)."""
+    n = 1
+    for d in shape:
+        n *= d
+    return torch.zeros(n + TWIN_SLACK, dtype=torch.uint8, device=dev)[:n].view(*shape)
+
+
 class RankBatch:
     """One rank's slice of the global batch, resident in HBM: data shards [B, k, 1216] and
     parity shards [B, m, 1216] in separate buffers, one erased data shard per block (masks),
@@ -115,11 +130,11 @@ class RankBatch:
         self.B, self.k, self.m, self.first = B, k, m, first_block
         self.data = torch.empty((B, k, SHARD_STRIDE), dtype=torch.uint8, device=dev)
         codec.synth_data(seed, first_block, B, k, PAYLOAD, self.data.data_ptr(), k * SHARD_STRIDE, SHARD_STRIDE)
-        self.parity = torch.zeros((B, m, SHARD_STRIDE), dtype=torch.uint8, device=dev)
+        self.parity = padded(torch, (B, m, SHARD_STRIDE), dev)
         self.masks = torch.empty((B,), dtype=torch.int32, device=dev)
         self.erased = torch.empty((B,), dtype=torch.int32, device=dev)
         codec.synth_single_erasures(seed, first_block, B, k, m, self.masks.data_ptr(), self.erased.data_ptr())
-        self.recovered = torch.zeros((B, 1, SHARD_STRIDE), dtype=torch.uint8, device=dev)
+        self.recovered = padded(torch, (B, 1, SHARD_STRIDE), dev)
 
 
 class RankStep:
@@ -182,7 +197,8 @@ def host_threads():
 
 def oracle_spot_check(k, m, sample):
     """cpu_baseline leg, the checker half: the parity of 64 blocks the device encoded equals the
-    CPU oracle's (oracle/oracle.py, the reference's buildMatrix and mulTable restated)."""
+    CPU oracle's (oracle/oracle.py, the reference's buildMatrix and mulTable restated). None when
+    the oracle cannot run (never a truthy string)."""
     try:
         import numpy as np
         from oracle import oracle as orc
@@ -190,7 +206,8 @@ def oracle_spot_check(k, m, sample):
         orc.rs_encode(k, m, want)
         return bool(np.array_equal(sample[:, :, :SHARD_LEN], want))
     except Exception as exc:  # oracle unavailable: report, do not hide
-        return "unchecked: %s" % exc
+        print("bench.py: oracle spot-check not run: %s" % exc, file=sys.stderr, flush=True)
+        return None
 
 
 def cpu_baseline(k, m, blocks, seed, budget_s=12.0):
@@ -337,19 +354,55 @@ def host_resident(torch, fec, codec, k, m, blocks, seed, reps=6):
     return out
 
 
+def timed_bursts(torch, stream, fn, burst=3, bursts=3):
+    """ms per launch of fn: the median over `bursts` bursts of `burst` back-to-back launches."""
+    r = []
+    for _ in range(bursts):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(burst):
+            fn()
+        e1.record(stream)
+        e1.synchronize()
+        r.append(e0.elapsed_time(e1) / burst)
+    return sorted(r)[len(r) // 2]
+
+
+def best_twin(torch, stream, twin, nbytes, offsets=TWIN_OFFSETS, wpcs=TWIN_WPC):
+    """The box's ceiling for an access shape: twin(wpc, off) (a traffic twin at `wpc` resident
+    workgroups per CU, output `off` bytes into its buffer) timed at every residency and output
+    offset; returns the best TB/s with its (wpc, off) and every rate measured."""
+    rates = {}
+    for off in offsets:
+        for w in wpcs:
+            fn = lambda w=w, off=off: twin(w, off)
+            fn()
+            rates["wpc%d off%d" % (w, off)] = round(nbytes / timed_bursts(torch, stream, fn) / 1e9, 3)
+    best = max(rates, key=rates.get)
+    return {"probe_best_TBps": rates[best], "probe_best_at": best, "sweep_TBps": rates}
+
+
 def box_probe(torch, codec, b, step, stream, enc_bytes, dec_bytes, rounds=5, burst=4):
     """Times the traffic twin of the encode and of the direct decode (fec_probe.hip: the same bytes,
     launch shape, residency and cache policy, no field arithmetic) in bursts interleaved with bursts
-    of the kernels themselves. Returns per kernel the twin's TB/s (the box's ceiling for that
-    access shape), the kernel's TB/s in the same interleaved bursts, and their ratio."""
-    def enc_twin():
-        codec.probe_encode_traffic_raw(b.k, b.m, SHARD_LEN, b.B, b.data.data_ptr(), b.k * SHARD_STRIDE,
-                                       b.parity.data_ptr(), b.m * SHARD_STRIDE, SHARD_STRIDE)
+    of the kernels themselves. Returns per kernel the twin's TB/s at the kernel's own residency
+    (the same-shape figure), the kernel's TB/s in the same interleaved bursts, and their ratio; then
+    each twin's best over residency and output placement (probe_best_TBps, best_twin), and the
+    shape-independent reference: the block's k data shards read whole plus one store per block
+    (fec_probe_stream_traffic), at its best residency."""
+    L, S = SHARD_LEN, SHARD_STRIDE
 
-    def dec_twin():
-        codec.probe_recover_traffic_raw(b.k, b.m, SHARD_LEN, b.B, b.data.data_ptr(), b.k * SHARD_STRIDE,
-                                        b.parity.data_ptr(), b.m * SHARD_STRIDE, SHARD_STRIDE, b.masks.data_ptr(),
-                                        b.recovered.data_ptr(), SHARD_STRIDE)
+    def enc_twin(wpc=-1, off=0):
+        codec.probe_encode_traffic_raw(b.k, b.m, L, b.B, b.data.data_ptr(), b.k * S, b.parity.data_ptr() + off,
+                                       b.m * S, S, wpc)
+
+    def dec_twin(wpc=-1, off=0):
+        codec.probe_recover_traffic_raw(b.k, b.m, L, b.B, b.data.data_ptr(), b.k * S, b.parity.data_ptr(), b.m * S, S,
+                                        b.masks.data_ptr(), b.recovered.data_ptr() + off, S, wpc)
+
+    def stream_ref(wpc=0, off=0):
+        codec.probe_stream_traffic_raw(b.k, L, b.B, b.data.data_ptr(), b.k * S, b.recovered.data_ptr() + off, S, S,
+                                       wpc)
 
     def timed_burst(fn):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -373,6 +426,10 @@ def box_probe(torch, codec, b, step, stream, enc_bytes, dec_bytes, rounds=5, bur
         out[name] = {"probe_ms": round(tw, 4), "probe_TBps": round(nbytes / tw / 1e9, 3),
                      "kernel_ms_interleaved": round(kt, 4), "kernel_TBps_interleaved": round(nbytes / kt / 1e9, 3),
                      "kernel_frac_of_probe_interleaved": round(tw / kt, 4)}
+        out[name].update(best_twin(torch, stream, twin, nbytes))
+    # the reference moves k reads + 1 write per block, as the decode does
+    out["stream_reference"] = {"shape": "%d contiguous data shards read + 1 store per block" % b.k,
+                               **best_twin(torch, stream, stream_ref, dec_bytes)}
     return out
 
 
@@ -510,8 +567,9 @@ def main():
         ok_roundtrip = bool(okt.item())
 
     # 64 random blocks (data + parity) for the oracle spot-check, which runs in the cpu_baseline
-    # leg (N = 1, rank 0): the only part of bench.py that touches oracle/
-    ok_parity = "not run: the oracle spot-check is part of the N = 1 cpu_baseline leg"
+    # leg (N = 1, rank 0): the only part of bench.py that touches oracle/. Otherwise None (not
+    # run), with the reason beside it
+    ok_parity = None
     parity_sample = None
     if rank == 0:
         pick = torch.randperm(B, device=dev)[:64]
@@ -564,10 +622,13 @@ def main():
                          "traffic": None if traffic is None else round(traffic / 1e9, 3),
                          "traffic_unit": "GB per launch", "traffic_profile": traffic_src,
                          "kernel": dominant, "algorithmic_bytes_per_launch": dom_bytes,
-                         # this box's ceiling for the kernel's access shape (its traffic twin) and
-                         # the timed-region rate over it
+                         # the kernel's traffic twin at the kernel's own residency (same shape) and
+                         # its best over residency and placement (this box's ceiling for the shape),
+                         # with the timed-region rate over each
                          "probe_TBps": probe[dom_name]["probe_TBps"],
                          "frac_of_probe": round(dom_bw / 1e12 / probe[dom_name]["probe_TBps"], 4),
+                         "probe_best_TBps": probe[dom_name]["probe_best_TBps"],
+                         "frac_of_probe_best": round(dom_bw / 1e12 / probe[dom_name]["probe_best_TBps"], 4),
                          "probe_kernel": "fec_probe.hip probe_%s_kernel (include/fec_probe.h)" % (
                              "encode" if dom_name == "encode" else "recover")},
             "kernels": {
@@ -576,19 +637,24 @@ def main():
                            "frac": round(enc_bw / HBM_PEAK, 4),
                            "read_frac": round(B * k * L / (enc_ms / 1000.0) / HBM_PEAK, 4),
                            "frac_of_probe": round(enc_bw / 1e12 / probe["encode"]["probe_TBps"], 4),
+                           "frac_of_probe_best": round(enc_bw / 1e12 / probe["encode"]["probe_best_TBps"], 4),
                            "probe": probe["encode"]},
                 "decode": {"ms": round(dec_ms, 4), "GB/s": round(dec_bw / 1e9, 1), "bytes": dec_bytes,
                            "frac": round(dec_bw / HBM_PEAK, 4),
                            "read_frac": round(B * k * L / (dec_ms / 1000.0) / HBM_PEAK, 4),
                            "api": "fec_rs_recover_batch (direct single-erasure kernel, no plan launch)",
                            "frac_of_probe": round(dec_bw / 1e12 / probe["decode"]["probe_TBps"], 4),
+                           "frac_of_probe_best": round(dec_bw / 1e12 / probe["decode"]["probe_best_TBps"], 4),
                            "probe": probe["decode"]},
+                "stream_reference": probe["stream_reference"],
                 "decode_inplace": {"ms": round(inplace_ms, 4),
                                    "GB/s": round(dec_bytes / (inplace_ms / 1e3) / 1e9, 1),
                                    "api": "fec_rs_reconstruct_batch (direct kernel, in place), not in the step"},
                 "step_frac": round((enc_bytes + dec_bytes) / ((enc_ms + dec_ms) / 1000.0) / HBM_PEAK, 4),
             },
-            "check": {"roundtrip_full_batch": ok_roundtrip, "encode_vs_oracle_64_blocks": ok_parity},
+            "check": {"roundtrip_full_batch": ok_roundtrip, "encode_vs_oracle_64_blocks": ok_parity,
+                      "encode_vs_oracle_note": "run in the N = 1 cpu_baseline leg only (the one part of bench.py "
+                                               "that may touch oracle/); the round trip checks every block"},
         }
         if world == 1 and args.host_blocks > 0:
             del batch, step, encode, decode, decode_inplace   # free the device batch first

@@ -18,6 +18,12 @@
  *                               (sorted plans + rebuild): per block the first k present shards
  *                               and one store per erased data shard into out (block b, row r at
  *                               out + b*out_bs + r*ss), in block order, at the rebuild's residency
+ *   fec_probe_stream_traffic    shape-independent reference: per block nin consecutive shards
+ *                               of `in` read (shard stride ss), one chunk-wise store to out
+ *                               (nin 2, 8, 16, 20)
+ * Every twin takes wpc, the resident workgroups per CU it runs at: -1 the twinned kernel's own
+ * (bench.py's same-shape figure), 0 as many as fit, n > 0 a cap; the best over residency is the
+ * box's ceiling for the access shape (probe_best_TBps).
  *   fec_probe_link              the host link as the FEC_HOST paths drive it: hipMemcpyAsync of
  *                               `bytes` between pinned host and device buffers, H2D alone, D2H
  *                               alone and both at once on two streams (best of reps); GB/s into
@@ -38,13 +44,15 @@ extern "C" {
 #endif
 
 int fec_probe_encode_traffic(fec_ctx *ctx, int k, int m, size_t shard_len, size_t nblocks, const void *data,
-                             size_t dbs, void *parity, size_t pbs, size_t ss);
+                             size_t dbs, void *parity, size_t pbs, size_t ss, int wpc);
 int fec_probe_recover_traffic(fec_ctx *ctx, int k, int m, size_t shard_len, size_t nblocks, const void *data,
                               size_t dbs, const void *parity, size_t pbs, size_t ss, const uint32_t *masks,
-                              void *out, size_t out_bs);
+                              void *out, size_t out_bs, int wpc);
 int fec_probe_rebuild_traffic(fec_ctx *ctx, int k, int m, size_t shard_len, size_t nblocks, const void *data,
                               size_t dbs, const void *parity, size_t pbs, size_t ss, const uint32_t *masks,
-                              void *out, size_t out_bs);
+                              void *out, size_t out_bs, int wpc);
+int fec_probe_stream_traffic(fec_ctx *ctx, int nin, size_t shard_len, size_t nblocks, const void *in, size_t in_bs,
+                             void *out, size_t out_bs, size_t ss, int wpc);
 int fec_probe_link(fec_ctx *ctx, size_t bytes, int reps, double *out);
 
 #ifdef __cplusplus

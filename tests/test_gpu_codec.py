@@ -160,10 +160,10 @@ def test_rs_host_path_matches_oracle(codec, oracle, k, m):
     assert np.array_equal(dmg[:, :k], sh[:, :k])
 
 
-@pytest.mark.parametrize("k,fix2", [(1, 1), (2, 1), (2, 0), (3, 1), (9, 1), (31, 1)])   # fix2: XOR(2,1)'s own kernel
+@pytest.mark.parametrize("k", [1, 2, 3, 5, 9, 31])
 @pytest.mark.parametrize("L", [1, 6, 18, 1202, 1436])
-def test_xor_device_matches_oracle(codec, oracle, torch, k, fix2, L):
-    rng = np.random.default_rng(k + L + 100 * fix2)
+def test_xor_device_matches_oracle(codec, oracle, torch, fec, k, L):
+    rng = np.random.default_rng(k + L)
     n = k + 1
     S = (L + 15) // 16 * 16
     B = 65
@@ -185,14 +185,9 @@ def test_xor_device_matches_oracle(codec, oracle, torch, k, fix2, L):
     st_ref = oracle.xor_reconstruct(k, want, masks)
     dd = torch.from_numpy(dmg).cuda()
     ds = torch.zeros(B, dtype=torch.int32, device="cuda")
-    old = codec.set_tuning(xor_fix2=fix2)
-    try:
-        codec.xor_reconstruct(k, dd, torch.from_numpy(masks.view(np.int32)).cuda(), status=ds, shard_len=L)
-        codec.sync()
-    except Exception:
-        pass
-    finally:
-        codec.set_tuning(**old)
+    codec.xor_reconstruct(k, dd, torch.from_numpy(masks.view(np.int32)).cuda(), status=ds, shard_len=L)
+    rc = codec.lib_sync_rc()
+    assert rc == (fec.FEC_ERR_TOO_FEW_SHARDS if (st_ref != 0).any() else fec.FEC_OK)
     got = dd.cpu().numpy()
     st = ds.cpu().numpy()
     assert np.array_equal(st == 0, st_ref == 0)
@@ -289,31 +284,15 @@ def test_rs_recover_out_of_place(codec, oracle, torch, fec, k, m, slots):
     assert saw_over == over
 
 
-# Every RS encode kernel form (fixed-shape flat grid, ticket-queue at prefetch depth 1 and 2,
-# generic runtime-shape kernel) against the oracle, at batch sizes that leave the 8 queue
-# ranges empty, partial and ragged (B * ceil(L/16) items vs 8 ranges of 256-item chunks).
+# Every shipped RS encode kernel against the oracle: the code's own kernel (RS(2,3) by its parity
+# row, RS(8,12) dyadic, RS(16,24) / RS(20,30) bit-sliced; every other shape the generic kernel) and
+# the generic kernel on the reference's shapes too (knob enc_fixed 0), at residency caps of the
+# fixed-shape forms, over batch sizes and tails that leave workgroups empty, partial and ragged.
 ENC_VARIANTS = {
+    "own": dict(enc_fixed=1),
+    "own_wpc2": dict(enc_fixed=1, enc_wpc=2, enc_bwpc=2),
     "generic": dict(enc_fixed=0),
-    "fixed_flat": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=1, enc_x23=0),
-    "fixed_flat_matrix": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=0, enc_x23=0),
-    # shard loads issued before the table staging (knob enc_early), dyadic and matrix bodies
-    "fixed_flat_early": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=1, enc_bits=0, enc_early=1, enc_x23=0),
-    "fixed_flat_matrix_early": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_dyadic=0, enc_bits=0, enc_early=1,
-                                    enc_x23=0),
-    # RS(2,3) by its [3 2] parity row, no tables (knob enc_x23; other codes: the fixed kernels)
-    "fixed_flat_x23": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_x23=1),
-    "fixed_flat_x23_plain": dict(enc_fixed=1, enc_queue=0, enc_wpc=3, enc_x23=1, enc_nt=0),
-    "queue_d0": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=0),
-    "queue_d0_nodrain": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=-1),
-    "queue_d1": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=1),
-    "queue_d2": dict(enc_fixed=1, enc_queue=1, enc_qwpc=2, enc_qdepth=2),
-    "queue_d1_1wg": dict(enc_fixed=1, enc_queue=1, enc_qwpc=1, enc_qdepth=1),
-    # bit-sliced XOR network (RS(8,12), RS(16,24), RS(20,30); RS(2,3) keeps the fixed kernel)
-    "bits": dict(enc_fixed=1, enc_queue=0, enc_bits=11, enc_bwpc=0),
-    "bits_wpc2": dict(enc_fixed=1, enc_queue=0, enc_bits=11, enc_bwpc=2),
-    "bits_plain": dict(enc_fixed=1, enc_queue=0, enc_bits=11, enc_nt=0),
-    "bits_stream": dict(enc_fixed=1, enc_queue=0, enc_bits=15, enc_bwpc=0),
-    "bits_off": dict(enc_fixed=1, enc_queue=0, enc_bits=0),
+    "generic_wpc2": dict(enc_fixed=0, gen_wpc=2),
 }
 
 
@@ -342,40 +321,28 @@ def test_rs_encode_kernel_variants_match_oracle(codec, oracle, torch, variant, k
     assert not got[:, :, L:].any()               # pad to the 16-byte boundary written as zeros
 
 
-# Both reconstruct kernel forms (workgroup tiles; wave-private plans for shards of 32+ chunks)
-# in place and out of place, against the oracle, with the erasure counts mixed inside waves.
-# wave 2: plans built in-kernel; 3, 4: as 1, 2 with two items per lane loaded together (shards
-# of 64+ chunks, at most 4 erasures per block); 5, 6: as 1, 2 with two items one after the other;
-# 7: the direct form (fec_recover.hip: single-erasure tables, in-wave plans for waves holding a
-# multi-erasure block) where the code's tables fit, else as 1; 1, 3, 5 use the sorted parallel
-# plans (fec_plan.hip), 8 is 1 with the one-lane-per-block plan kernel in block order, 9 is 1
-# with the compile-time-k rebuild loading all k inputs up front (1 and the rest: RS(16,24) with
-# the rolling load window where shards have 64+ chunks); 10, 11, 12 are 1 with the two-tier
-# rebuild (fec_decode.hip: waves of <= 1, 2, 4 rows in the small-register launch, the rest from
-# the worklist; RS(16,24) and RS(20,30) with shards of 64+ chunks, else as 1); 13 is 7 with the
-# RS(16,24) / RS(20,30) direct form too (coefficient rows by scalar loads from device memory);
-# 14 is 13 gated on the device (rs_classify_kernel picks the direct or the plan path per batch),
-# 15 the same with the threshold at 100 % (always the direct path and its worklist kernel); 16 is
-# 1 with the row-pipelined rolling rebuild for RS(16,24) too (dec_fixk 3; RS(20,30) has it by default);
-# 17 is 1 with the table-copy rebuild of fec_rebuild.hip (dec_fixk 4: PermTab rows copied from the
-# workgroup's 256-coefficient table, input addresses as per-block offsets), 18 and 19 the same with
-# rolling windows of 4 and 6 loads, 20 is 17 with the inputs split by 64-bit shifts, 21 is 17 with the
-# plan records sorted over 256-block windows (dec_psort 4; the rest over 64, the default), 22 is 17
-# with the records sorted per segment (dec_psort 0, the round-2 order); 23 and 24 are 17 and 22 with
-# the plan kernel's form 2 (dec_pv 2, the default: conflict-free log(i ^ j) table copies, merged D / N
-# sums; the rest run form 1), 25 is 23 with the padded rebuild slice (dec_lpad: the wave's two blocks'
-# PermTab rows 32 banks apart), 26 is 23 with plan form 3 (dec_pv 3: RS(16,24) and RS(20,30) by the
-# kernel compiled for the code), 27 and 28 are 23 and 22 with form 3 on two segments at a time (dec_pv
-# 4; 28's one-segment windows grow to the pair), 29-31 are 23 with the rank-first form (dec_pv 5:
-# windows ranked from the masks, records straight to their positions) over 256-, 64- and 512-block
-# windows
-@pytest.mark.parametrize("wave", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22,
-                                  23, 24, 25, 26, 27, 28, 29, 30, 31])
-@pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10)])
-# L = 1008 / 1017: shards of 63 / 64 chunks, the edge of the two-block wave slices (rolling window)
+# Every shipped reconstruct path against the oracle, in place and out of place, with the erasure
+# counts mixed inside waves: "default" (the direct kernel and its multi-erasure worklist for RS(2,3)
+# and RS(8,12); sorted plans + the rebuild for RS(16,24) / RS(20,30): fec_rebuild.hip where shards
+# have 64+ chunks, the compile-time-k wave form below that), "plan" (no direct kernel: sorted plans +
+# the wave form for every code), "tile" (plans in block order + the workgroup-tile rebuild, the
+# short-shard path, on long shards too), "table" (the direct kernel's rows copied from the PermTab
+# table rather than expanded from the kernel argument), and "wpc2" (the default at two workgroups
+# per CU). L = 1008 / 1017: shards of 63 / 64 chunks, the edge of the rebuild's two-block slices.
+DEC_VARIANTS = {
+    "default": {},
+    "plan": dict(dec_direct=0),
+    "tile": dict(dec_direct=0, dec_wave=0),
+    "table": dict(dec_direct=2),
+    "wpc2": dict(dir_wpc=2, dec_wpc=2),
+}
+
+
+@pytest.mark.parametrize("variant", sorted(DEC_VARIANTS))
+@pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10), (4, 8), (10, 22)])
 @pytest.mark.parametrize("L", [513, 1008, 1017, 1202, 1436])
-def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, wave, k, m, L):
-    rng = np.random.default_rng(11 * k + L + wave)
+def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, tune, variant, k, m, L):
+    rng = np.random.default_rng(11 * k + L + 1000 * sorted(DEC_VARIANTS).index(variant))
     n, B = k + m, 389
     S = (L + 15) // 16 * 16
     sh = _rand_shards(rng, B, n, S, L)
@@ -388,96 +355,52 @@ def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, 
                 data_np[b, i] = 0x3C
     par = torch.from_numpy(np.ascontiguousarray(sh[:, k:])).cuda()
     dm = torch.from_numpy(masks.view(np.int32)).cuda()
-    old = codec.set_tuning(dec_wave=1 if wave else 0, dec_fused=1 if wave in (2, 4, 6) else 0,
-                           dec_ipl={3: 2, 4: 2, 5: 3, 6: 3}.get(wave, 1),
-                           dec_direct=1 if wave in (7, 13, 14, 15) else 0,
-                           dec_direct_big=1 if wave in (13, 14, 15) else 0, dec_gate=1 if wave in (14, 15) else 0,
-                           dec_gate_pm=1000 if wave == 15 else 10,
-                           dec_sorted=0 if wave == 8 else 1, dec_fixk={9: 1, 16: 3, 17: 4, 18: 4, 19: 4, 20: 4, 21: 4, 22: 4, 23: 4, 24: 4, 25: 4, 26: 4, 27: 4, 28: 4, 29: 4, 30: 4, 31: 4}.get(wave, 2),
-                           dec_win={18: 4, 19: 6}.get(wave, 0), dec_s64=1 if wave == 20 else 0,
-                           dec_psort={21: 4, 22: 0, 24: 0, 28: 0}.get(wave, 1), dec_pv={23: 2, 24: 2, 25: 2, 26: 3, 27: 4, 28: 4, 29: 5, 30: 5, 31: 5}.get(wave, 1),
-                           dec_rwin={30: 1, 31: 8}.get(wave, 4),
-                           dec_lpad=1 if wave == 25 else 0,
-                           dec_tier={10: 1, 11: 2, 12: 4}.get(wave, 0))
-    try:
-        out = torch.full((B, m, S), 0xEE, dtype=torch.uint8, device="cuda")
-        data = torch.from_numpy(data_np).cuda()
-        codec.rs_recover_split(k, m, data, par, dm, out, shard_len=L)
-        codec.sync()
-        got = out.cpu().numpy()
-        for b in range(B):
-            miss = [i for i in range(k) if not (masks[b] >> i) & 1]
-            for r, i in enumerate(miss):
-                assert np.array_equal(got[b, r, :L], sh[b, i, :L]), (b, r, i)
-        codec.rs_reconstruct_split(k, m, data, par, dm, shard_len=L)
-        codec.sync()
-        assert np.array_equal(data.cpu().numpy()[:, :, :L], sh[:, :k, :L])
-    finally:
-        codec.set_tuning(**old)
+    tune(**DEC_VARIANTS[variant])
+    out = torch.full((B, m, S), 0xEE, dtype=torch.uint8, device="cuda")
+    data = torch.from_numpy(data_np).cuda()
+    codec.rs_recover_split(k, m, data, par, dm, out, shard_len=L)
+    codec.sync()
+    got = out.cpu().numpy()
+    for b in range(B):
+        miss = [i for i in range(k) if not (masks[b] >> i) & 1]
+        for r, i in enumerate(miss):
+            assert np.array_equal(got[b, r, :L], sh[b, i, :L]), (b, r, i)
+    codec.rs_reconstruct_split(k, m, data, par, dm, shard_len=L)
+    codec.sync()
+    assert np.array_equal(data.cpu().numpy()[:, :, :L], sh[:, :k, :L])
 
 
 # The sorted plan kernel's two forms on codes of both sum forms: n - k < k sums over the
-# complement (RS(16,24), RS(20,30), RS(9,10)), n - k >= k over the inputs (RS(4,12), RS(8,16),
-# RS(10,32), RS(1,4)), with 1..min(k, m) data erasures and parity losses mixed in.
-@pytest.mark.parametrize("pv", [1, 2, 3, 4, 5])   # 3-5: RS(16,24) / RS(20,30) by the compiled-code form (4: two
-# segments at a time, 5: rank-first), the rest 2
+# complement (RS(16,24), RS(20,30) by the form compiled for the code; RS(9,10) by the general
+# form), n - k >= k over the inputs (RS(4,12), RS(8,16), RS(10,32), RS(1,4)), with 1..min(k, m)
+# data erasures and parity losses mixed in, over batches whose last sort window is ragged.
 @pytest.mark.parametrize("k,m", [(16, 8), (20, 10), (9, 1), (4, 8), (8, 8), (10, 22), (1, 3)])
-def test_rs_plan_forms_match_oracle(codec, oracle, torch, pv, k, m):
-    rng = np.random.default_rng(1000 * k + m + pv)
-    n, B, L = k + m, 517, 1202
-    S = (L + 15) // 16 * 16
-    sh = _rand_shards(rng, B, n, S, L)
-    oracle.rs_encode(k, m, sh)
-    masks = _random_masks(rng, B, k, m)
-    data_np = np.ascontiguousarray(sh[:, :k]).copy()
-    for b in range(B):
-        for i in range(k):
-            if not (masks[b] >> i) & 1:
-                data_np[b, i] = 0x5A
-    par = torch.from_numpy(np.ascontiguousarray(sh[:, k:])).cuda()
-    dm = torch.from_numpy(masks.view(np.int32)).cuda()
-    old = codec.set_tuning(dec_pv=pv, dec_direct=0)
-    try:
-        data = torch.from_numpy(data_np).cuda()
-        codec.rs_reconstruct_split(k, m, data, par, dm, shard_len=L)
-        codec.sync()
-        assert np.array_equal(data.cpu().numpy()[:, :, :L], sh[:, :k, :L])
-    finally:
-        codec.set_tuning(**old)
-
-
-# The plan kernels of later sub-batches on a side stream beside the rebuild of earlier ones (knob
-# dec_povl): batches of several sub-batches with a ragged last one, out of place and in place.
-@pytest.mark.parametrize("povl,pv,lpad", [(2, 1, 0), (4, 2, 0), (8, 1, 1), (3, 2, 1), (1, 2, 1), (1, 3, 0), (3, 3, 0), (1, 4, 0), (3, 4, 1), (1, 5, 0), (3, 5, 1)])
-@pytest.mark.parametrize("k,m", [(16, 8), (20, 10)])
-def test_rs_plan_overlap_matches_oracle(codec, oracle, torch, povl, pv, lpad, k, m):
-    rng = np.random.default_rng(7 * k + povl + pv)
-    n, B, L = k + m, 9000 + 37, 1202
+@pytest.mark.parametrize("B", [517, 9037])
+def test_rs_plan_forms_match_oracle(codec, oracle, torch, tune, k, m, B):
+    rng = np.random.default_rng(1000 * k + m + B)
+    n, L = k + m, 1202
     S = (L + 15) // 16 * 16
     sh = _rand_shards(rng, B, n, S, L)
     oracle.rs_encode(k, m, sh)
     masks = _random_masks(rng, B, k, m)
     data_np = np.ascontiguousarray(sh[:, :k]).copy()
     lost = ~((masks[:, None] >> np.arange(k)[None, :]) & 1).astype(bool)
-    data_np[lost] = 0x77
+    data_np[lost] = 0x5A
     par = torch.from_numpy(np.ascontiguousarray(sh[:, k:])).cuda()
     dm = torch.from_numpy(masks.view(np.int32)).cuda()
-    old = codec.set_tuning(dec_povl=povl, dec_pv=pv, dec_lpad=lpad, dec_direct=0)
-    try:
-        data = torch.from_numpy(data_np).cuda()
-        out = torch.full((B, m, S), 0xEE, dtype=torch.uint8, device="cuda")
-        codec.rs_recover_split(k, m, data, par, dm, out, shard_len=L)
-        codec.sync()
-        got = out.cpu().numpy()
-        ne = lost.sum(axis=1)
-        for b in np.flatnonzero(ne):
-            miss = np.flatnonzero(lost[b])
-            assert np.array_equal(got[b, :len(miss), :L], sh[b, miss, :L]), b
-        codec.rs_reconstruct_split(k, m, data, par, dm, shard_len=L)
-        codec.sync()
-        assert np.array_equal(data.cpu().numpy()[:, :, :L], sh[:, :k, :L])
-    finally:
-        codec.set_tuning(**old)
+    tune(dec_direct=0)
+    data = torch.from_numpy(data_np).cuda()
+    out = torch.full((B, m, S), 0xEE, dtype=torch.uint8, device="cuda")
+    codec.rs_recover_split(k, m, data, par, dm, out, shard_len=L)
+    codec.sync()
+    got = out.cpu().numpy()
+    ne = lost.sum(axis=1)
+    for b in np.flatnonzero(ne):
+        miss = np.flatnonzero(lost[b])
+        assert np.array_equal(got[b, :len(miss), :L], sh[b, miss, :L]), b
+    codec.rs_reconstruct_split(k, m, data, par, dm, shard_len=L)
+    codec.sync()
+    assert np.array_equal(data.cpu().numpy()[:, :, :L], sh[:, :k, :L])
 
 
 def test_rs_32_0_fully_present_is_untouched(codec, torch, fec):
@@ -647,19 +570,18 @@ def test_rs_host_pipeline_many_chunks_multi_erasure(codec, oracle, fec, k, m, ch
         codec.set_tuning(**old)
 
 
-@pytest.mark.parametrize("pool,threads,chunk", [(1, 8, 0), (1, 3, 1100), (0, 8, 1100), (1, 16, 600), (0, 5, 0)])
-def test_rs_host_copy_pool_matches_oracle(codec, oracle, fec, pool, threads, chunk):
+@pytest.mark.parametrize("threads,chunk", [(8, 0), (3, 1100), (16, 600), (5, 0)])
+def test_rs_host_copy_pool_matches_oracle(codec, oracle, fec, threads, chunk):
     """FEC_HOST (pageable) with chunks of >= 512 blocks, whose staging and scatter copies run on
-    several host threads: the persistent copy workers (knob host_pool 1) or threads made per call
-    (0), with 3..16 parts and one chunk or several. Encode and a multi-erasure reconstruct against
-    the oracle."""
-    rng = np.random.default_rng(300 + pool + threads + chunk)
+    the persistent copy workers, with 3..16 parts and one chunk or several. Encode and a
+    multi-erasure reconstruct against the oracle."""
+    rng = np.random.default_rng(300 + threads + chunk)
     k, m, B, L = 8, 4, 3000, 600
     n = k + m
     full = np.zeros((B, n, L), dtype=np.uint8)
     full[:, :k] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
     oracle.rs_encode(k, m, full)
-    old = codec.set_tuning(host_pool=pool, host_threads=threads, host_chunk=chunk)
+    old = codec.set_tuning(host_threads=threads, host_chunk=chunk)
     try:
         data = full[:, :k].copy()
         par = np.zeros((B, m, L), dtype=np.uint8)

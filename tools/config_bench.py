@@ -12,6 +12,11 @@
 Algorithmic bytes (L = 1202): encode k*L read + m*L written per block; decode (recover into an
 output buffer) (k + e_d)*L per block with e_d >= 1 erased data shards, nothing for blocks whose
 data shards all arrived. Prints one JSON line per config.
+
+Beside each kernel: its traffic twin (include/fec_probe.h) at the kernel's own residency (the
+same-shape figure, *_probe_TB/s) and the twin's best over residency and output placement
+(*_probe_best_TB/s, bench.best_twin: the box's ceiling for the access shape), with the kernel's
+fraction of each.
 """
 import argparse
 import importlib
@@ -20,6 +25,8 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import bench  # noqa: E402  (best_twin, padded: the bench's ceiling search)
 
 PAYLOAD, L, S = 1200, 1202, 1216
 
@@ -51,12 +58,23 @@ def make_data(torch, B, k, g):
     return data
 
 
+def twin_fields(torch, name, twin, nbytes, t_kernel, iters):
+    """The twin at the kernel's residency and its best over residency and placement, with the
+    kernel's fraction of each (t_kernel: ms per launch)."""
+    same = round(nbytes / timed(torch, twin, iters) / 1e9, 3)
+    best = bench.best_twin(torch, torch.cuda.current_stream(), twin, nbytes)
+    kern = nbytes / t_kernel / 1e9
+    return {"%s_probe_TB/s" % name: same, "%s_frac_of_probe" % name: round(kern / same, 4),
+            "%s_probe_best_TB/s" % name: best["probe_best_TBps"], "%s_probe_best_at" % name: best["probe_best_at"],
+            "%s_frac_of_probe_best" % name: round(kern / best["probe_best_TBps"], 4)}
+
+
 def run_rs(torch, fec, codec, k, m, B, multi, iters, seed):
     n = k + m
     g = torch.Generator(device="cuda")
     g.manual_seed(seed)
     data = make_data(torch, B, k, g)
-    parity = torch.zeros((B, m, S), dtype=torch.uint8, device="cuda")
+    parity = bench.padded(torch, (B, m, S), "cuda")
     if multi:
         # e ~ U{1..multi} erasures per block, a uniform subset of the n shards
         e = torch.randint(1, multi + 1, (B,), generator=g, device="cuda")
@@ -73,7 +91,7 @@ def run_rs(torch, fec, codec, k, m, B, multi, iters, seed):
     e_d = lost[:, :k].sum(dim=1)
     slots = int(e_d.max().item())
     # multi-erasure configs: m output rows per block, as the rebuild traffic twin writes
-    out = torch.zeros((B, m if multi else max(slots, 1), S), dtype=torch.uint8, device="cuda")
+    out = bench.padded(torch, (B, m if multi else max(slots, 1), S), "cuda")
     status = torch.zeros((B,), dtype=torch.int32, device="cuda")
 
     # raw C-ABI calls with the arguments precomputed: the shapes whose launches take tens of
@@ -112,18 +130,16 @@ def run_rs(torch, fec, codec, k, m, B, multi, iters, seed):
     # arithmetic, timed after the kernels (they overwrite parity and out): this box's ceiling
     probe = {}
     if (k, m) in ((2, 1), (8, 4), (16, 8), (20, 10)):
-        def enc_twin():
-            codec.probe_encode_traffic_raw(k, m, L, B, dp, k * S, pp, m * S, S)
-        probe["encode_probe_TB/s"] = round(enc_bytes / timed(torch, enc_twin, iters) / 1e9, 3)
-        probe["encode_frac_of_probe"] = round(enc_bytes / t_enc / 1e9 / probe["encode_probe_TB/s"], 4)
+        def enc_twin(wpc=-1, off=0):
+            codec.probe_encode_traffic_raw(k, m, L, B, dp, k * S, pp + off, m * S, S, wpc)
         if multi and (k, m) in ((16, 8), (20, 10)):
-            def dec_twin():
-                codec.probe_rebuild_traffic_raw(k, m, L, B, dp, k * S, pp, m * S, S, mp, op, slots_ * S)
+            def dec_twin(wpc=-1, off=0):
+                codec.probe_rebuild_traffic_raw(k, m, L, B, dp, k * S, pp, m * S, S, mp, op + off, slots_ * S, wpc)
         else:
-            def dec_twin():
-                codec.probe_recover_traffic_raw(k, m, L, B, dp, k * S, pp, m * S, S, mp, op, slots_ * S)
-        probe["decode_probe_TB/s"] = round(dec_bytes / timed(torch, dec_twin, iters) / 1e9, 3)
-        probe["decode_frac_of_probe"] = round(dec_bytes / t_dec / 1e9 / probe["decode_probe_TB/s"], 4)
+            def dec_twin(wpc=-1, off=0):
+                codec.probe_recover_traffic_raw(k, m, L, B, dp, k * S, pp, m * S, S, mp, op + off, slots_ * S, wpc)
+        probe.update(twin_fields(torch, "encode", enc_twin, enc_bytes, t_enc, iters))
+        probe.update(twin_fields(torch, "decode", dec_twin, dec_bytes, t_dec, iters))
     return {"config": "RS(%d,%d)" % (k, n), "blocks": B,
             "erasures": ("U{1..%d} of %d shards" % (multi, n)) if multi else "1 data shard",
             "mean_data_erasures": round(float(e_d.float().mean().item()), 3),
@@ -172,18 +188,18 @@ def run_xor(torch, fec, codec, k, B, iters, seed):
     probe = {}
     if k == 2:
         # the RS(2,3) twins over the interleaved XOR layout: k reads + 1 write per block either way
-        # (the decode twin writes the rebuilt shard to a separate buffer, as many bytes)
-        out = torch.zeros((B, 1, S), dtype=torch.uint8, device="cuda")
+        # (the decode twin writes the rebuilt shard to a separate buffer, as many bytes; the encode
+        # twin writes the parity slots in place, so it is not moved)
+        out = bench.padded(torch, (B, 1, S), "cuda")
 
-        def enc_twin():
-            codec.probe_encode_traffic_raw(k, 1, L, B, shp, n * S, shp + k * S, n * S, S)
+        def enc_twin(wpc=-1, off=0):
+            codec.probe_encode_traffic_raw(k, 1, L, B, shp, n * S, shp + k * S, n * S, S, wpc)
 
-        def dec_twin():
-            codec.probe_recover_traffic_raw(k, 1, L, B, shp, n * S, shp + k * S, n * S, S, mp, out.data_ptr(), S)
-        probe["encode_probe_TB/s"] = round(enc_bytes / timed(torch, enc_twin, iters) / 1e9, 3)
-        probe["encode_frac_of_probe"] = round(enc_bytes / t_enc / 1e9 / probe["encode_probe_TB/s"], 4)
-        probe["decode_probe_TB/s"] = round(dec_bytes / timed(torch, dec_twin, iters) / 1e9, 3)
-        probe["decode_frac_of_probe"] = round(dec_bytes / t_dec / 1e9 / probe["decode_probe_TB/s"], 4)
+        def dec_twin(wpc=-1, off=0):
+            codec.probe_recover_traffic_raw(k, 1, L, B, shp, n * S, shp + k * S, n * S, S, mp, out.data_ptr() + off,
+                                            S, wpc)
+        probe.update(twin_fields(torch, "encode", enc_twin, enc_bytes, t_enc, iters))
+        probe.update(twin_fields(torch, "decode", dec_twin, dec_bytes, t_dec, iters))
     return {"config": "XOR(%d,1)" % k, "blocks": B, "erasures": "1 data shard",
             "encode_ms": round(t_enc, 4), "decode_ms": round(t_dec, 4),
             "encode_TB/s": round(enc_bytes / t_enc / 1e9, 3), "decode_TB/s": round(dec_bytes / t_dec / 1e9, 3),

@@ -7,7 +7,7 @@
 #   tests smoke bench prof pmc configs go counters
 # steps:
 #   tests       pytest -m gpu (the whole GPU suite)
-#   variants    pytest -m gpu -k kernel_variants / plan forms (every kernel variant against the oracle)
+#   variants    pytest -m gpu -k kernel_variants / plan_forms (every shipped kernel path against the oracle)
 #   smoke       __graft_entry__.smoke()
 #   bench       bench.py (the contract line)
 #   prof        rocprofv3 --kernel-trace --stats of bench.py -> kernel_trace_summary.json
@@ -16,9 +16,7 @@
 #   go          tools/go_batch_bench (host-resident Go ABI, copy and ref submit)
 #   burst       tools/go_batch_bench burst (receive-side run-loop stall per burst, p50 / p99)
 #   counters    SQ / TCC / LDS counter passes of the configs furthest from the roofline
-#   counters:KNOB=V,..  the same passes of RS(16,24) / RS(20,30) with tuning knobs set
-#   ab:K:M:MULTI:ONLY   tools/dec_select.py interleaved A/B (ONLY: comma list, '_' for spaces)
-#   enc:K,M:BLOCKS:ONLY tools/enc_select.py interleaved encode A/B (BLOCKS 0: 2^23 / k)
+#   dectwin     tools/dec_twin_probe.py (RS(8,12) decode and its traffic twins at every residency)
 #   torchrun1   bench.py under torchrun with one rank (the RCCL branch on one device)
 #   rehearse2   bench.py --gpus 2 --rehearse-one-gpu (the N-rank code path, gloo, one device)
 #   hostsweep   tools/host_chunk_sweep.py (host-resident pipeline chunk size)
@@ -42,7 +40,7 @@ for s in $STEPS; do
       timeout -k 10 600 $PYT tests --maxfail=3 > "$O/pytest_gpu.log" 2>&1 || { tail -30 "$O/pytest_gpu.log"; exit 1; }
       tail -2 "$O/pytest_gpu.log" ;;
     variants)
-      timeout -k 10 300 $PYT tests/test_gpu_codec.py -x -k "kernel_variants or plan_forms or plan_overlap" > "$O/pytest_variants.log" 2>&1 || { tail -30 "$O/pytest_variants.log"; exit 1; }
+      timeout -k 10 300 $PYT tests/test_gpu_codec.py -x -k "kernel_variants or plan_forms" > "$O/pytest_variants.log" 2>&1 || { tail -30 "$O/pytest_variants.log"; exit 1; }
       tail -1 "$O/pytest_variants.log" ;;
     smoke)
       timeout -k 10 120 python -u -c 'import __graft_entry__ as g; g.smoke()' > "$O/smoke.log" 2>&1
@@ -85,18 +83,9 @@ for s in $STEPS; do
       cat "$O/go_burst.log" ;;
     counters)
       tools/pmc_configs.sh "$TAG/counters" "rs1624,rs2030m,rs23" ;;
-    counters:*)
-      TUNE=${s#counters:}
-      tools/pmc_configs.sh "$TAG/counters_${TUNE//[=,]/_}" "rs1624,rs2030m" --tune "$TUNE" ;;
-    enc:*)
-      IFS=: read -r _ KM BLK ONLY <<< "$s"
-      timeout -k 10 200 python -u tools/enc_select.py "$KM" "$BLK" "${ONLY//_/ }" > "$O/enc_${KM/,/_}_$BLK.log" 2>&1
-      tail -30 "$O/enc_${KM/,/_}_$BLK.log" ;;
-    ab:*)
-      IFS=: read -r _ K M MULTI ONLY <<< "$s"
-      timeout -k 10 200 python -u tools/dec_select.py --k "$K" --m "$M" --blocks 524288 --multi "$MULTI" --rounds 7 \
-        --only "${ONLY//_/ }" > "$O/ab_${K}_${M}_${MULTI}.log" 2>&1
-      tail -3 "$O/ab_${K}_${M}_${MULTI}.log" ;;
+    dectwin)
+      timeout -k 10 400 python -u tools/dec_twin_probe.py > "$O/dec_twin.log" 2>&1
+      grep -v amdgpu.ids "$O/dec_twin.log" | tail -60 ;;
     torchrun1)
       timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
         --master-port 29611 bench.py --gpus 1 --steps 10 --warmup 3 --no-cpu-baseline --host-blocks 0 > "$O/bench_torchrun_n1_rccl.log" 2>&1
@@ -112,7 +101,7 @@ for s in $STEPS; do
       timeout -k 10 400 python -u tools/host_chunk_sweep.py --chunks 0,3072,4096,6144,8192 > "$O/host_chunk_sweep.log" 2>&1
       grep -v amdgpu.ids "$O/host_chunk_sweep.log" | cut -c1-400 ;;
     hostthreads)
-      timeout -k 10 400 python -u tools/host_chunk_sweep.py --threads 8,12,16 --pools 0,1 --reps 3 > "$O/host_thread_sweep.log" 2>&1
+      timeout -k 10 400 python -u tools/host_chunk_sweep.py --threads 8,12,16 --reps 3 > "$O/host_thread_sweep.log" 2>&1
       grep -v amdgpu.ids "$O/host_thread_sweep.log" | tail -1 ;;
     duplex)
       timeout -k 10 120 tools/pcie_duplex_probe > "$O/pcie_duplex_probe.log" 2>&1

@@ -3,7 +3,7 @@
 measured with bench.py's own host_resident() step (RS(8,12) encode + single-erasure reconstruct,
 packed pinned and pageable host buffers).
 
-    python tools/host_chunk_sweep.py [--blocks 131072] [--threads 4,8,12,16 [--pools 0,1] [--reps 3]]
+    python tools/host_chunk_sweep.py [--blocks 131072] [--threads 4,8,12,16 [--reps 3]]
 
 One JSON line per setting: knob host_chunk (blocks per chunk; 0 = the library's default, 128 MiB
 of staged shards) and host_gather (1: sparse parity planes pulled by the device, dense ones by
@@ -23,7 +23,6 @@ def main():
     ap.add_argument("--blocks", type=int, default=1 << 17)
     ap.add_argument("--chunks", default="0,2048,4096,8192,16384,32768")
     ap.add_argument("--threads", default="", help="sweep knob host_threads instead (comma list), interleaved")
-    ap.add_argument("--pools", default="1", help="with --threads: knob host_pool values (comma list)")
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
     import torch
@@ -34,26 +33,24 @@ def main():
     if args.threads:
         res = {}
         for _ in range(args.reps):
-            for pool in [int(x) for x in args.pools.split(",")]:
-                for t in [int(x) for x in args.threads.split(",")]:
-                    old = codec.set_tuning(host_threads=t, host_pool=pool)
-                    r = bench.host_resident(torch, fec, codec, 8, 4, args.blocks, 0x0FEC)
-                    codec.set_tuning(**old)
-                    key = "pool%d threads%d" % (pool, t)
-                    res.setdefault(key, []).append((r["pageable"]["value"], r["pinned"]["value"]))
-                    print(json.dumps({"host_pool": pool, "host_threads": t, "pageable": r["pageable"]["value"],
-                                      "pinned": r["pinned"]["value"]}), flush=True)
+            for t in [int(x) for x in args.threads.split(",")]:
+                old = codec.set_tuning(host_threads=t)
+                r = bench.host_resident(torch, fec, codec, 8, 4, args.blocks, 0x0FEC)
+                codec.set_tuning(**old)
+                key = "threads%d" % t
+                res.setdefault(key, []).append((r["pageable"]["value"], r["pinned"]["value"]))
+                print(json.dumps({"host_threads": t, "pageable": r["pageable"]["value"],
+                                  "pinned": r["pinned"]["value"]}), flush=True)
         print(json.dumps({"median_pageable_GiBps": {t: sorted(v[0] for v in vs)[len(vs) // 2] for t, vs in res.items()},
                           "median_pinned_GiBps": {t: sorted(v[1] for v in vs)[len(vs) // 2] for t, vs in res.items()}}))
         codec.close()
         return
     for chunk in [int(c) for c in args.chunks.split(",")]:
-        for gather in (1, 2) if chunk == 0 else (1,):
-            old = codec.set_tuning(host_chunk=chunk, host_gather=gather)
-            r = bench.host_resident(torch, fec, codec, 8, 4, args.blocks, 0x0FEC)
-            codec.set_tuning(**old)
-            print(json.dumps({"host_chunk": chunk, "host_gather": gather, "link_bound_GiBps": r["link_bound_GiBps"],
-                              "pinned": r["pinned"], "pageable": r["pageable"]}), flush=True)
+        old = codec.set_tuning(host_chunk=chunk)
+        r = bench.host_resident(torch, fec, codec, 8, 4, args.blocks, 0x0FEC)
+        codec.set_tuning(**old)
+        print(json.dumps({"host_chunk": chunk, "link_bound_GiBps": r["link_bound_GiBps"],
+                          "pinned": r["pinned"], "pageable": r["pageable"]}), flush=True)
     codec.close()
 
 
