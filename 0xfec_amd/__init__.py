@@ -63,6 +63,7 @@ lib.fec_ctx_destroy.argtypes = [_vp]
 lib.fec_ctx_destroy.restype = None
 lib.fec_ctx_set_stream.argtypes = [_vp, _vp]
 lib.fec_ctx_reset_stream.argtypes = [_vp]
+lib.fec_ctx_release_staging.argtypes = [_vp]
 lib.fec_ctx_stream.argtypes = [_vp]
 lib.fec_ctx_stream.restype = _vp
 lib.fec_sync.argtypes = [_vp]
@@ -184,6 +185,10 @@ class Codec:
 
     def sync(self):
         return _check(lib.fec_sync(self._h), "fec_sync")
+
+    def release_staging(self):
+        """Free the host-path staging sets (fec_ctx_release_staging); the next host call makes them."""
+        return _check(lib.fec_ctx_release_staging(self._h), "fec_ctx_release_staging")
 
     def lib_sync_rc(self):
         """fec_sync's return code (FEC_ERR_TOO_FEW_SHARDS after a failed block) without raising."""

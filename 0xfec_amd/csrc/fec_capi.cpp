@@ -512,9 +512,17 @@ static int check_device_layout(const void* p, size_t bs, size_t ss, size_t len) 
 // shards and the parity planes its blocks read, and returns only the rebuilt shards. Chunks run
 // through HostPipe's three streams (up / kernels / down), kHostSets at a time.
 
-static size_t host_chunk_blocks(size_t bytes_per_block) {
-    if (fk::g_tune.host_chunk > 0) return (size_t)fk::g_tune.host_chunk;   // tests: many small chunks
-    return std::max<size_t>(1, kStageBytes / std::max<size_t>(1, bytes_per_block));
+// Blocks per chunk of a host-path call of nblocks: at most kStageBytes of staged input (128 MiB:
+// larger chunks gain nothing, r04o), and for a call of fewer than kHostSets such chunks, the call
+// split over the sets, so its three sets together hold about the call rather than three full
+// chunks; never below kMinChunkBlocks (chunks of 3072-4096 RS(8,12) blocks lose 10 % to their
+// per-chunk overhead, 6144 and up do not: host_chunk_sweep_r04o.log).
+constexpr size_t kMinChunkBlocks = 6144;
+static size_t host_chunk_blocks(size_t nblocks, size_t bytes_per_block) {
+    if (fk::g_tune.host_chunk > 0) return std::min(nblocks, (size_t)fk::g_tune.host_chunk);   // tests: many small chunks
+    const size_t full = std::max<size_t>(1, kStageBytes / std::max<size_t>(1, bytes_per_block));
+    const size_t split = std::max(kMinChunkBlocks, (nblocks + kHostSets - 1) / kHostSets);
+    return std::max<size_t>(1, std::min({nblocks, full, split}));
 }
 
 // Copy workers made once per process for parallel_for: a chunk's staging or scatter copy then
@@ -787,7 +795,7 @@ static int host_pipeline(fec_ctx* ctx, size_t nblocks, size_t chunk, Up up, Kern
 static int host_encode(fec_ctx* ctx, Code* code, int k, int m, size_t len, size_t nblocks, const uint8_t* data,
                        size_t dbs, uint8_t* parity, size_t pbs, size_t ss, bool pinned) {
     const size_t ssd = round16(len);
-    const size_t chunk = std::min(nblocks, host_chunk_blocks((size_t)k * ssd));
+    const size_t chunk = host_chunk_blocks(nblocks, (size_t)k * ssd);
     HostPipe& p = ctx->pipe;
     int rc;
     if ((rc = host_pipe_grow(p, chunk * k * ssd, chunk * m * ssd, 1))) return rc;
@@ -858,7 +866,7 @@ static int host_reconstruct_rs(fec_ctx* ctx, Code* code, int k, int m, size_t le
     const size_t n = (size_t)k + m;
     const uint32_t all = fk::low_mask((uint32_t)n), kmask = fk::low_mask((uint32_t)k);
     const size_t maxe = (size_t)std::max(1, std::min(k, m));
-    const size_t chunk = std::min(nblocks, host_chunk_blocks(n * ssd));
+    const size_t chunk = host_chunk_blocks(nblocks, n * ssd);
     HostPipe& p = ctx->pipe;
     int rc;
     if ((rc = host_pipe_grow(p, chunk * n * ssd, chunk * maxe * ssd, chunk))) return rc;
@@ -982,7 +990,7 @@ static int host_reconstruct_xor(fec_ctx* ctx, int k, size_t len, size_t nblocks,
     const size_t ssd = round16(len);
     const size_t n = (size_t)k + 1;
     const uint32_t all = fk::low_mask((uint32_t)n), kmask = fk::low_mask((uint32_t)k);
-    const size_t chunk = std::min(nblocks, host_chunk_blocks(n * ssd));
+    const size_t chunk = host_chunk_blocks(nblocks, n * ssd);
     int rc;
     if ((rc = grow_stage(ctx, chunk * n * ssd))) return rc;
     if ((rc = grow_masks(ctx, chunk))) return rc;
@@ -1145,6 +1153,31 @@ static int switch_stream(fec_ctx* ctx, hipStream_t next) {
     HIP_TRY(hipEventRecord(ctx->handoff, ctx->stream));
     HIP_TRY(hipStreamWaitEvent(next, ctx->handoff, 0));
     ctx->stream = next;
+    return FEC_OK;
+}
+
+int fec_ctx_release_staging(fec_ctx* ctx) {
+    int rc = select_device(ctx);
+    if (rc) return rc;
+    HostPipe& p = ctx->pipe;
+    for (hipStream_t q : {p.up, p.comp, p.down})
+        if (q) HIP_TRY(hipStreamSynchronize(q));
+    if (ctx->stream) HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (HostSet& s : p.set) {
+        for (void* q : {(void*)s.h_in, (void*)s.h_out, (void*)s.h_masks, (void*)s.h_status})
+            if (q) HIP_TRY(hipHostFree(q));
+        for (void* q : {(void*)s.d_in, (void*)s.d_out, (void*)s.d_masks, (void*)s.d_status, (void*)s.d_raw_in,
+                        (void*)s.d_raw_out})
+            if (q) HIP_TRY(hipFree(q));
+        s.h_in = s.h_out = s.d_in = s.d_out = s.d_raw_in = s.d_raw_out = nullptr;
+        s.h_masks = s.d_masks = nullptr;
+        s.h_status = s.d_status = nullptr;
+        s.in_cap = s.out_cap = s.blk_cap = s.raw_in_cap = s.raw_out_cap = 0;
+    }
+    if (ctx->h_stage) HIP_TRY(hipHostFree(ctx->h_stage));
+    if (ctx->d_stage) HIP_TRY(hipFree(ctx->d_stage));
+    ctx->h_stage = ctx->d_stage = nullptr;
+    ctx->stage_cap = 0;
     return FEC_OK;
 }
 

@@ -98,6 +98,12 @@ int fec_ctx_set_stream(fec_ctx *ctx, void *hip_stream);
 /* Go back to the ctx-owned stream. */
 int fec_ctx_reset_stream(fec_ctx *ctx);
 void *fec_ctx_stream(fec_ctx *ctx);
+/* Free the host-path staging (FEC_HOST / FEC_HOST_PINNED: kHostSets = 3 sets of pinned host and
+ * device buffers, each up to one 128 MiB chunk of input plus its outputs, kept by the ctx between
+ * calls so that a stream of calls does not re-register memory) after the ctx's host-path work
+ * has finished. The next host-path call allocates them again. No reference counterpart (the
+ * reference codes in Go memory); INTEGRATION.md lists the per-ctx footprint. */
+int fec_ctx_release_staging(fec_ctx *ctx);
 /* Wait for the ctx stream. Returns FEC_ERR_TOO_FEW_SHARDS if any FEC_DEVICE reconstruct
  * since the last fec_sync met a block with fewer than k present shards, or
  * FEC_ERR_INVALID_ARG if a recover met a block with more erasures than output slots

@@ -599,6 +599,29 @@ def test_rs_host_copy_pool_matches_oracle(codec, oracle, fec, threads, chunk):
         codec.set_tuning(**old)
 
 
+def test_host_staging_release_and_regrow(codec, oracle, fec):
+    """fec_ctx_release_staging frees the host path's staging sets between calls; calls before and
+    after it (a mid-sized call split over the three sets, then a small one) stay exact."""
+    rng = np.random.default_rng(77)
+    k, m, L = 8, 4, 1202
+    for B in (20000, 300, 7000):
+        full = np.zeros((B, k + m, L), dtype=np.uint8)
+        full[:, :k] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+        oracle.rs_encode(k, m, full)
+        data = full[:, :k].copy()
+        par = np.zeros((B, m, L), dtype=np.uint8)
+        codec.rs_encode_split(k, m, data, par, shard_len=L)
+        assert np.array_equal(par, full[:, k:])
+        masks = _random_masks(rng, B, k, m, max_loss=m)
+        dmg = full[:, :k].copy()
+        dmg[~((masks[:, None] >> np.arange(k)[None, :]) & 1).astype(bool)] = 0xA1
+        st = np.full(B, 7, dtype=np.int32)
+        assert codec.rs_reconstruct_split(k, m, dmg, par, masks, status=st, shard_len=L) == fec.FEC_OK
+        assert (st == 0).all() and np.array_equal(dmg, full[:, :k])
+        codec.release_staging()
+        codec.release_staging()   # twice: a no-op
+
+
 def test_rs_host_copy_pool_concurrent_contexts(oracle, fec):
     """Two contexts on two threads in FEC_HOST calls at once: one gets the persistent copy
     workers, the other finds them busy and copies on threads of its own; both results exact."""

@@ -9,7 +9,13 @@ addresses known at launch), scalar (masks by scalar loads), read8 (the block's 8
 store: no holes, no parity region). Each mode as a pure-traffic twin (xor) and with the decode's
 field arithmetic (arith). Rates are algorithmic bytes (9 shards of 1202 B per block) / time.
 
-usage: dec_twin_probe.py [blocks] [rounds]"""
+With --multi: the RS(16,24) multi-erasure decode instead (2^19 blocks), every block with one
+erasure pattern (3 data + 2 parity shards lost: 16 reads + 3 stores), against rebuild twins whose
+present mask arrives by a per-lane vector load, by scalar loads, as a kernel argument (addresses
+known at launch) or through the rebuild's plan-record staging (a record per block, vector-loaded
+into LDS); and the library's decode of the config #4 distribution (e ~ U{1..8} of 24) beside it.
+
+usage: dec_twin_probe.py [blocks] [rounds] [--multi] [--rebuild (recompile the probe)] [--build-only]"""
 import ctypes
 import importlib
 import json
@@ -28,6 +34,8 @@ def main():
                                os.path.join(HERE, "dec_twin_probe.hip")])
     if "--build-only" in sys.argv:
         return
+    if "--multi" in sys.argv:
+        return rebuild_main()
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     B = int(args[0]) if args else 1 << 20
     rounds = int(args[1]) if len(args) > 1 else 7
@@ -94,6 +102,83 @@ def main():
         print("round %d done" % r, flush=True)
     codec.set_tuning(**base)
     med = {n: round(sorted(v)[len(v) // 2], 3) for n, v in res.items()}
+    print(json.dumps({"blocks": B, "rounds": rounds, "decode_ok": ok, "TBps_median": med}, indent=1), flush=True)
+
+
+def rebuild_main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    B = int(args[0]) if args else 1 << 19
+    rounds = int(args[1]) if len(args) > 1 else 7
+    import torch
+    fec = importlib.import_module("0xfec_amd")
+    lib = ctypes.CDLL(SO)
+    vp, sz, i, u = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint
+    lib.rebuild_probe.argtypes = [i, i, vp, vp, vp, vp, vp, u, sz, sz, sz, sz, u, u, vp]
+    k, m, L, S, n = 16, 8, 1202, 1216, 24
+    codec = fec.Codec(0).use_torch_stream()
+    codec.prepare(k, m)
+    st = torch.cuda.current_stream().cuda_stream
+    data = torch.empty((B, k, S), dtype=torch.uint8, device="cuda")
+    codec.synth_data(0x0FEC, 0, B, k, 1200, data.data_ptr(), k * S, S)
+    par = torch.zeros((B, m, S), dtype=torch.uint8, device="cuda")
+    codec.rs_encode_raw(k, m, L, B, data.data_ptr(), k * S, par.data_ptr(), m * S, S, fec.FEC_DEVICE)
+    lost = (1, 7, 12, 17, 20)                  # data 1, 7, 12; parity 1, 4
+    cmask = ((1 << n) - 1) & ~sum(1 << x for x in lost)
+    masks = torch.full((B,), cmask, dtype=torch.int32, device="cuda")
+    recs = torch.zeros((B, 40), dtype=torch.int32, device="cuda")
+    recs[:, 0] = cmask
+    out = torch.zeros((B, m, S), dtype=torch.uint8, device="cuda")
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x1624)
+    e = torch.randint(1, m + 1, (B,), device="cuda", generator=g)
+    rank = torch.rand((B, n), device="cuda", generator=g).argsort(dim=1).argsort(dim=1)
+    lostu = rank < e[:, None]
+    w = torch.bitwise_left_shift(torch.ones(n, dtype=torch.int64, device="cuda"), torch.arange(n, device="cuda"))
+    masks_u = ((~lostu).to(torch.int64) * w).sum(dim=1).to(torch.int32)
+    bytes_c = B * (k + 3) * L
+    bytes_u = int(((k + lostu[:, :k].sum(dim=1)) * (lostu[:, :k].sum(dim=1) > 0)).sum().item()) * L
+
+    def lib_decode(mk):
+        def fn():
+            rc = codec.rs_recover_raw(k, m, L, B, data.data_ptr(), k * S, par.data_ptr(), m * S, S, mk.data_ptr(),
+                                      out.data_ptr(), m * S, m, None)
+            assert rc == 0, rc
+        return fn
+
+    def probe(mode, wpc):
+        def fn():
+            rc = lib.rebuild_probe(mode, wpc, data.data_ptr(), par.data_ptr(), out.data_ptr(), masks.data_ptr(),
+                                   recs.data_ptr(), cmask, k * S, m * S, S, m * S, L, B, st)
+            assert rc == 0, rc
+        return fn
+
+    def timed(fn, iters=3):
+        fn()
+        s, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e_.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e_) / iters / 1e3
+
+    lib_decode(masks)()
+    torch.cuda.synchronize()
+    ok = all(bool(torch.equal(out[:, r, :L], data[:, x, :L])) for r, x in enumerate((1, 7, 12)))
+    base = codec.set_tuning(dec_wpc=0)
+    res = {}
+    print("rebuild probe start B=%d rounds=%d decode_ok=%s" % (B, rounds, ok), flush=True)
+    names = {0: "vecmask", 1: "scalarmask", 2: "constmask", 3: "record"}
+    for r in range(rounds):
+        for wp in (2, 3, 4, 5, 0):
+            codec.set_tuning(dec_wpc=wp)
+            res.setdefault("decode 1pattern wpc%d" % wp, []).append(bytes_c / timed(lib_decode(masks)) / 1e12)
+            res.setdefault("decode U1..8 wpc%d" % wp, []).append(bytes_u / timed(lib_decode(masks_u)) / 1e12)
+            for md, nm in names.items():
+                res.setdefault("%s wpc%d" % (nm, wp), []).append(bytes_c / timed(probe(md, wp)) / 1e12)
+        print("round %d done" % r, flush=True)
+    codec.set_tuning(**base)
+    med = {nm: round(sorted(v)[len(v) // 2], 3) for nm, v in res.items()}
     print(json.dumps({"blocks": B, "rounds": rounds, "decode_ok": ok, "TBps_median": med}, indent=1), flush=True)
 
 
