@@ -57,9 +57,9 @@ struct CoefWords {
 // read from the code's coefficient table in device memory (a.single_coef, through the constant
 // address space: scalar loads), for codes whose rows do not fit the argument (RS(20,30): 1000
 // dwords).
-template <int K, int POL, int TAB>
+template <int K, int TAB>
 __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a, CoefWords cwords) {
-    constexpr bool NTL = POL & 1, NTS = (POL & 2) != 0;
+    constexpr bool NTL = true, NTS = true;   // non-temporal loads and stores (see launch_rs_recover_direct)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     {
         const uint32_t vb = blockIdx.x;
@@ -342,7 +342,7 @@ bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t stride,
     return 4 * hard_wave_bytes(m, k, maxe, stride) <= g_max_lds;
 }
 
-template <int K, int POL, int TAB>
+template <int K, int TAB>
 static hipError_t direct_launch(const ReconArgs& a0, const CoefWords& cw, hipStream_t s) {
     const uint64_t total = (uint64_t)a0.nblocks * a0.cps;
     const int flat = (int)((total + kThreads - 1) / kThreads);
@@ -353,7 +353,7 @@ static hipError_t direct_launch(const ReconArgs& a0, const CoefWords& cw, hipStr
     // small codes uncapped
     const int wpc = g_tune.dir_wpc >= 0 ? (int)g_tune.dir_wpc : (a0.k >= 8 ? 3 : 0);
     const size_t lds = occupancy_lds(wpc, 4 * direct_wave_bytes(a0.k));
-    hipLaunchKernelGGL((rs_recover_direct_kernel<K, POL, TAB>), dim3(flat), dim3(kThreads), lds, s, a0, cw);
+    hipLaunchKernelGGL((rs_recover_direct_kernel<K, TAB>), dim3(flat), dim3(kThreads), lds, s, a0, cw);
     return hipGetLastError();
 }
 
@@ -368,26 +368,26 @@ static hipError_t hard_launch(const ReconArgs& a, int ncu, hipStream_t s) {
 }
 
 hipError_t launch_rs_recover_direct(const ReconArgs& a, int ncu, hipStream_t s) {
-    // the reference's benchmark shapes at compile time, the rest by runtime k. Cache policy by
-    // shape: non-temporal loads and stores (POL 3); for k <= 4 plain loads and non-temporal stores
-    // (POL 2: RS(2,3) +8 %, r02; at k = 8 plain loads cost 4 %)
+    // the reference's benchmark shapes at compile time, the rest by runtime k. Non-temporal loads
+    // and stores for every code: plain loads measured +8 % for RS(2,3) (r02), but only because its
+    // 65 536-block batch (239 MB) fits the 256 MiB Infinity Cache and back-to-back launches re-read
+    // it from there (the encode's plain-load A/B, r04, showed the same +11 %); shards streamed in
+    // once do not come back, so the decode streams as the encode does (round 5)
     hipError_t e;
     CoefWords cw{};
     const size_t kw = (a.k + 3) / 4, words = (size_t)a.k * a.m * kw;
     const bool by_arg = g_tune.dec_direct != 2 && a.single_coef_host && words <= kCoefWords;
     if (by_arg) memcpy(cw.w, a.single_coef_host, words * 4);
     if (a.k == 20)   // RS(20,30), RS(16,24): rows from the device coefficient table
-        e = direct_launch<20, 3, 2>(a, cw, s);
+        e = direct_launch<20, 2>(a, cw, s);
     else if (a.k == 16)
-        e = direct_launch<16, 3, 2>(a, cw, s);
+        e = direct_launch<16, 2>(a, cw, s);
     else if (a.k == 8)
-        e = by_arg ? direct_launch<8, 3, 1>(a, cw, s) : direct_launch<8, 3, 0>(a, cw, s);
+        e = by_arg ? direct_launch<8, 1>(a, cw, s) : direct_launch<8, 0>(a, cw, s);
     else if (a.k == 2)
-        e = by_arg ? direct_launch<2, 2, 1>(a, cw, s) : direct_launch<2, 2, 0>(a, cw, s);
-    else if (a.k <= 4)
-        e = by_arg ? direct_launch<0, 2, 1>(a, cw, s) : direct_launch<0, 2, 0>(a, cw, s);
+        e = by_arg ? direct_launch<2, 1>(a, cw, s) : direct_launch<2, 0>(a, cw, s);
     else
-        e = by_arg ? direct_launch<0, 3, 1>(a, cw, s) : direct_launch<0, 3, 0>(a, cw, s);
+        e = by_arg ? direct_launch<0, 1>(a, cw, s) : direct_launch<0, 0>(a, cw, s);
     // m = 1: two erasures always leave too few shards; one output slot: a block with two or more
     // erasures is an error the direct kernel reports itself (nothing goes to the worklist)
     if (e != hipSuccess || a.m < 2 || a.max_out == 1) return e;
