@@ -50,6 +50,46 @@ struct CoefWords {
     uint32_t w[kCoefWords];
 };
 
+// Statuses (recover: e rebuilt; in place: 0; failures as rs_plan_kernel reports them) and failure
+// flags of blocks [64 w, 64 w + 64), w = the calling wave's launch index: one coalesced mask load
+// and one coalesced status store per 64 blocks. (Stored by the waves of each block, the 4-byte
+// statuses of neighbouring blocks were scattered partial-line stores from different waves: RS(2,3)
+// 45 -> 57 us with a status array.)
+__device__ __forceinline__ void direct_status_pass(const ReconArgs& a, uint32_t k, uint32_t w, uint32_t lane) {
+    if (w * 64u >= a.nblocks) return;   // wave-uniform
+    const uint32_t all = low_mask(k + a.m), kmask = low_mask(k);
+    const uint32_t b = w * 64u + lane;
+    uint32_t bad = 0;
+    if (b < a.nblocks) {
+        const uint32_t mask = a.masks[b] & all;
+        const uint32_t e = k - __popc(mask & kmask);
+        int32_t st = a.max_out ? (int32_t)e : 0;
+        if (e != 0 && (uint32_t)__popc(mask) < k) {
+            st = -4;   // FEC_ERR_TOO_FEW_SHARDS
+            bad = 1;
+        } else if (a.max_out && e > a.max_out) {
+            st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
+            bad = 2;
+        }
+        if (a.status) a.status[b] = st;
+    }
+    const bool f1 = __ballot(bad == 1) != 0, f2 = __ballot(bad == 2) != 0;
+    if (lane == 0 && (f1 || f2)) atomicOr(a.err, (f1 ? 1 : 0) | (f2 ? 2 : 0));
+}
+
+// The wave's <= 3 block masks (blocks bfirst, +1, +2, clamped to the batch) by scalar loads.
+struct WaveMasks {
+    uint32_t m0, m1, m2;
+    __device__ __forceinline__ uint32_t of(uint32_t g) const { return g == 0 ? m0 : g == 1 ? m1 : m2; }
+};
+__device__ __forceinline__ WaveMasks wave_masks(const uint32_t* masks, uint32_t bfirst, uint32_t nblocks) {
+    typedef __attribute__((address_space(4))) const uint32_t ConstU32;
+    ConstU32* cm = (ConstU32*)masks;
+    const uint32_t bf = (uint32_t)__builtin_amdgcn_readfirstlane((int)bfirst), last = nblocks - 1;
+    return {cm[bf], cm[(uint32_t)__builtin_amdgcn_readfirstlane((int)min(bf + 1, last))],
+            cm[(uint32_t)__builtin_amdgcn_readfirstlane((int)min(bf + 2, last))]};
+}
+
 // K: compile-time data shard count (0: runtime a.k). TAB: how a wave gets the PermTabs of its
 // blocks' rows: 0 copies them from the code's PermTab table (one vector load per wave, L1/L2
 // hits); 1 reads the rows' coefficient bytes from the kernel arguments (scalar loads, off the
@@ -68,33 +108,7 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
         uint8_t* slice = smem + (size_t)wave * direct_wave_bytes(k);
         const uint32_t total = a.nblocks * a.cps;
         const uint32_t all = low_mask(k + m), kmask = low_mask(k);
-        // Statuses (recover: e rebuilt; in place: 0; failures as rs_plan_kernel reports them) and
-        // failure flags of blocks [64 w, 64 w + 64), w = this wave's launch index: one coalesced mask
-        // load and one coalesced status store per 64 blocks. (Stored by the waves of each block, the
-        // 4-byte statuses of neighbouring blocks were scattered partial-line stores from different
-        // waves: RS(2,3) 45 -> 57 us with a status array.)
-        {
-            const uint32_t w = vb * (kThreads / 64) + wave;
-            if (w * 64u < a.nblocks) {   // wave-uniform
-                const uint32_t b = w * 64u + lane;
-                uint32_t bad = 0;
-                if (b < a.nblocks) {
-                    const uint32_t mask = a.masks[b] & all;
-                    const uint32_t e = k - __popc(mask & kmask);
-                    int32_t st = a.max_out ? (int32_t)e : 0;
-                    if (e != 0 && (uint32_t)__popc(mask) < k) {
-                        st = -4;   // FEC_ERR_TOO_FEW_SHARDS
-                        bad = 1;
-                    } else if (a.max_out && e > a.max_out) {
-                        st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
-                        bad = 2;
-                    }
-                    if (a.status) a.status[b] = st;
-                }
-                const bool f1 = __ballot(bad == 1) != 0, f2 = __ballot(bad == 2) != 0;
-                if (lane == 0 && (f1 || f2)) atomicOr(a.err, (f1 ? 1 : 0) | (f2 ? 2 : 0));
-            }
-        }
+        direct_status_pass(a, k, vb * (kThreads / 64) + wave, lane);
         const uint32_t i0 = xcd_order() * kThreads + (wave << 6);
         if (i0 >= total) return;
         const uint32_t bfirst = fdiv(i0, a.div_cps);
@@ -105,16 +119,8 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
         // shard loads (decode twin at 4 workgroups/CU: 5.73 TB/s with a vector mask load, 5.84
         // with scalar ones, 5.85 with no mask at all; with the field arithmetic 5.70 / 5.83 /
         // 5.87; profiles/r05/dec_twin_r05b.log)
-        uint32_t m0, m1, m2;
-        {
-            typedef __attribute__((address_space(4))) const uint32_t ConstU32;
-            ConstU32* cm = (ConstU32*)a.masks;
-            const uint32_t bf = (uint32_t)__builtin_amdgcn_readfirstlane((int)bfirst), last = a.nblocks - 1;
-            m0 = cm[bf];
-            m1 = cm[(uint32_t)__builtin_amdgcn_readfirstlane((int)min(bf + 1, last))];
-            m2 = cm[(uint32_t)__builtin_amdgcn_readfirstlane((int)min(bf + 2, last))];
-        }
-        auto mask_of = [&](uint32_t g) { return g == 0 ? m0 : g == 1 ? m1 : m2; };   // g < nb
+        const WaveMasks wm = wave_masks(a.masks, bfirst, a.nblocks);
+        auto mask_of = [&](uint32_t g) { return wm.of(g); };   // g < nb
 
         // A block with two or more erasures (and enough shards) sends the whole wave to the
         // worklist of rs_recover_hard_kernel.
@@ -326,6 +332,55 @@ __global__ __launch_bounds__(kThreads) void rs_recover_hard_kernel(ReconArgs a) 
     }
 }
 
+// RS(2,3) (k = 2, m = 1): a block is rebuilt from its other data shard and the parity with the
+// two coefficients of its erased shard's row, x_E0 = c[E0][0] * x_other ^ c[E0][1] * p. Both rows'
+// PermTabs (4 x 32 bytes) arrive as a kernel argument, so a lane picks its row's words from scalar
+// registers with v_cndmask: no LDS, no wave barrier and no per-wave table expansion between the
+// two shard loads and the store (the general kernel's <2, 1> form expands 2 rows per block on the
+// lanes and synchronises the wave before the products).
+struct K2Rows {
+    gf::PermTab t[2][2];   // [E0][input: 0 the other data shard, 1 the parity]
+};
+
+__global__ __launch_bounds__(kThreads) void rs_recover_k2m1_kernel(ReconArgs a, K2Rows rows) {
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t total = a.nblocks * a.cps;
+    direct_status_pass(a, 2, blockIdx.x * (kThreads / 64) + wave, lane);
+    const uint32_t i0 = xcd_order() * kThreads + (wave << 6);
+    if (i0 >= total) return;
+    const uint32_t bfirst = fdiv(i0, a.div_cps);
+    const WaveMasks wm = wave_masks(a.masks, bfirst, a.nblocks);
+    const uint32_t item = i0 + lane;
+    if (item >= total) return;
+    const uint32_t blk = fdiv(item, a.div_cps), c = item - blk * a.cps;
+    const uint32_t mask = wm.of(blk - bfirst) & 7u;
+    // one data shard lost and the parity present (6: x0 lost, 5: x1 lost); any other mask has
+    // nothing to rebuild or too few shards (the status pass reports those)
+    if (mask != 5u && mask != 6u) return;
+    const bool e1 = mask == 5u;
+    const uint8_t* dblk = a.data + (uint64_t)blk * a.dbs + (uint64_t)c * kChunk;
+    const uint4 x = ld16<true>(dblk + (e1 ? 0 : a.ss));
+    const uint4 p = ld16<true>(a.parity + (uint64_t)blk * a.pbs + (uint64_t)c * kChunk);
+    const gf::PermTab &ta0 = rows.t[0][0], &ta1 = rows.t[1][0], &tb0 = rows.t[0][1], &tb1 = rows.t[1][1];
+    const uint4 la = make_uint4(e1 ? ta1.t0lo : ta0.t0lo, e1 ? ta1.t0hi : ta0.t0hi, e1 ? ta1.t1lo : ta0.t1lo,
+                                e1 ? ta1.t1hi : ta0.t1hi);
+    const uint4 lb = make_uint4(e1 ? tb1.t0lo : tb0.t0lo, e1 ? tb1.t0hi : tb0.t0hi, e1 ? tb1.t1lo : tb0.t1lo,
+                                e1 ? tb1.t1hi : tb0.t1hi);
+    const uint32_t a2 = e1 ? ta1.t2 : ta0.t2, b2 = e1 ? tb1.t2 : tb0.t2;
+    Idx ia[4], ib[4];
+    split4(ia, x);
+    split4(ib, p);
+    uint32_t acc[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const Prod3 u = gprod(ia[d], la, a2), v = gprod(ib[d], lb, b2);
+        acc[d] = xor3(xor3(u.p0, u.p1, u.p2), v.p0, v.p1) ^ v.p2;
+    }
+    uint8_t* dst = a.out ? a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk
+                         : const_cast<uint8_t*>(dblk) + (e1 ? a.ss : 0);
+    store_chunk<true>(dst, as_uint4(acc), a.len - c * kChunk);
+}
+
 size_t direct_table_words(uint32_t k, uint32_t m) { return (size_t)k * m * k * 8; }
 
 bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t stride, bool single_slot) {
@@ -384,7 +439,17 @@ hipError_t launch_rs_recover_direct(const ReconArgs& a, int ncu, hipStream_t s) 
         e = direct_launch<16, 2>(a, cw, s);
     else if (a.k == 8)
         e = by_arg ? direct_launch<8, 1>(a, cw, s) : direct_launch<8, 0>(a, cw, s);
-    else if (a.k == 2)
+    else if (a.k == 2 && a.m == 1 && by_arg) {
+        K2Rows rows;
+        for (int e0 = 0; e0 < 2; ++e0)
+            for (int j = 0; j < 2; ++j) rows.t[e0][j] = gf::make_permtab((uint8_t)(cw.w[e0] >> (8 * j)));
+        const uint64_t total = (uint64_t)a.nblocks * a.cps;
+        const int flat = (int)((total + kThreads - 1) / kThreads);
+        if (flat == 0) return hipSuccess;
+        const int wpc = g_tune.dir_wpc >= 0 ? (int)g_tune.dir_wpc : 0;
+        hipLaunchKernelGGL(rs_recover_k2m1_kernel, dim3(flat), dim3(kThreads), occupancy_lds(wpc, 0), s, a, rows);
+        e = hipGetLastError();
+    } else if (a.k == 2)
         e = by_arg ? direct_launch<2, 1>(a, cw, s) : direct_launch<2, 0>(a, cw, s);
     else
         e = by_arg ? direct_launch<0, 1>(a, cw, s) : direct_launch<0, 0>(a, cw, s);
