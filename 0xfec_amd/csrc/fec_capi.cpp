@@ -486,6 +486,7 @@ static int xor_reconstruct_device(fec_ctx* ctx, int k, size_t len, size_t nblock
         a.len = (uint32_t)len;
         a.cps = cps;
         a.total = (uint32_t)(nb * cps);
+        a.nblocks = (uint32_t)nb;
         a.div_cps = fk::make_fastdiv(cps);
         HIP_TRY(fk::launch_xor_reconstruct(a, flat_grid(a.total), ctx->stream));
     }

@@ -57,11 +57,11 @@ __global__ __launch_bounds__(kPlanThreads) void rs_plan_kernel(PlanArgs a) {
         } else if ((uint32_t)__popc(mask) < k) {
             P[lay.nout_off] = 0;
             st = -4;  // FEC_ERR_TOO_FEW_SHARDS
-            atomicOr(a.err, 1);
+            wave_flag(a.err, 1);
         } else if (a.max_out && e > a.max_out) {
             P[lay.nout_off] = 0;
             st = -1;  // FEC_ERR_INVALID_ARG: more erasures than output slots
-            atomicOr(a.err, 2);
+            wave_flag(a.err, 2);
         } else if (e == 1) {
             // one erasure: x_E = inv(A[R0][E0]) * (p_R0 ^ sum_j A[R0][j] x_j)
             const uint32_t E0 = __ffs(~mask & kmask) - 1;

@@ -139,6 +139,31 @@ __device__ __forceinline__ void split4(Idx (&ix)[4], const uint4& x) {
     ix[3] = split(x.w);
 }
 
+// err |= bit from the lanes that reach this point together, as one atomic per wave: the library
+// is built without the compiler's atomic combining (_build.py), and per-lane atomics on one
+// address serialise at L2 (XOR(2,1) with U{1..2} losses, half the blocks failing: 5.97 ms with an
+// atomic per failing block, 0.48 ms with one per wave; profiles/r05/xor_ab_r05g.log).
+__device__ __forceinline__ void wave_flag(int* err, int bit) {
+    const uint64_t act = __ballot(1);
+    if (__lane_id() == (uint32_t)__ffsll((unsigned long long)act) - 1) atomicOr(err, bit);
+}
+
+// The wave's <= 3 block masks (blocks bfirst, +1, +2, clamped to the batch; a wave of 64 items
+// spans at most 3 blocks when cps >= 32) by scalar loads: wave-uniform addresses through the
+// constant cache, which the scalar unit turns into shard addresses while the vector memory path is
+// free (a vector load of the masks puts a dependent vector round trip in front of the shard loads).
+struct WaveMasks {
+    uint32_t m0, m1, m2;
+    __device__ __forceinline__ uint32_t of(uint32_t g) const { return g == 0 ? m0 : g == 1 ? m1 : m2; }
+};
+__device__ __forceinline__ WaveMasks wave_masks(const uint32_t* masks, uint32_t bfirst, uint32_t nblocks) {
+    typedef __attribute__((address_space(4))) const uint32_t ConstU32;
+    ConstU32* cm = (ConstU32*)masks;
+    const uint32_t bf = (uint32_t)__builtin_amdgcn_readfirstlane((int)bfirst), last = nblocks - 1;
+    return {cm[bf], cm[(uint32_t)__builtin_amdgcn_readfirstlane((int)min(bf + 1, last))],
+            cm[(uint32_t)__builtin_amdgcn_readfirstlane((int)min(bf + 2, last))]};
+}
+
 __device__ __forceinline__ uint4 as_uint4(const uint32_t (&v)[4]) { return make_uint4(v[0], v[1], v[2], v[3]); }
 
 }  // namespace fk

@@ -111,6 +111,7 @@ struct XorArgs {
     int32_t* status;           // reconstruct only, optional
     int* err;
     uint32_t k, len, cps, total;
+    uint32_t nblocks;          // reconstruct: blocks in this launch (total / cps)
     FastDiv div_cps;
 };
 

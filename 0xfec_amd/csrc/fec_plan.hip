@@ -166,10 +166,10 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
         if (e != 0) {
             if ((uint32_t)__popc(mask) < k) {
                 st = -4;   // FEC_ERR_TOO_FEW_SHARDS
-                if (gl == 0) atomicOr(a.err, 1);
+                if (gl == 0) wave_flag(a.err, 1);
             } else if (a.max_out && e > a.max_out) {
                 st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
-                if (gl == 0) atomicOr(a.err, 2);
+                if (gl == 0) wave_flag(a.err, 2);
             } else {
                 nout = e;
             }
@@ -332,10 +332,10 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_code_kernel(PlanArgs
         if (e != 0) {
             if ((uint32_t)__popc(mask) < K) {
                 st = -4;   // FEC_ERR_TOO_FEW_SHARDS
-                if (gl == 0) atomicOr(a.err, 1);
+                if (gl == 0) wave_flag(a.err, 1);
             } else if (a.max_out && e > a.max_out) {
                 st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
-                if (gl == 0) atomicOr(a.err, 2);
+                if (gl == 0) wave_flag(a.err, 2);
             } else {
                 nout = e;
             }

@@ -77,19 +77,6 @@ __device__ __forceinline__ void direct_status_pass(const ReconArgs& a, uint32_t 
     if (lane == 0 && (f1 || f2)) atomicOr(a.err, (f1 ? 1 : 0) | (f2 ? 2 : 0));
 }
 
-// The wave's <= 3 block masks (blocks bfirst, +1, +2, clamped to the batch) by scalar loads.
-struct WaveMasks {
-    uint32_t m0, m1, m2;
-    __device__ __forceinline__ uint32_t of(uint32_t g) const { return g == 0 ? m0 : g == 1 ? m1 : m2; }
-};
-__device__ __forceinline__ WaveMasks wave_masks(const uint32_t* masks, uint32_t bfirst, uint32_t nblocks) {
-    typedef __attribute__((address_space(4))) const uint32_t ConstU32;
-    ConstU32* cm = (ConstU32*)masks;
-    const uint32_t bf = (uint32_t)__builtin_amdgcn_readfirstlane((int)bfirst), last = nblocks - 1;
-    return {cm[bf], cm[(uint32_t)__builtin_amdgcn_readfirstlane((int)min(bf + 1, last))],
-            cm[(uint32_t)__builtin_amdgcn_readfirstlane((int)min(bf + 2, last))]};
-}
-
 // K: compile-time data shard count (0: runtime a.k). TAB: how a wave gets the PermTabs of its
 // blocks' rows: 0 copies them from the code's PermTab table (one vector load per wave, L1/L2
 // hits); 1 reads the rows' coefficient bytes from the kernel arguments (scalar loads, off the

@@ -46,35 +46,52 @@ __global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
     constexpr bool NTL = true, NTS = true;
     const uint32_t k = a.k, n = k + 1;
     const uint32_t all = low_mask(n);
-    const uint32_t item = xcd_order() * kThreads + threadIdx.x;
-    if (item < a.total) {
-        const uint32_t b = fdiv(item, a.div_cps);
-        const uint32_t c = item - b * a.cps;
-        const uint32_t miss = ~a.masks[b] & all;
-        const uint32_t nmiss = __popc(miss);
-        const uint32_t mi = miss ? (uint32_t)__ffs(miss) - 1 : 0;
-        const bool work = nmiss == 1 && mi < k;
-        const bool fail = nmiss > 1 && (miss & low_mask(k));
-        if (c == 0) {
-            if (a.status) a.status[b] = fail ? -4 : 0;
-            if (fail) atomicOr(a.err, 1);
-        }
-        if (!work) return;
-        uint8_t* blk = a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk;
-        const uint8_t* par = a.parity + (uint64_t)b * a.par_bs + (uint64_t)c * kChunk;
-        uint4 acc = make_uint4(0, 0, 0, 0);
-        for (uint32_t j0 = 0; j0 < k; j0 += KG) {
-            uint4 x[KG];
-#pragma unroll
-            for (int jj = 0; jj < KG; ++jj) {
-                const uint32_t j = min(j0 + jj, k - 1);
-                const uint32_t s = j + (j >= mi);     // the k shards other than the missing one
-                x[jj] = ld16<NTL>(s < k ? blk + (uint64_t)s * a.ss : par);
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // Statuses and failure flags of blocks [64 w, 64 w + 64), w = this wave's launch index: one
+    // coalesced mask load and one coalesced status store per 64 blocks (as the direct RS decode)
+    {
+        const uint32_t w = blockIdx.x * (kThreads / 64) + wave;
+        if (w * 64u < a.nblocks) {   // wave-uniform
+            const uint32_t b = w * 64u + lane;
+            bool fail = false;
+            if (b < a.nblocks) {
+                const uint32_t miss = ~a.masks[b] & all;
+                fail = __popc(miss) > 1 && (miss & low_mask(k));
+                if (a.status) a.status[b] = fail ? -4 : 0;
             }
-            xor_fold<KG>(acc, x, k - j0);
+            if (__ballot(fail) != 0 && lane == 0) atomicOr(a.err, 1);
         }
-        store_chunk<NTS>(blk + (uint64_t)mi * a.ss, acc, a.len - c * kChunk);
     }
+    const uint32_t i0 = xcd_order() * kThreads + (wave << 6);
+    if (i0 >= a.total) return;
+    const uint32_t item = i0 + lane;
+    const uint32_t b = fdiv(min(item, a.total - 1u), a.div_cps);
+    uint32_t mk;
+    if (a.cps >= 32) {   // the wave's <= 3 masks by scalar loads, off the vector memory path
+        const uint32_t bfirst = fdiv(i0, a.div_cps);
+        mk = wave_masks(a.masks, bfirst, a.nblocks).of(b - bfirst);
+    } else {
+        mk = a.masks[b];
+    }
+    if (item >= a.total) return;
+    const uint32_t c = item - b * a.cps;
+    const uint32_t miss = ~mk & all;
+    const uint32_t mi = miss ? (uint32_t)__ffs(miss) - 1 : 0;
+    if (__popc(miss) != 1 || mi >= k) return;   // nothing to rebuild, or a failure reported above
+    uint8_t* blk = a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk;
+    const uint8_t* par = a.parity + (uint64_t)b * a.par_bs + (uint64_t)c * kChunk;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (uint32_t j0 = 0; j0 < k; j0 += KG) {
+        uint4 x[KG];
+#pragma unroll
+        for (int jj = 0; jj < KG; ++jj) {
+            const uint32_t j = min(j0 + jj, k - 1);
+            const uint32_t s = j + (j >= mi);     // the k shards other than the missing one
+            x[jj] = ld16<NTL>(s < k ? blk + (uint64_t)s * a.ss : par);
+        }
+        xor_fold<KG>(acc, x, k - j0);
+    }
+    store_chunk<NTS>(blk + (uint64_t)mi * a.ss, acc, a.len - c * kChunk);
 }
 
 template <int KG>
