@@ -19,8 +19,8 @@ SOURCES = ["fec_encode.hip", "fec_encode23.hip", "fec_decode.hip", "fec_rebuild.
 HEADERS = ["fec_kernels.hpp", "fec_device.hpp", "fec_recon.hpp", "gf256.h", "rs_matrix.hpp", "fec_bitslice.inc"]
 PUBLIC = ["fec_hip.h", "fec_scheme.h", "fec_batch.h", "fec_batch.hpp", "fec_scheme.hpp", "fec_wire.h", "fec_go.h", "fec_synth.h", "fec_probe.h"]
 
-# The atomic optimizer would wrap every single-lane atomic (the direct decode's worklist append, the
-# sticky error words) in wave-aggregation code it never needs: each is issued by one lane already.
+# The atomic optimizer would wrap every single-lane atomic (the sticky error words: one lane per
+# wave sets them, fec_device.hpp wave_flag) in wave-aggregation code it never needs.
 CFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall",
           "-mllvm", "-amdgpu-atomic-optimizer-strategy=None", "-I", INCLUDE]
 

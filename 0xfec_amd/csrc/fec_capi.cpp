@@ -77,18 +77,15 @@ constexpr uint64_t kMaxItems = uint64_t(1) << 31;
 
 }  // namespace
 
-// Device scratch of the kernels enqueued on one stream: decode plan records and the direct decode's
-// multi-erasure worklist. Each stream the ctx launches on
-// (its own / the caller's, and one per host-path staging set) has its own, so launches that
-// overlap on different streams never share one (nor free one the other stream still reads).
+// Device scratch of the kernels enqueued on one stream: decode plan records. Each stream the ctx
+// launches on (its own / the caller's, and one per host-path staging set) has its own, so
+// launches that overlap on different streams never share one (nor free one the other stream
+// still reads).
 struct Work {
     uint8_t* d_plans = nullptr;
     size_t plans_cap = 0;
-    uint32_t* d_hard = nullptr;   // fk::kHardList + waves words; count and done rewound by the kernel
-    size_t hard_cap = 0;
     void release() {
-        for (void* q : {(void*)d_plans, (void*)d_hard})
-            if (q) (void)hipFree(q);
+        if (d_plans) (void)hipFree(d_plans);
         *this = Work{};
     }
 };
@@ -140,7 +137,6 @@ struct fec_ctx {
     uint32_t* d_masks = nullptr;
     int32_t* d_status = nullptr;
     size_t masks_cap = 0;
-    int ncu = 256;           // compute units of the device
     HostPipe pipe;           // host-resident path (FEC_HOST / FEC_HOST_PINNED)
     hipEvent_t handoff = nullptr;   // orders a newly set stream after the previous one
 };
@@ -266,23 +262,6 @@ static int grow_plans(fec_ctx* ctx, size_t bytes) {
     return FEC_OK;
 }
 
-static int grow_hard(fec_ctx* ctx, size_t waves) {
-    Work& w = *ctx->work;
-    const size_t words = fk::kHardList + waves;
-    if (words <= w.hard_cap) return FEC_OK;
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    if (w.d_hard) HIP_TRY(hipFree(w.d_hard));
-    w.d_hard = nullptr;
-    w.hard_cap = 0;
-    HIP_TRY(hipMalloc(&w.d_hard, words * 4));
-    // count and done (the kernel rewinds them after each use). Ordered on the stream: a plain
-    // hipMemset runs on the null stream, which does not order against the ctx's non-blocking
-    // streams, so the next direct kernel could append to a worklist still holding garbage.
-    HIP_TRY(hipMemsetAsync(w.d_hard, 0, fk::kHardList * 4, ctx->stream));
-    w.hard_cap = words;
-    return FEC_OK;
-}
-
 static int grow_stage(fec_ctx* ctx, size_t bytes) {
     if (bytes <= ctx->stage_cap) return FEC_OK;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -364,21 +343,21 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
     const uint32_t cps = (uint32_t)((len + fk::kChunk - 1) / fk::kChunk);
     const fk::PlanLayout lay_block = fk::plan_layout(k, maxe), lay_sorted = fk::plan_layout(k, maxe, true);
     // Three forms:
-    //  * direct (fec_recover.hip): no plan kernel; single-erasure tables of the code, multi-erasure
-    //    waves planned in-wave from a worklist. Small codes (RS(2,3), RS(8,12)), and the big ones
-    //    when the caller gave one output slot per block (RS(20,30) single erasure +15 % over plan +
-    //    rebuild, r03h);
+    //  * direct (fec_recover.hip): no plan kernel; single-erasure tables of the code, for calls
+    //    where no block can need more (one output slot per block, or m = 1). Small codes (RS(2,3),
+    //    RS(8,12)) and RS(16,24) / RS(20,30) (RS(20,30) single erasure +15 % over plan + rebuild,
+    //    r03h);
     //  * shards of 32+ chunks: sorted plans (fec_plan.hip), then the wave-form rebuild
     //    (fec_rebuild.hip for RS(16,24) / RS(20,30) with 64+ chunks, else fec_decode.hip);
     //  * short shards: plans in block order, then the workgroup-tile rebuild.
     const bool single_slot = out && out_slots == 1;
-    const bool direct = code->d_single_coef && fk::direct_recon_applies(k, m, cps, lay_block.stride, single_slot);
+    const bool direct = code->d_single_coef && fk::direct_recon_applies(k, m, cps, single_slot);
     const bool wave = !direct && fk::wave_recon_applies(cps, k, maxe, lay_sorted.stride);
     const fk::PlanLayout lay = wave ? lay_sorted : lay_block;
     size_t per_launch = std::min<size_t>(direct ? nblocks : kPlanBytes / lay.stride, (size_t)(kMaxItems / cps));
     per_launch = std::max<size_t>(1, std::min(per_launch, nblocks));
-    {
-        const int rc = direct ? grow_hard(ctx, (per_launch * cps + 63) / 64) : grow_plans(ctx, per_launch * lay.stride);
+    if (!direct) {
+        const int rc = grow_plans(ctx, per_launch * lay.stride);
         if (rc) return rc;
     }
     const uint32_t G = fk::pick_tile_blocks(cps, k, maxe, lay);
@@ -427,9 +406,7 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
             a.single = code->d_single;
             a.single_coef = code->d_single_coef;
             a.single_coef_host = code->single_coef.data();
-            a.hard = ctx->work->d_hard;
-            a.hard_cap = (uint32_t)(ctx->work->hard_cap - fk::kHardList);
-            HIP_TRY(fk::launch_rs_recover_direct(a, ctx->ncu, ctx->stream));
+            HIP_TRY(fk::launch_rs_recover_direct(a, ctx->stream));
         } else if (wave) {
             HIP_TRY(fk::launch_rs_plan_sorted(p, ctx->stream));
             if (fk::rebuild_k_applies(k, maxe, cps)) HIP_TRY(fk::launch_rs_rebuild_k(a, ctx->stream));
@@ -1091,11 +1068,6 @@ int fec_ctx_create(int device, fec_ctx** out) {
         if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess && lds > 0)
             fk::g_max_lds = (size_t)lds;
     }
-    if (hipDeviceGetAttribute(&ctx->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
-        ctx->ncu <= 0) {
-        (void)hipGetLastError();
-        ctx->ncu = 256;
-    }
     *out = ctx;
     return FEC_OK;
 }
@@ -1142,7 +1114,7 @@ void fec_ctx_destroy(fec_ctx* ctx) {
 }
 
 // Switch the ctx to `next`. The ctx's own / caller's stream share one workspace (`main`: plan
-// records, the self-rewinding worklist), so work already queued on the old
+// records), so work already queued on the old
 // stream must finish before anything on the new one touches it: the new stream waits on an
 // event recorded on the old one (no host wait). grow_* then sync only the current stream,
 // which by this wait covers the old one's kernels too.
@@ -1246,18 +1218,6 @@ int fec__selftest_permtab(void) {
     return 0;
 }
 
-// Internal diagnostics (not part of the public ABI): the multi-erasure worklist's count and
-// done words of the ctx's own workspace, after waiting for its stream. Both are 0 between calls.
-int fec__worklist_state(fec_ctx* ctx, uint32_t* out2) {
-    if (!ctx || !out2) return FEC_ERR_INVALID_ARG;
-    out2[0] = out2[1] = 0;
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    if (!ctx->main.d_hard) return FEC_OK;
-    HIP_TRY(hipMemcpy(&out2[0], ctx->main.d_hard, 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(&out2[1], ctx->main.d_hard + fk::kHardDone, 4, hipMemcpyDeviceToHost));
-    return FEC_OK;
-}
-
 int fec_ctx_reset_stream(fec_ctx* ctx) {
     if (!ctx) return FEC_ERR_INVALID_ARG;
     return switch_stream(ctx, ctx->own);
@@ -1273,8 +1233,8 @@ int fec_sync(fec_ctx* ctx) {
     HIP_TRY(hipMemcpy(&err, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (err) {
         HIP_TRY(hipMemsetAsync(ctx->d_err, 0, sizeof(int), ctx->stream));
-        // 1: a block with too few shards; 2: more erasures than output slots; 4: internal
-        // (a worklist past its capacity)
+        // 1: a block with too few shards; 2: more erasures than output slots; 4: internal (the
+        // form-3 plan kernel's LDS-alignment guard)
         return (err & 1) ? FEC_ERR_TOO_FEW_SHARDS : (err & 4) ? FEC_ERR_HIP : FEC_ERR_INVALID_ARG;
     }
     return FEC_OK;

@@ -254,7 +254,7 @@ hipError_t launch_rs_reconstruct(const ReconArgs& a, int grid, hipStream_t s) {
 // The wave form applies to shards of 32+ chunks (at most 3 blocks per wave) while its LDS
 // (4 wave slices per workgroup) fits a workgroup (gfx950: 160 KiB; RS(20,30) needs 80 KiB).
 bool wave_recon_applies(uint32_t cps, uint32_t k, uint32_t maxe, uint32_t stride) {
-    return g_tune.dec_wave && cps >= 32 && 4 * fused_slice_bytes(k, maxe, stride) + 2048 <= g_max_lds;
+    return g_tune.dec_wave && cps >= 32 && 4 * wave_slice_bytes(k, maxe, stride) + 2048 <= g_max_lds;
 }
 
 hipError_t launch_rs_reconstruct_wave(const ReconArgs& a, hipStream_t s) {

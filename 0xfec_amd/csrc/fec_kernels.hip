@@ -20,8 +20,6 @@
 // holds the process-wide tuning and the host helpers.
 #include <hip/hip_runtime.h>
 
-#include <map>
-#include <mutex>
 
 #include "fec_kernels.hpp"
 
@@ -48,21 +46,6 @@ PlanLayout plan_layout(uint32_t k, uint32_t maxe, bool sorted) {
     l.coef_off = sorted ? l.blk_off + 4 : (l.nout_off + 1 + 3) & ~3u;
     l.stride = (l.coef_off + maxe * k + 15) & ~15u;
     return l;
-}
-
-int resident_per_cu(const void* kernel, size_t lds) {
-    static std::mutex mu;
-    static std::map<std::pair<const void*, size_t>, int> cache;
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = cache.find({kernel, lds});
-    if (it != cache.end()) return it->second;
-    int per = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kThreads, lds) != hipSuccess || per <= 0) {
-        (void)hipGetLastError();
-        per = 1;
-    }
-    cache[{kernel, lds}] = per;
-    return per;
 }
 
 }  // namespace fk

@@ -95,11 +95,8 @@ struct ReconArgs {
     const uint32_t* single;
     const uint32_t* single_coef;   // the same plans' coefficient bytes: (k*m) rows of ceil(k/4) dwords
     const uint32_t* single_coef_host;   // host copy of single_coef (passed as a kernel argument when small)
-    uint32_t* hard;            // multi-erasure worklist: [0] count, [kHardDone] done, [kHardList..] wave items
-    uint32_t hard_cap;         // entries the worklist holds (a count past it is reported, never written)
 };
 
-constexpr uint32_t kHardDone = 32, kHardList = 64;   // worklist words (own 128-byte lines)
 
 struct XorArgs {
     const uint8_t* in;         // data shard 0 of block 0
@@ -144,9 +141,6 @@ constexpr int kTuningKeys = 11;   // fec__set_tuning keys 0..10, in the order ab
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):
 // halfway between 160K/(wpc+1) and 160K/wpc, never below what the kernel itself needs.
-// Workgroups of `kernel` (kThreads each, `lds` dynamic LDS) resident on one CU at once, by the
-// runtime's occupancy calculator; cached per (kernel, lds). At least 1.
-int resident_per_cu(const void* kernel, size_t lds);
 
 inline size_t occupancy_lds(int wpc, size_t own) {
     if (wpc <= 0) return own;
@@ -180,9 +174,9 @@ hipError_t launch_rs_reconstruct_wave(const ReconArgs& a, hipStream_t s);
 bool rebuild_k_applies(uint32_t k, uint32_t maxe, uint32_t cps);
 hipError_t launch_rs_rebuild_k(const ReconArgs& a, hipStream_t s);
 // Direct form (fec_recover.hip): applies when the single-erasure tables of (k, m) fit in LDS.
-bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t stride, bool single_slot);
+bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, bool single_slot);
 size_t direct_table_words(uint32_t k, uint32_t m);
-hipError_t launch_rs_recover_direct(const ReconArgs& a, int ncu, hipStream_t s);
+hipError_t launch_rs_recover_direct(const ReconArgs& a, hipStream_t s);
 hipError_t launch_xor_encode(const XorArgs& a, int grid, hipStream_t s);
 hipError_t launch_xor_reconstruct(const XorArgs& a, int grid, hipStream_t s);
 

@@ -1,6 +1,6 @@
 // fec_recon.hpp — device pieces shared by the reconstruct kernels (fec_decode.hip: plan + wave /
-// tile rebuild; fec_recover.hip: direct single-erasure rebuild and its multi-erasure worklist;
-// fec_rebuild.hip): the per-item rebuild, the wave slice layout and the in-wave plan construction.
+// tile rebuild; fec_recover.hip: direct single-erasure rebuild; fec_rebuild.hip): the per-item
+// rebuild and the wave slice layout.
 #pragma once
 
 #include "fec_device.hpp"
@@ -174,100 +174,10 @@ __host__ __device__ inline size_t wave_slice_bytes(uint32_t k, uint32_t maxe, ui
     return (size_t)nblk * maxe * k * 32 + (size_t)nblk * stride;
 }
 
-// A wave slice that also holds the scratch of build_wave_plans (below): the direct decode's
-// multi-erasure worklist kernel builds its blocks' plans in-wave (fec_recover.hip).
-__host__ __device__ inline size_t fused_slice_bytes(uint32_t k, uint32_t maxe, uint32_t stride) {
-    return (wave_slice_bytes(k, maxe, stride) + (size_t)k + maxe + 15) & ~(size_t)15;
-}
-
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Build the plan records of the wave's nb (<= 3) blocks bfirst.. into the wave-private `plans`
-// (the work of rs_plan_kernel for these blocks, lanes in parallel): slots and erased indices by
-// prefix popcounts, one erasure by the single-parity-row solution, several by the Lagrange
-// coefficients with the k^2 + e*k lookups spread over the 64 lanes. Writes status / err.
-// `mine`: lane g < nb holds block bfirst + g's present mask.
-__device__ inline void build_wave_plans(const ReconArgs& a, uint8_t* plans, uint32_t bfirst, uint32_t nb,
-                                        uint32_t lane, uint32_t mine, const uint8_t* s_exp, const uint8_t* s_log,
-                                        const uint8_t* s_prows) {
-    const uint32_t k = a.k;
-    const PlanLayout& lay = a.lay;
-    uint8_t* Dt = plans + (size_t)kWaveBlocks * lay.stride;   // k bytes
-    uint8_t* Nt = Dt + k;                                       // maxe bytes
-    const uint32_t m = a.m, n = k + m;
-    const uint32_t all = low_mask(n);
-    const uint32_t kmask = low_mask(k);
-    auto mul = [&](uint32_t x, uint32_t y) -> uint32_t { return (x && y) ? s_exp[s_log[x] + s_log[y]] : 0u; };
-    for (uint32_t g = 0; g < nb; ++g) {
-        const uint32_t b = bfirst + g;
-        uint8_t* P = plans + g * lay.stride;
-        const uint32_t mask = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)g) & all;
-        const uint32_t e = k - __popc(mask & kmask);
-        int32_t st = a.max_out ? (int32_t)e : 0;
-        uint32_t nout = 0;
-        if (e != 0) {
-            if ((uint32_t)__popc(mask) < k) {
-                st = -4;   // FEC_ERR_TOO_FEW_SHARDS
-                if (lane == 0) atomicOr(a.err, 1);
-            } else if (a.max_out && e > a.max_out) {
-                st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
-                if (lane == 0) atomicOr(a.err, 2);
-            } else {
-                nout = e;
-            }
-        }
-        if (lane == 0) {
-            P[lay.nout_off] = (uint8_t)nout;
-            if (a.status) a.status[b] = st;
-        }
-        if (nout) {
-            // the first k present shards (index order) and the erased data shards
-            const uint32_t below = lane < 32 ? ((1u << lane) - 1u) : 0xFFFFFFFFu;
-            if (lane < n && ((mask >> lane) & 1u)) {
-                const uint32_t pos = __popc(mask & below);
-                if (pos < k) P[lay.in_off + pos] = (uint8_t)lane;
-            }
-            if (lane < k && !((mask >> lane) & 1u)) P[lay.out_off + (lane - __popc(mask & kmask & below))] = (uint8_t)lane;
-            wave_sync();
-            const uint8_t* S = P + lay.in_off;
-            uint8_t* C = P + lay.coef_off;
-            if (e == 1) {
-                const uint32_t E0 = __ffs(~mask & kmask) - 1;
-                const uint32_t R0 = __ffs(k < 32 ? mask >> k : 0u) - 1;
-                const uint8_t* row = s_prows + R0 * k;
-                const uint32_t inv = s_exp[255 - s_log[row[E0]]];
-                if (lane < k) {
-                    const uint32_t sj = S[lane];
-                    C[lane] = (uint8_t)(sj < k ? mul(inv, row[sj]) : inv);
-                }
-            } else {
-                if (lane < k) {
-                    const uint32_t sp = S[lane];
-                    uint32_t d = 0;
-                    for (uint32_t q = 0; q < k; ++q)
-                        if (q != lane) d += s_log[sp ^ S[q]];
-                    Dt[lane] = (uint8_t)(d % 255u);
-                }
-                if (lane < e) {
-                    const uint32_t i = P[lay.out_off + lane];
-                    uint32_t ns = 0;
-                    for (uint32_t q = 0; q < k; ++q) ns += s_log[i ^ S[q]];
-                    Nt[lane] = (uint8_t)(ns % 255u);
-                }
-                wave_sync();
-                for (uint32_t t = lane; t < e * k; t += 64) {
-                    const uint32_t r = t / k, p = t - r * k;
-                    const uint32_t v = Nt[r] + 2u * 255u - s_log[P[lay.out_off + r] ^ S[p]] - Dt[p];
-                    C[r * k + p] = s_exp[v % 255u];
-                }
-            }
-        }
-        wave_sync();
-    }
 }
 
 }  // namespace fk

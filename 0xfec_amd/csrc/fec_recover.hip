@@ -11,9 +11,13 @@
 // straight away, while its wave copies the <= 3 table rows it needs into LDS. No plan kernel, no
 // plan records in HBM, no PermTab expansion on the device.
 //
-// A wave holding a block with two or more erasures is put on a worklist instead; a second,
-// persistent kernel (rs_recover_hard_kernel) builds those waves' plans in-wave and rebuilds them
-// through the general path, so the single-erasure kernel keeps its small register footprint.
+// The direct form serves calls where no block can need a multi-erasure rebuild: one output
+// slot per block, or one parity shard (m = 1: two erasures leave too few shards). A block with
+// more erasures than that is an error the kernel reports itself. Multi-slot and in-place calls
+// of the codes with m >= 2 take the sorted-plan route (fec_plan.hip + fec_decode.hip) instead:
+// on batches with multi-erasure blocks mixed in, a direct kernel that handed such waves to a
+// second, multi-erasure kernel ran at half that route's rate, and on single-erasure batches
+// gained only 2.4 % over it (round 5, profiles/r05/mixed_route_*_r05g.log).
 #include <string.h>
 
 #include "fec_recon.hpp"
@@ -23,13 +27,6 @@ namespace fk {
 // LDS of one direct wave (4 per workgroup, no workgroup-level staging, no barrier): the PermTab
 // rows of its <= 3 blocks.
 __host__ __device__ inline size_t direct_wave_bytes(uint32_t k) { return (size_t)kWaveBlocks * k * sizeof(gf::PermTab); }
-
-// LDS of one wave of the multi-erasure kernel: exp/log and the parity rows, then a fused slice
-// (PermTabs of <= 3 blocks' rows, their plan records, Lagrange scratch).
-__host__ __device__ inline size_t hard_head_bytes(uint32_t m, uint32_t k) { return (768 + (size_t)m * k + 15) & ~(size_t)15; }
-__host__ __device__ inline size_t hard_wave_bytes(uint32_t m, uint32_t k, uint32_t maxe, uint32_t stride) {
-    return hard_head_bytes(m, k) + fused_slice_bytes(k, maxe, stride);
-}
 
 constexpr size_t kDirectTableBytes = 16 * 1024;
 
@@ -109,22 +106,6 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
         const WaveMasks wm = wave_masks(a.masks, bfirst, a.nblocks);
         auto mask_of = [&](uint32_t g) { return wm.of(g); };   // g < nb
 
-        // A block with two or more erasures (and enough shards) sends the whole wave to the
-        // worklist of rs_recover_hard_kernel.
-        bool hard = false;
-        for (uint32_t g = 0; g < nb; ++g) {
-            const uint32_t mask = mask_of(g) & all;
-            const uint32_t e = k - __popc(mask & kmask);
-            if (e >= 2 && (uint32_t)__popc(mask) >= k && !(a.max_out && e > a.max_out)) hard = true;
-        }
-        if (hard) {
-            if (lane == 0) {
-                const uint32_t slot = atomicAdd(a.hard, 1u);
-                if (slot < a.hard_cap) a.hard[kHardList + slot] = i0;
-                else atomicOr(a.err, 4);   // never expected: the worklist holds one entry per wave
-            }
-            return;
-        }
         // Per block (uniform): the table row (E0 * m + R0) of a single-erasure block.
         uint32_t row[kWaveBlocks] = {0, 0, 0};
     #pragma unroll
@@ -259,66 +240,6 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
     }
 }
 
-// Waves the direct kernel found holding a multi-erasure block (worklist a.hard: [0] count,
-// [kHardDone] finished workgroups, [kHardList..] item bases): a persistent grid of waves takes them
-// in turn, builds the plans of each wave's blocks in-wave (build_wave_plans, the fused form of
-// fec_decode.hip) and rebuilds them through the general per-item path. With an empty list every
-// wave exits at once. The last workgroup to finish rewinds the worklist for the next launch.
-template <int MAXE>
-__global__ __launch_bounds__(kThreads) void rs_recover_hard_kernel(ReconArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t k = a.k, m = a.m, maxe = a.maxe;
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t count = min(__hip_atomic_load(a.hard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.hard_cap);
-    const uint32_t W = gridDim.x * (kThreads / 64);
-    uint32_t t = blockIdx.x * (kThreads / 64) + wave;
-    if (t < count) {
-        uint8_t* f = smem + (size_t)wave * hard_wave_bytes(m, k, maxe, a.lay.stride);
-        for (uint32_t i = lane; i < 512; i += 64) f[i] = gf::kTables.exp[i];
-        for (uint32_t i = lane; i < 256; i += 64) f[512 + i] = gf::kTables.log[i];
-        for (uint32_t i = lane; i < m * k; i += 64) f[768 + i] = a.prows[i];
-        uint8_t* fs = f + hard_head_bytes(m, k);
-        gf::PermTab* wt = reinterpret_cast<gf::PermTab*>(fs);
-        uint8_t* plans = fs + (size_t)kWaveBlocks * maxe * k * sizeof(gf::PermTab);
-        const uint32_t total = a.nblocks * a.cps;
-        for (; t < count; t += W) {
-            const uint32_t i0 = a.hard[kHardList + t];
-            const uint32_t bfirst = fdiv(i0, a.div_cps);
-            const uint32_t nb = fdiv(min(i0 + 63u, total - 1u), a.div_cps) - bfirst + 1;
-            const uint32_t mine = lane < nb ? a.masks[bfirst + lane] : 0u;
-            wave_sync();   // the previous wave's reads of the slice are done; staging is visible
-            build_wave_plans(a, plans, bfirst, nb, lane, mine, f, f + 512, f + 768);   // statuses too
-            wave_sync();
-            const uint32_t ne = nb * maxe * k;
-            for (uint32_t i = lane; i < ne; i += 64) {
-                const uint32_t g = i / (maxe * k);
-                const uint32_t rem = i - g * maxe * k;
-                const uint32_t r = rem / k, j = rem - r * k;
-                const uint8_t* P = plans + g * a.lay.stride;
-                if (r < P[a.lay.nout_off]) wt[i] = gf::make_permtab_fast(P[a.lay.coef_off + r * k + j]);
-            }
-            wave_sync();
-            const uint32_t item = i0 + lane;
-            const bool inr = item < total;
-            const uint32_t blk = inr ? fdiv(item, a.div_cps) : bfirst;
-            const uint32_t g = blk - bfirst;
-            const uint32_t c = item - blk * a.cps;
-            const uint8_t* P = plans + g * a.lay.stride;
-            const uint32_t nout = inr ? P[a.lay.nout_off] : 0;
-            const uint32_t rows = wave_rows<MAXE>(nout);
-            if (nout) recon_item<MAXE>(a, P, wt + g * maxe * k, blk, c, rows, nout);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (atomicAdd(a.hard + kHardDone, 1u) == gridDim.x - 1) {
-            atomicExch(a.hard, 0u);
-            atomicExch(a.hard + kHardDone, 0u);
-        }
-    }
-}
-
 // RS(2,3) (k = 2, m = 1): a block is rebuilt from its other data shard and the parity with the
 // two coefficients of its erased shard's row, x_E0 = c[E0][0] * x_other ^ c[E0][1] * p. Both rows'
 // PermTabs (4 x 32 bytes) arrive as a kernel argument, so a lane picks its row's words from scalar
@@ -370,18 +291,16 @@ __global__ __launch_bounds__(kThreads) void rs_recover_k2m1_kernel(ReconArgs a, 
 
 size_t direct_table_words(uint32_t k, uint32_t m) { return (size_t)k * m * k * 8; }
 
-bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t stride, bool single_slot) {
+bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, bool single_slot) {
     if (!g_tune.dec_direct || m == 0 || k + m > 32 || cps < 32) return false;
-    // small codes (their PermTab table fits), or RS(20,30) / RS(16,24) with their rows read from
-    // device memory when the caller gave one output slot per block (no block can need the
-    // multi-erasure worklist: two or more erasures are an error the kernel reports itself). For
-    // mixed batches of the big codes the plan path is level with the direct one on single
-    // erasures and faster on mixed ones (r04p: a device-side classify picking per batch cost 3-7 %).
+    // only where no block can need a multi-erasure rebuild (one output slot, or one parity shard:
+    // more erasures are an error the kernel reports itself; see the top of this file), for small
+    // codes (their PermTab table fits) and RS(20,30) / RS(16,24) with their rows read from device
+    // memory
+    if (!single_slot && m != 1) return false;
     const bool small = (size_t)k * m * k * sizeof(gf::PermTab) <= kDirectTableBytes;
     const bool big = (k == 20 && m == 10) || (k == 16 && m == 8);
-    if (!small && !(big && single_slot)) return false;
-    const uint32_t maxe = std::max<uint32_t>(1, std::min(k, m));
-    return 4 * hard_wave_bytes(m, k, maxe, stride) <= g_max_lds;
+    return (small || big) && 4 * direct_wave_bytes(k) <= g_max_lds;
 }
 
 template <int K, int TAB>
@@ -399,17 +318,7 @@ static hipError_t direct_launch(const ReconArgs& a0, const CoefWords& cw, hipStr
     return hipGetLastError();
 }
 
-template <int MAXE>
-static hipError_t hard_launch(const ReconArgs& a, int ncu, hipStream_t s) {
-    const size_t lds = 4 * hard_wave_bytes(a.m, a.k, a.maxe, a.lay.stride);
-    // a persistent grid of exactly the workgroups that are resident at once: more would wait
-    // for a second round behind the first
-    const int grid = ncu * resident_per_cu((const void*)rs_recover_hard_kernel<MAXE>, lds);
-    hipLaunchKernelGGL((rs_recover_hard_kernel<MAXE>), dim3(grid), dim3(kThreads), lds, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_rs_recover_direct(const ReconArgs& a, int ncu, hipStream_t s) {
+hipError_t launch_rs_recover_direct(const ReconArgs& a, hipStream_t s) {
     // the reference's benchmark shapes at compile time, the rest by runtime k. Non-temporal loads
     // and stores for every code: plain loads measured +8 % for RS(2,3) (r02), but only because its
     // 65 536-block batch (239 MB) fits the 256 MiB Infinity Cache and back-to-back launches re-read
@@ -440,13 +349,7 @@ hipError_t launch_rs_recover_direct(const ReconArgs& a, int ncu, hipStream_t s) 
         e = by_arg ? direct_launch<2, 1>(a, cw, s) : direct_launch<2, 0>(a, cw, s);
     else
         e = by_arg ? direct_launch<0, 1>(a, cw, s) : direct_launch<0, 0>(a, cw, s);
-    // m = 1: two erasures always leave too few shards; one output slot: a block with two or more
-    // erasures is an error the direct kernel reports itself (nothing goes to the worklist)
-    if (e != hipSuccess || a.m < 2 || a.max_out == 1) return e;
-    if (a.maxe <= 2) return hard_launch<2>(a, ncu, s);
-    if (a.maxe <= 4) return hard_launch<4>(a, ncu, s);
-    if (a.maxe <= 8) return hard_launch<8>(a, ncu, s);
-    return hard_launch<16>(a, ncu, s);
+    return e;
 }
 
 }  // namespace fk

@@ -321,14 +321,16 @@ def test_rs_encode_kernel_variants_match_oracle(codec, oracle, torch, variant, k
     assert not got[:, :, L:].any()               # pad to the 16-byte boundary written as zeros
 
 
-# Every shipped reconstruct path against the oracle, in place and out of place, with the erasure
-# counts mixed inside waves: "default" (the direct kernel and its multi-erasure worklist for RS(2,3)
-# and RS(8,12); sorted plans + the rebuild for RS(16,24) / RS(20,30): fec_rebuild.hip where shards
-# have 64+ chunks, the compile-time-k wave form below that), "plan" (no direct kernel: sorted plans +
-# the wave form for every code), "tile" (plans in block order + the workgroup-tile rebuild, the
-# short-shard path, on long shards too), "table" (the direct kernel's rows copied from the PermTab
-# table rather than expanded from the kernel argument), and "wpc2" (the default at two workgroups
-# per CU). L = 1008 / 1017: shards of 63 / 64 chunks, the edge of the rebuild's two-block slices.
+# Every shipped reconstruct path against the oracle, in place and out of place (m slots), with the
+# erasure counts mixed inside waves: "default" (the direct kernel for RS(2,3) and the other m = 1
+# codes; sorted plans + the rebuild for the rest: fec_rebuild.hip for RS(16,24) / RS(20,30) where
+# shards have 64+ chunks, the compile-time-k or runtime-k wave form below that), "plan" (no direct
+# kernel: sorted plans + the wave form for every code), "tile" (plans in block order + the
+# workgroup-tile rebuild, the short-shard path, on long shards too), "table" (the direct kernel's
+# rows copied from the PermTab table rather than expanded from the kernel argument), and "wpc2"
+# (the default at two workgroups per CU). L = 1008 / 1017: shards of 63 / 64 chunks, the edge of
+# the rebuild's two-block slices. The single-slot test below covers the direct kernel of the
+# m >= 2 codes.
 DEC_VARIANTS = {
     "default": {},
     "plan": dict(dec_direct=0),
@@ -368,6 +370,46 @@ def test_rs_reconstruct_kernel_variants_match_oracle(codec, oracle, torch, fec, 
     codec.rs_reconstruct_split(k, m, data, par, dm, shard_len=L)
     codec.sync()
     assert np.array_equal(data.cpu().numpy()[:, :, :L], sh[:, :k, :L])
+
+
+# One output slot per block (the bench's form): the direct kernel for every code whose tables it
+# serves (RS(8,12), RS(4,12), RS(2,3), and RS(16,24) / RS(20,30) from the device table), mixed
+# erasure counts: a block with one erased data shard is rebuilt into its slot, status 1; none
+# erased, status 0; two or more with enough shards, status -1 (FEC_ERR_INVALID_ARG: more erasures
+# than slots); too few shards, -4. The same semantics on the plan routes ("plan", "tile").
+@pytest.mark.parametrize("variant", sorted(DEC_VARIANTS))
+@pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10), (4, 8), (10, 22)])
+@pytest.mark.parametrize("L", [513, 1202])
+def test_rs_recover_single_slot_variants_match_oracle(codec, oracle, torch, fec, tune, variant, k, m, L):
+    rng = np.random.default_rng(3 * k + L + 100 * sorted(DEC_VARIANTS).index(variant))
+    n, B = k + m, 517
+    S = (L + 15) // 16 * 16
+    sh = _rand_shards(rng, B, n, S, L)
+    oracle.rs_encode(k, m, sh)
+    masks = _random_masks(rng, B, k, m, max_loss=min(n, m + 1))
+    lost = ~((masks[:, None] >> np.arange(n)[None, :]) & 1).astype(bool)
+    e_d = lost[:, :k].sum(axis=1)
+    few = (n - lost.sum(axis=1)) < k
+    want = np.where(e_d == 0, 0, np.where(few, -4, np.where(e_d > 1, -1, 1)))
+    data_np = np.ascontiguousarray(sh[:, :k]).copy()
+    data_np[lost[:, :k]] = 0x3C
+    data = torch.from_numpy(data_np).cuda()
+    par = torch.from_numpy(np.ascontiguousarray(sh[:, k:])).cuda()
+    dm = torch.from_numpy(masks.view(np.int32)).cuda()
+    tune(**DEC_VARIANTS[variant])
+    out = torch.full((B, 1, S), 0xEE, dtype=torch.uint8, device="cuda")
+    st = torch.full((B,), 99, dtype=torch.int32, device="cuda")
+    codec.rs_recover_split(k, m, data, par, dm, out, status=st, shard_len=L)
+    if (want < 0).any():
+        with pytest.raises(fec.FecError):
+            codec.sync()
+    else:
+        codec.sync()
+    assert np.array_equal(st.cpu().numpy(), want)
+    got = out.cpu().numpy()
+    for b in np.nonzero(want == 1)[0]:
+        i = int(np.nonzero(lost[b, :k])[0][0])
+        assert np.array_equal(got[b, 0, :L], sh[b, i, :L]), (b, i)
 
 
 # The sorted plan kernel's two forms on codes of both sum forms: n - k < k sums over the
@@ -545,9 +587,8 @@ def test_xor_host_pipeline_matches_oracle(codec, oracle, torch, fec, pinned):
 @pytest.mark.parametrize("k,m,chunk", [(8, 4, 61), (16, 8, 37), (20, 10, 64)])
 def test_rs_host_pipeline_many_chunks_multi_erasure(codec, oracle, fec, k, m, chunk):
     """Host-path reconstruct over many small chunks (consecutive chunks run on the two staging
-    sets' streams at once) with up to m erasures per block: the multi-erasure worklist (RS(8,12))
-    and the plan records (RS(16,24), RS(20,30)) are per stream, so overlapping chunks never share
-    one. Checked against the oracle block by block."""
+    sets' streams at once) with up to m erasures per block: the plan records are per stream, so
+    overlapping chunks never share one. Checked against the oracle block by block."""
     rng = np.random.default_rng(7000 + k + chunk)
     n, B, L = k + m, 1500, 600
     full = np.zeros((B, n, L), dtype=np.uint8)

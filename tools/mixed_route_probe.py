@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
-"""Diagnostics: RS decode routes on mixed-erasure batches of the small codes (those the direct
-single-erasure kernel serves by default: k*m*k PermTabs <= 16 KiB). Each code runs a batch with
-e ~ U{1..m} losses uniform over all n shards (every block recoverable), one output slot per
-possible data loss, through the default route (direct kernel + hard worklist), the sorted-plan
-wave route (knob dec_direct=0) and the tile route (dec_direct=0, dec_wave=0), interleaved in one
-process; the outputs of the routes are compared byte for byte.
+"""Diagnostics: RS decode routes on mixed-erasure batches of the small codes (k*m*k PermTabs <=
+16 KiB, the direct kernel's). Each code runs a batch with e ~ U{1..MULTI} losses uniform over all
+n shards (every block recoverable), m output slots per block (a caller that does not scan the
+masks first), through the default route, the sorted-plan wave route (knob dec_direct=0) and the
+tile route (dec_direct=0, dec_wave=0), interleaved in one process; the outputs of the routes are
+compared byte for byte. (Round 5 measured with it the direct kernel + multi-erasure worklist that
+multi-slot calls took before: profiles/r05/mixed_route*_r05g.log.)
 
-usage: mixed_route_probe.py [blocks] [rounds]"""
+usage: mixed_route_probe.py [blocks] [rounds] [--code K,M,MULTI ...] [--routes default,wave]"""
 import importlib
 import json
 import os
@@ -19,14 +20,24 @@ ROUTES = {"default": {}, "wave": {"dec_direct": 0}, "tile": {"dec_direct": 0, "d
 
 
 def main():
-    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    argv = sys.argv[1:]
+    codes, routes = [], list(ROUTES)
+    while "--code" in argv:
+        i = argv.index("--code")
+        codes.append(tuple(int(x) for x in argv[i + 1].split(",")))
+        del argv[i:i + 2]
+    if "--routes" in argv:
+        i = argv.index("--routes")
+        routes = argv[i + 1].split(",")
+        del argv[i:i + 2]
+    args = [a for a in argv if not a.startswith("--")]
     B = int(args[0]) if args else 1 << 18
     rounds = int(args[1]) if len(args) > 1 else 5
     import torch
     fec = importlib.import_module("0xfec_amd")
     codec = fec.Codec(0).use_torch_stream()
     res = {}
-    for k, m, multi in ((8, 4, 4), (8, 4, 2), (10, 4, 4), (4, 2, 2), (2, 2, 2)):
+    for k, m, multi in codes or ((8, 4, 4), (8, 4, 2), (8, 4, 1), (10, 4, 4), (4, 2, 2), (2, 2, 2)):
         n = k + m
         codec.prepare(k, m)
         g = torch.Generator(device="cuda")
@@ -40,9 +51,9 @@ def main():
         w = torch.bitwise_left_shift(torch.ones(n, dtype=torch.int64, device="cuda"), torch.arange(n, device="cuda"))
         masks = ((~lost).to(torch.int64) * w).sum(dim=1).to(torch.int32)
         e_d = lost[:, :k].sum(dim=1)
-        slots = max(1, int(e_d.max().item()))
+        slots = m   # as a caller that does not scan the masks first
         nbytes = int(((k + e_d) * (e_d > 0)).sum().item()) * L
-        outs = {r: torch.zeros((B, slots, S), dtype=torch.uint8, device="cuda") for r in ROUTES}
+        outs = {r: torch.zeros((B, slots, S), dtype=torch.uint8, device="cuda") for r in routes}
 
         def dec(r):
             def fn():
@@ -63,12 +74,12 @@ def main():
 
         name = "RS(%d,%d) U{1..%d}" % (k, n, multi)
         for _ in range(rounds):
-            for r, knobs in ROUTES.items():
-                old = codec.set_tuning(**knobs)
+            for r in routes:
+                old = codec.set_tuning(**ROUTES[r])
                 res.setdefault(name, {}).setdefault(r, []).append(timed(dec(r)))
                 codec.set_tuning(**old)
         torch.cuda.synchronize()
-        same = all(torch.equal(outs["default"], outs[r]) for r in ROUTES)
+        same = all(torch.equal(outs[routes[0]], outs[r]) for r in routes)
         med = {r: round(sorted(v)[len(v) // 2], 4) for r, v in res[name].items()}
         print(json.dumps({"code": name, "blocks": B, "routes_agree": same, "median_ms": med,
                           "TBps": {r: round(nbytes / t / 1e9, 3) for r, t in med.items()}}), flush=True)
