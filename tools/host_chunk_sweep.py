@@ -5,9 +5,10 @@ packed pinned and pageable host buffers).
 
     python tools/host_chunk_sweep.py [--blocks 131072] [--threads 4,8,12,16 [--reps 3]]
 
-One JSON line per setting: knob host_chunk (blocks per chunk; 0 = the library's default, 128 MiB
-of staged shards) and host_gather (1: sparse parity planes pulled by the device, dense ones by
-2D DMA; 2: every plane pulled by the device; 0: every plane by DMA)."""
+One JSON line per setting of knob host_chunk (blocks per chunk; 0 = the library's default: up to
+128 MiB of staged shards, a mid-sized call split over the three staging sets), or of host_threads
+with --threads. (Round 4 also swept host_gather, the parity-plane policy; round 5 fixed it to the
+measured rule, sparse planes pulled by the device and dense ones by 2D DMA, and removed the knob.)"""
 import argparse
 import importlib
 import json
