@@ -154,15 +154,19 @@ def xor_main(args):
         ctxs.append(ctx)
     FEC_DEVICE = 0
 
+    # each library its own buffers for the byte comparison, then both the same ones for the timing
+    # (as in the RS mode)
+    own = [True]
+
     def enc(i):
-        p = shs[i].data_ptr()
+        p = shs[i if own[0] else 0].data_ptr()
         assert libs[i].fec_xor_encode_batch(ctxs[i], k, L, B, p, n * S, p + k * S, n * S, S, FEC_DEVICE) == 0
 
     use_status = [True]
 
     def rec(i):
-        p = shs[i].data_ptr()
-        st = sts[i].data_ptr() if use_status[0] else None
+        p = shs[i if own[0] else 0].data_ptr()
+        st = sts[i if own[0] else 0].data_ptr() if use_status[0] else None
         assert libs[i].fec_xor_reconstruct_batch(ctxs[i], k, L, B, p, n * S, p + k * S, n * S, S, masks.data_ptr(),
                                                  st, FEC_DEVICE) == 0
 
@@ -187,6 +191,7 @@ def xor_main(args):
     assert torch.equal(sts[0], sts[1]), "statuses differ"
     assert torch.equal(shs[0], shs[1]), "reconstruct outputs differ"
     use_status[0] = not args.no_status
+    own[0] = False
 
     def t(fn, i):
         fn(i)
