@@ -7,7 +7,8 @@ against one contiguous allocation.
 
 usage: arena_probe.py [blocks] [rounds] [--more (three more arrangements)] [--sweep (the gap between
        data and parity in one allocation)] [--order (which region lies above which)]
-       [--arena-first]"""
+       [--arena-first] [--interleaved | --interleaved-first (each block's n
+       shards contiguous)]"""
 import importlib
 import json
 import os
@@ -44,9 +45,22 @@ def main():
         keep.append(a)
         a0 = a.data_ptr()
         lay["arena"] = (a0, a0 + nd, a0 + nd + npar)
+    def interleaved():
+        # each block's k data and m parity shards contiguous ([B][n][S], the batch layer's staging
+        # layout), the recovered shards after them
+        il = torch.zeros(B * (k + m) * S + no, dtype=torch.uint8, device="cuda")
+        keep.append(il)
+        i0 = il.data_ptr()
+        lay["interleaved"] = (i0, i0 + k * S, i0 + B * (k + m) * S)
     # --arena-first: the arena is allocated before the separate buffers (the first allocations of
-    # a process take the first device memory the runtime hands out)
-    for f in ((arena, separate) if "--arena-first" in sys.argv else (separate, arena)):
+    # a process take the first device memory the runtime hands out); --interleaved: the
+    # interleaved layout too, allocated last, or first with --interleaved-first
+    order = [arena, separate] if "--arena-first" in sys.argv else [separate, arena]
+    if "--interleaved-first" in sys.argv:
+        order = [interleaved] + order
+    elif "--interleaved" in sys.argv:
+        order = order + [interleaved]
+    for f in order:
         f()
     if "--more" in sys.argv:
         # regions in the other order; with 1 GiB gaps between them; data alone + parity and
@@ -88,8 +102,9 @@ def main():
         for g in gaps:
             lay["gap%dM" % (g // MB)] = (b0, b0 + nd + g, b0 + nd + g + npar)
         del lay["separate"], lay["arena"]
-    for dp, _, _ in lay.values():
-        codec.synth_data(0x0FEC, 0, B, k, 1200, dp, k * S, S)
+    strides = {nm: ((k + m) * S, (k + m) * S) if nm == "interleaved" else (k * S, m * S) for nm in lay}
+    for nm, (dp, _, _) in lay.items():
+        codec.synth_data(0x0FEC, 0, B, k, 1200, dp, strides[nm][0], S)
 
     def timed(fn, n=20):
         fn()
@@ -104,11 +119,13 @@ def main():
     res = {}
     for _ in range(rounds):
         for name, (dp, pp, op) in lay.items():
+            dbs, pbs = strides[name]
+
             def enc():
-                codec.rs_encode_raw(k, m, L, B, dp, k * S, pp, m * S, S, fec.FEC_DEVICE)
+                codec.rs_encode_raw(k, m, L, B, dp, dbs, pp, pbs, S, fec.FEC_DEVICE)
 
             def dec():
-                rc = codec.rs_recover_raw(k, m, L, B, dp, k * S, pp, m * S, S, masks.data_ptr(), op, S, 1, None)
+                rc = codec.rs_recover_raw(k, m, L, B, dp, dbs, pp, pbs, S, masks.data_ptr(), op, S, 1, None)
                 assert rc == 0
             res.setdefault(name + " encode", []).append(timed(enc))
             res.setdefault(name + " decode", []).append(timed(dec))
