@@ -94,17 +94,20 @@ def test_single_erasure_config_full_batch(fec, oracle, torch, k, m, B):
         codec.close()
 
 
-@pytest.mark.parametrize("k,m", [(16, 8), (20, 10)], ids=["config4_rs16_24", "rs20_30_reference_code"])
+@pytest.mark.parametrize("k,m", [(16, 8), (20, 10), (8, 4)], ids=["config4_rs16_24", "rs20_30_reference_code",
+                                                                 "rs8_12_mixed"])
 def test_mixed_erasures_full_batch(fec, oracle, torch, k, m):
-    """2^19 blocks with e ~ U{1..m} lost shards per block, uniform over all n: RS(16,24) (config #4)
-    and RS(20,30), the reference's own sender/receiver code (manager.go:58-59,81-82)."""
+    """2^19 blocks with e ~ U{1..m} lost shards per block, uniform over all n: RS(16,24) (config #4),
+    RS(20,30), the reference's own sender/receiver code (manager.go:58-59,81-82), and RS(8,12)
+    (the bench's code with multi-erasure blocks: the sorted-plan route with the runtime-k
+    rebuild, which multi-slot calls of the small codes take since round 5)."""
     B = 1 << 19
     n = k + m
     codec = fec.Codec(0).use_torch_stream()
     try:
         data, par = _batch(torch, codec, k, m, B)
         g = torch.Generator(device="cuda")
-        g.manual_seed(0x1624 if k == 16 else 0x2030)
+        g.manual_seed({16: 0x1624, 20: 0x2030}.get(k, 0x0812))
         e = torch.randint(1, m + 1, (B,), device="cuda", generator=g)
         rank = torch.rand((B, n), device="cuda", generator=g).argsort(dim=1).argsort(dim=1)
         lost = rank < e[:, None]
