@@ -8,6 +8,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 RT=$(ls /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so | head -n1)
 python "$ROOT/tests/c/build.py"
 cd /tmp
-LD_PRELOAD="$RT" ASAN_OPTIONS=detect_leaks=0:halt_on_error=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
+# the ASan runtime goes first in LD_PRELOAD; anything already preloaded stays behind it
+LD_PRELOAD="$RT${LD_PRELOAD:+:$LD_PRELOAD}" ASAN_OPTIONS=detect_leaks=0:halt_on_error=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
     FEC_LIB_PATH="$ROOT/0xfec_amd/_san/lib0xfec_hip_san.so" \
     python -m pytest "$ROOT/tests" -m "not gpu" -q -p no:cacheprovider "$@"
