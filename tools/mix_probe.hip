@@ -72,7 +72,7 @@ extern "C" int mix_probe(const void* in, void* out, size_t in_bs, size_t out_bs,
     }
     MK(1, 1, 1) MK(1, 1, 2) MK(1, 1, 4) MK(8, 4, 1) MK(8, 4, 2) MK(8, 1, 1) MK(8, 1, 2) MK(8, 0, 1) MK(0, 1, 1)
     MK(0, 1, 4) MK(2, 1, 1) MK(4, 1, 1) MK(2, 2, 1) MK(4, 4, 1) MK(8, 8, 1) MK(8, 2, 1) MK(4, 2, 1) MK(16, 8, 1)
-    MK(16, 3, 1)
+    MK(16, 3, 1) MK(8, 4, 4) MK(8, 1, 4)
     return -1;
 }
 

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Diagnostics: mixed read/write HBM rates vs output offset, XCD mapping, occupancy, items per
-lane (tools/mix_probe.hip). Prints one JSON object; rates are bytes moved / time in GB/s."""
+lane (tools/mix_probe.hip). Prints one JSON object; rates are bytes moved / time in GB/s.
+
+usage: mix_probe.py [sweep1|sweep2|sweep3|persist|ipl] [--rebuild] [--build-only]"""
 import ctypes
 import json
 import os
@@ -113,6 +115,19 @@ def main():
                 res["r%d w%d ss%d cps%d" % (nin, nout, sst, c)] = run_ss()
                 res["r%d w%d ss%d cps%d swz wg2" % (nin, nout, sst, c)] = run_ss(swz=1, pad=64 << 10)
             flush()
+    elif mode == "ipl":
+        # items per lane x resident workgroups per CU, XCD-contiguous order, interleaved rounds:
+        # whether fewer waves with more loads each move the encode / decode shapes faster
+        B = 1 << 20
+        pads = {1: 96 << 10, 2: 64 << 10, 3: 48 << 10, 4: 36 << 10, 5: 30 << 10}
+        acc = {}
+        for rnd in range(3):
+            for nin, nout in ((8, 4), (8, 1)):
+                for ipl in (1, 2, 4):
+                    for w, pad in pads.items():
+                        acc.setdefault("r%d w%d ipl%d wg%d" % (nin, nout, ipl, w), []).append(
+                            run(nin, nout, B, nin * ss, nout * ss, 0, ipl=ipl, swz=1, pad=pad))
+        res.update({kk: sorted(v)[1] for kk, v in acc.items()})
     elif mode == "persist":
         B = 1 << 20
         ctr = torch.zeros(1024, dtype=torch.int32, device="cuda")
