@@ -161,8 +161,10 @@ def test_rs_host_path_matches_oracle(codec, oracle, k, m):
 
 
 @pytest.mark.parametrize("k", [1, 2, 3, 5, 9, 31])
-@pytest.mark.parametrize("L", [1, 6, 18, 1202, 1436])
+@pytest.mark.parametrize("L", [1, 6, 18, 513, 1202, 1436])
 def test_xor_device_matches_oracle(codec, oracle, torch, fec, k, L):
+    # L = 513: 33 chunks per shard, so a wave's 64 items span three blocks (the reconstruct's
+    # scalar mask loads take up to three); L < 497: the per-lane mask load
     rng = np.random.default_rng(k + L)
     n = k + 1
     S = (L + 15) // 16 * 16
