@@ -10,7 +10,8 @@ against the oracle (internal/fec reed_solomon.go:51,124 through klauspost's Reco
   * encode parity, bit-exact, pad bytes up to the 16-byte boundary written as zeros;
   * recover: per-block status (rebuilt count, -1 more erasures than slots, -4 too few shards)
     and every rebuilt shard, in ascending order of its index;
-  * reconstruct in place: the data region of every block that has enough shards.
+  * reconstruct in place: the data region of every block that has enough shards;
+  * every fourth case also through the host-resident form (FEC_HOST, packed numpy shards).
 XOR(k, 1) cases run beside them. The draws are fixed by the seed, so a failure names its case.
 """
 import numpy as np
@@ -132,3 +133,19 @@ def test_random_case_matches_oracle(codec, oracle, torch, fec, case):
     g = data.cpu().numpy()
     ok = ~few | (e_d == 0)
     assert np.array_equal(g[ok, :, :L], ref[ok, :k, :L]), (tag, "in place")
+    if case % 4 == 0:
+        # the host-resident form (FEC_HOST: numpy buffers staged through pinned memory), packed
+        # shards (stride = shard length) as the reference's per-block slices are
+        hs = np.ascontiguousarray(ref[:, :, :L])
+        enc = hs.copy()
+        enc[:, k:] = 0
+        codec.rs_encode(k, m, enc)
+        assert np.array_equal(enc, hs), (tag, "host parity")
+        dmg = hs.copy()
+        dmg[lost] = 0x77
+        hst = np.full(B, 7, dtype=np.int32)
+        rc = codec.rs_reconstruct(k, m, dmg, masks, status=hst)
+        bad = few & (e_d > 0)
+        assert rc == (fec.FEC_ERR_TOO_FEW_SHARDS if bad.any() else fec.FEC_OK), (tag, "host rc")
+        assert np.array_equal(hst == 0, ~bad), (tag, "host status")
+        assert np.array_equal(dmg[~bad, :k], hs[~bad, :k]), (tag, "host rebuilt")
