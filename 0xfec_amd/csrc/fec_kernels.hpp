@@ -129,8 +129,9 @@ struct Tuning {
     std::atomic<int> enc_fixed{1};  // 0: every shape by the generic encode
     std::atomic<int> dec_wave{1};   // 0: the workgroup-tile rebuild for long shards too
     std::atomic<int> dec_direct{1}; // 0: no direct decode (plan path for every code); 1: direct where it
-                                    // applies, rows by scalar loads where the coefficient words fit the
-                                    // kernel argument; 2: rows always copied from the PermTab table
+                                    // applies (one output slot, or m = 1), rows from the kernel
+                                    // argument where the coefficient words fit it (RS(2,3): its own
+                                    // kernel); 2: rows always copied from the PermTab table
     // host paths
     std::atomic<int> host_chunk{0};     // FEC_HOST / FEC_HOST_PINNED: blocks per staging chunk (0: 128 MiB worth)
     std::atomic<int> host_threads{8};   // FEC_HOST (pageable): copy workers for the staging / scatter copies
