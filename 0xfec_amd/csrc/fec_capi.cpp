@@ -84,8 +84,11 @@ constexpr uint64_t kMaxItems = uint64_t(1) << 31;
 struct Work {
     uint8_t* d_plans = nullptr;
     size_t plans_cap = 0;
+    uint32_t* d_wflags = nullptr;   // deferred in-place decode: one word per 64-block window
+    size_t wflags_cap = 0;
     void release() {
         if (d_plans) (void)hipFree(d_plans);
+        if (d_wflags) (void)hipFree(d_wflags);
         *this = Work{};
     }
 };
@@ -262,6 +265,18 @@ static int grow_plans(fec_ctx* ctx, size_t bytes) {
     return FEC_OK;
 }
 
+static int grow_wflags(fec_ctx* ctx, size_t n) {
+    Work& w = *ctx->work;
+    if (n <= w.wflags_cap) return FEC_OK;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (w.d_wflags) HIP_TRY(hipFree(w.d_wflags));
+    w.d_wflags = nullptr;
+    w.wflags_cap = 0;
+    HIP_TRY(hipMalloc(&w.d_wflags, n * 4));
+    w.wflags_cap = n;
+    return FEC_OK;
+}
+
 static int grow_stage(fec_ctx* ctx, size_t bytes) {
     if (bytes <= ctx->stage_cap) return FEC_OK;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -350,14 +365,24 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
     //  * shards of 32+ chunks: sorted plans (fec_plan.hip), then the wave-form rebuild
     //    (fec_rebuild.hip for RS(16,24) / RS(20,30) with 64+ chunks, else fec_decode.hip);
     //  * short shards: plans in block order, then the workgroup-tile rebuild.
+    //  * deferred (in-place calls of the small m >= 2 codes): the direct kernel rebuilds the blocks
+    //    with one erased data shard and flags each 64-block window holding a block with more; the
+    //    sorted plans and the wave rebuild then run over the flagged windows only (their launches
+    //    exit at once on single-erasure batches).
     const bool single_slot = out && out_slots == 1;
     const bool direct = code->d_single_coef && fk::direct_recon_applies(k, m, cps, single_slot);
     const bool wave = !direct && fk::wave_recon_applies(cps, k, maxe, lay_sorted.stride);
+    const bool defer = wave && !out && code->d_single_coef && fk::defer_recon_applies(k, m, cps) &&
+                       !fk::rebuild_k_applies(k, maxe, cps);
     const fk::PlanLayout lay = wave ? lay_sorted : lay_block;
     size_t per_launch = std::min<size_t>(direct ? nblocks : kPlanBytes / lay.stride, (size_t)(kMaxItems / cps));
     per_launch = std::max<size_t>(1, std::min(per_launch, nblocks));
     if (!direct) {
         const int rc = grow_plans(ctx, per_launch * lay.stride);
+        if (rc) return rc;
+    }
+    if (defer) {
+        const int rc = grow_wflags(ctx, (per_launch + 63) / 64);
         if (rc) return rc;
     }
     const uint32_t G = fk::pick_tile_blocks(cps, k, maxe, lay);
@@ -396,7 +421,7 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         a.sorted = wave ? 1u : 0u;
         a.out = out ? out + b0 * out_bs : nullptr;
         a.out_bs = out_bs;
-        if (direct) {
+        if (direct || defer) {
             a.masks = p.masks;
             a.status = p.status;
             a.err = p.err;
@@ -406,7 +431,16 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
             a.single = code->d_single;
             a.single_coef = code->d_single_coef;
             a.single_coef_host = code->single_coef.data();
+        }
+        if (direct) {
             HIP_TRY(fk::launch_rs_recover_direct(a, ctx->stream));
+        } else if (defer) {
+            a.wflags = ctx->work->d_wflags;
+            HIP_TRY(fk::launch_rs_recover_direct(a, ctx->stream));
+            p.wflags = a.wflags;
+            p.min_e = 2;
+            HIP_TRY(fk::launch_rs_plan_sorted(p, ctx->stream));
+            HIP_TRY(fk::launch_rs_reconstruct_wave(a, ctx->stream));
         } else if (wave) {
             HIP_TRY(fk::launch_rs_plan_sorted(p, ctx->stream));
             if (fk::rebuild_k_applies(k, maxe, cps)) HIP_TRY(fk::launch_rs_rebuild_k(a, ctx->stream));
@@ -471,6 +505,12 @@ static int xor_reconstruct_device(fec_ctx* ctx, int k, size_t len, size_t nblock
 }
 
 // ---------------------------------------------------------------- validation helpers
+
+// FEC_DEVICE masks and statuses are read and written as 4-byte words (the masks by scalar loads,
+// which ignore the low two address bits: a misaligned mask array would be read wrong, silently).
+static int check_device_words(const uint32_t* masks, const int32_t* status) {
+    return (((uintptr_t)masks | (uintptr_t)status) & 3u) ? FEC_ERR_ALIGNMENT : FEC_OK;
+}
 
 static int check_device_layout(const void* p, size_t bs, size_t ss, size_t len) {
     if (!p) return FEC_ERR_INVALID_ARG;
@@ -1136,21 +1176,31 @@ int fec_ctx_release_staging(fec_ctx* ctx) {
     for (hipStream_t q : {p.up, p.comp, p.down})
         if (q) HIP_TRY(hipStreamSynchronize(q));
     if (ctx->stream) HIP_TRY(hipStreamSynchronize(ctx->stream));
+    // Every buffer is freed and forgotten even when a free fails (the first failure is returned),
+    // so the ctx never keeps a pointer it has handed back.
+    hipError_t first = hipSuccess;
+    auto drop = [&first](hipError_t e) {
+        if (e != hipSuccess && first == hipSuccess) first = e;
+    };
     for (HostSet& s : p.set) {
         for (void* q : {(void*)s.h_in, (void*)s.h_out, (void*)s.h_masks, (void*)s.h_status})
-            if (q) HIP_TRY(hipHostFree(q));
+            if (q) drop(hipHostFree(q));
         for (void* q : {(void*)s.d_in, (void*)s.d_out, (void*)s.d_masks, (void*)s.d_status, (void*)s.d_raw_in,
                         (void*)s.d_raw_out})
-            if (q) HIP_TRY(hipFree(q));
+            if (q) drop(hipFree(q));
         s.h_in = s.h_out = s.d_in = s.d_out = s.d_raw_in = s.d_raw_out = nullptr;
         s.h_masks = s.d_masks = nullptr;
         s.h_status = s.d_status = nullptr;
         s.in_cap = s.out_cap = s.blk_cap = s.raw_in_cap = s.raw_out_cap = 0;
     }
-    if (ctx->h_stage) HIP_TRY(hipHostFree(ctx->h_stage));
-    if (ctx->d_stage) HIP_TRY(hipFree(ctx->d_stage));
+    if (ctx->h_stage) drop(hipHostFree(ctx->h_stage));
+    if (ctx->d_stage) drop(hipFree(ctx->d_stage));
     ctx->h_stage = ctx->d_stage = nullptr;
     ctx->stage_cap = 0;
+    if (first != hipSuccess) {
+        (void)hipGetLastError();
+        return FEC_ERR_HIP;
+    }
     return FEC_OK;
 }
 
@@ -1168,7 +1218,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
     fk::Tuning& t = fk::g_tune;
     std::atomic<int>* slots[fk::kTuningKeys] = {&t.enc_wpc,   &t.gen_wpc,    &t.dec_wpc,      &t.dir_wpc,
                                                 &t.enc_bwpc,  &t.enc_fixed,  &t.dec_wave,     &t.dec_direct,
-                                                &t.host_chunk, &t.host_threads, &t.bat_zc};
+                                                &t.host_chunk, &t.host_threads, &t.bat_zc,     &t.enc_glds,
+                                                &t.dec_defer,  &t.st_pol};
     if (key < 0 || key >= fk::kTuningKeys) return FEC_ERR_INVALID_ARG;
     return slots[key]->exchange(value);
 }
@@ -1299,6 +1350,7 @@ int fec_rs_reconstruct_batch(fec_ctx* ctx, int k, int m, size_t shard_len, size_
     if (flags == FEC_DEVICE) {
         if ((rc = check_device_layout(data, data_block_stride, shard_stride, shard_len))) return rc;
         if ((rc = check_device_layout(parity, parity_block_stride, shard_stride, shard_len))) return rc;
+        if ((rc = check_device_words(present_mask, block_status))) return rc;
         return rs_reconstruct_device(ctx, code, shard_len, nblocks, data, data_block_stride, parity,
                                      parity_block_stride, shard_stride, present_mask, block_status, ctx->d_err);
     }
@@ -1325,6 +1377,7 @@ int fec_rs_recover_batch(fec_ctx* ctx, int k, int m, size_t shard_len, size_t nb
     if ((rc = check_device_layout(data, data_block_stride, shard_stride, shard_len))) return rc;
     if ((rc = check_device_layout(parity, parity_block_stride, shard_stride, shard_len))) return rc;
     if ((rc = check_device_layout(out, out_block_stride, shard_stride, shard_len))) return rc;
+    if ((rc = check_device_words(present_mask, block_status))) return rc;
     return rs_reconstruct_device(ctx, code, shard_len, nblocks, const_cast<uint8_t*>(data), data_block_stride,
                                  parity, parity_block_stride, shard_stride, present_mask, block_status, ctx->d_err,
                                  out, out_block_stride, (uint32_t)out_slots);
@@ -1367,6 +1420,7 @@ int fec_xor_reconstruct_batch(fec_ctx* ctx, int k, size_t shard_len, size_t nblo
     if (flags == FEC_DEVICE) {
         if ((rc = check_device_layout(data, data_block_stride, shard_stride, shard_len))) return rc;
         if ((rc = check_device_layout(parity, parity_block_stride, shard_stride, shard_len))) return rc;
+        if ((rc = check_device_words(present_mask, block_status))) return rc;
         return xor_reconstruct_device(ctx, k, shard_len, nblocks, data, data_block_stride, parity,
                                       parity_block_stride, shard_stride, present_mask, block_status, ctx->d_err);
     }

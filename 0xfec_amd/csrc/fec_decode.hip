@@ -193,10 +193,25 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs
     if (i0 >= total) return;
     const uint32_t bfirst = fdiv(i0, a.div_cps);
     const uint32_t nb = fdiv(min(i0 + 63u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
+    // deferred form: records of windows the plan kernel skipped (no multi-erasure block: the direct
+    // kernel did them) are not read; a wave with none in a flagged window exits here
+    uint32_t live = 7u;
+    if (a.wflags) {
+        typedef __attribute__((address_space(4))) const uint32_t ConstU32;
+        ConstU32* wf = (ConstU32*)a.wflags;
+        const uint32_t bf = (uint32_t)__builtin_amdgcn_readfirstlane((int)bfirst);
+        const uint32_t bl = (uint32_t)__builtin_amdgcn_readfirstlane((int)(bfirst + nb - 1));
+        const uint32_t f0 = wf[bf >> 6], f1 = wf[bl >> 6];
+        if (!f0 && !f1) return;
+        live = 0;
+        for (uint32_t g = 0; g < nb; ++g) live |= (((bf + g) >> 6) == (bf >> 6) ? f0 : f1) ? 1u << g : 0u;
+    }
     {
         const uint32_t nw = nb * lay.stride / 16;
         const uint4* src = reinterpret_cast<const uint4*>(a.plans + (uint64_t)bfirst * lay.stride);
         if (lane < nw) reinterpret_cast<uint4*>(plans)[lane] = src[lane];
+        // (LDS writes of one wave land in issue order: the stale record's count is overwritten)
+        if (lane < nb && !((live >> lane) & 1u)) plans[lane * lay.stride + lay.nout_off] = 0;
     }
     wave_sync();
     {

@@ -66,6 +66,25 @@ __device__ __forceinline__ void st16(uint8_t* p, const uint4& v) {
     }
 }
 
+// 16-byte store with cache policy SP (measurement knob st_pol): 0 nt (st16<true>), 1 sc1, 2 sc0 sc1,
+// 3 nt sc1. sc1 / sc0 sc1 stores drop the line from the XCD's L2 (MI355X_MICROARCH.md, stores of
+// each flavour). The asm stores are not in the compiler's wait counts, which no kernel here needs:
+// nothing reads what a kernel stores before the kernel ends.
+template <int SP>
+__device__ __forceinline__ void st16p(uint8_t* p, const uint4& v) {
+    if constexpr (SP == 0) {
+        st16<true>(p, v);
+    } else {
+        const u32x4 w = {v.x, v.y, v.z, v.w};
+        if constexpr (SP == 1)
+            asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 0" ::"v"(p), "v"(w) : "memory");
+        else if constexpr (SP == 2)
+            asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 0" ::"v"(p), "v"(w) : "memory");
+        else
+            asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 0" ::"v"(p), "v"(w) : "memory");
+    }
+}
+
 __device__ __forceinline__ uint32_t word_of(const uint4& v, int d) {
     return d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
 }

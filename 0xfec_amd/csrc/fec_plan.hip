@@ -154,6 +154,9 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
         const uint32_t bn = b + G;
         mask_next = (sg + 1 < segs && bn < a.nblocks) ? a.masks[bn] : 0u;
         const uint32_t wl = sg % win;   // segment within the sort window
+        // deferred form: a window without a multi-erasure block was done by the direct kernel
+        // (workgroup-uniform; its records are not written, and the rebuild skips them too)
+        if (a.wflags && !a.wflags[(base - wl * G) >> 6]) continue;
         // a window's first segment: tables staged (first pass), the previous window's records
         // copied out; within a window a block group's scratch is its own lanes' (wave-local)
         if (wl == 0) __syncthreads();
@@ -166,18 +169,18 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
         if (e != 0) {
             if ((uint32_t)__popc(mask) < k) {
                 st = -4;   // FEC_ERR_TOO_FEW_SHARDS
-                if (gl == 0) wave_flag(a.err, 1);
+                if (gl == 0 && !a.wflags) wave_flag(a.err, 1);
             } else if (a.max_out && e > a.max_out) {
                 st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
                 if (gl == 0) wave_flag(a.err, 2);
             } else {
-                nout = e;
+                nout = e >= a.min_e ? e : 0u;
             }
         }
         if (gl == 0) {
             P[lay.nout_off] = (uint8_t)nout;
             *reinterpret_cast<uint32_t*>(P + lay.blk_off) = b;
-            if (valid && a.status) a.status[b] = st;
+            if (valid && a.status && !a.wflags) a.status[b] = st;
         }
         if (nout) {
             for (uint32_t t = gl; t < n; t += LPB) {

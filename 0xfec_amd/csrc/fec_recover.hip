@@ -52,11 +52,15 @@ struct CoefWords {
 // and one coalesced status store per 64 blocks. (Stored by the waves of each block, the 4-byte
 // statuses of neighbouring blocks were scattered partial-line stores from different waves: RS(2,3)
 // 45 -> 57 us with a status array.)
+// In the deferred form (a.wflags, in place) the same pass writes the window's flag: nonzero when a
+// block of the 64 has two or more erased data shards and enough present ones (its rows come from
+// the sorted plans and the wave rebuild that run after this kernel).
 __device__ __forceinline__ void direct_status_pass(const ReconArgs& a, uint32_t k, uint32_t w, uint32_t lane) {
     if (w * 64u >= a.nblocks) return;   // wave-uniform
     const uint32_t all = low_mask(k + a.m), kmask = low_mask(k);
     const uint32_t b = w * 64u + lane;
     uint32_t bad = 0;
+    bool multi = false;
     if (b < a.nblocks) {
         const uint32_t mask = a.masks[b] & all;
         const uint32_t e = k - __popc(mask & kmask);
@@ -67,11 +71,17 @@ __device__ __forceinline__ void direct_status_pass(const ReconArgs& a, uint32_t 
         } else if (a.max_out && e > a.max_out) {
             st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
             bad = 2;
+        } else {
+            multi = e >= 2;
         }
         if (a.status) a.status[b] = st;
     }
     const bool f1 = __ballot(bad == 1) != 0, f2 = __ballot(bad == 2) != 0;
     if (lane == 0 && (f1 || f2)) atomicOr(a.err, (f1 ? 1 : 0) | (f2 ? 2 : 0));
+    if (a.wflags) {
+        const bool any = __ballot(multi) != 0;
+        if (lane == 0) a.wflags[w] = any ? 1u : 0u;
+    }
 }
 
 // K: compile-time data shard count (0: runtime a.k). TAB: how a wave gets the PermTabs of its
@@ -81,7 +91,7 @@ __device__ __forceinline__ void direct_status_pass(const ReconArgs& a, uint32_t 
 // read from the code's coefficient table in device memory (a.single_coef, through the constant
 // address space: scalar loads), for codes whose rows do not fit the argument (RS(20,30): 1000
 // dwords).
-template <int K, int TAB>
+template <int K, int TAB, int SP = 0>
 __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a, CoefWords cwords) {
     constexpr bool NTL = true, NTS = true;   // non-temporal loads and stores (see launch_rs_recover_direct)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -236,7 +246,9 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
         }
         uint8_t* dst = a.out ? a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk
                              : const_cast<uint8_t*>(dblk) + (uint64_t)E0 * a.ss;
-        store_chunk<NTS>(dst, as_uint4(acc), a.len - c * kChunk);
+        const uint32_t nbytes = a.len - c * kChunk;
+        if constexpr (SP == 0) store_chunk<NTS>(dst, as_uint4(acc), nbytes);
+        else st16p<SP>(dst, nbytes >= 16 ? as_uint4(acc) : keep_bytes(as_uint4(acc), nbytes));
     }
 }
 
@@ -303,7 +315,15 @@ bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, bool single_slot
     return (small || big) && 4 * direct_wave_bytes(k) <= g_max_lds;
 }
 
-template <int K, int TAB>
+bool defer_recon_applies(uint32_t k, uint32_t m, uint32_t cps) {
+    // the sorted plans' sort windows must be the flags' 64 blocks (plan_lanes(k) >= 4: 64 or fewer
+    // blocks per plan segment); RS(16,24) / RS(20,30) keep the sorted-plan route in place (their
+    // rebuild is fec_rebuild.hip's)
+    if (!g_tune.dec_defer || !g_tune.dec_direct || m < 2 || k < 3 || k + m > 32 || cps < 32) return false;
+    return (size_t)k * m * k * sizeof(gf::PermTab) <= kDirectTableBytes && 4 * direct_wave_bytes(k) <= g_max_lds;
+}
+
+template <int K, int TAB, int SP = 0>
 static hipError_t direct_launch(const ReconArgs& a0, const CoefWords& cw, hipStream_t s) {
     const uint64_t total = (uint64_t)a0.nblocks * a0.cps;
     const int flat = (int)((total + kThreads - 1) / kThreads);
@@ -314,7 +334,7 @@ static hipError_t direct_launch(const ReconArgs& a0, const CoefWords& cw, hipStr
     // small codes uncapped
     const int wpc = g_tune.dir_wpc >= 0 ? (int)g_tune.dir_wpc : (a0.k >= 8 ? 3 : 0);
     const size_t lds = occupancy_lds(wpc, 4 * direct_wave_bytes(a0.k));
-    hipLaunchKernelGGL((rs_recover_direct_kernel<K, TAB>), dim3(flat), dim3(kThreads), lds, s, a0, cw);
+    hipLaunchKernelGGL((rs_recover_direct_kernel<K, TAB, SP>), dim3(flat), dim3(kThreads), lds, s, a0, cw);
     return hipGetLastError();
 }
 
@@ -333,6 +353,12 @@ hipError_t launch_rs_recover_direct(const ReconArgs& a, hipStream_t s) {
         e = direct_launch<20, 2>(a, cw, s);
     else if (a.k == 16)
         e = direct_launch<16, 2>(a, cw, s);
+    else if (a.k == 8 && by_arg && g_tune.st_pol == 1)
+        e = direct_launch<8, 1, 1>(a, cw, s);
+    else if (a.k == 8 && by_arg && g_tune.st_pol == 2)
+        e = direct_launch<8, 1, 2>(a, cw, s);
+    else if (a.k == 8 && by_arg && g_tune.st_pol == 3)
+        e = direct_launch<8, 1, 3>(a, cw, s);
     else if (a.k == 8)
         e = by_arg ? direct_launch<8, 1>(a, cw, s) : direct_launch<8, 0>(a, cw, s);
     else if (a.k == 2 && a.m == 1 && by_arg) {

@@ -373,14 +373,27 @@ def best_twin(torch, stream, twin, nbytes, offsets=TWIN_OFFSETS, wpcs=TWIN_WPC):
     """The box's ceiling for an access shape: twin(wpc, off) (a traffic twin at `wpc` resident
     workgroups per CU, output `off` bytes into its buffer) timed at every residency and output
     offset; returns the best TB/s with its (wpc, off) and every rate measured."""
-    rates = {}
+    rates, fns = {}, {}
     for off in offsets:
         for w in wpcs:
-            fn = lambda w=w, off=off: twin(w, off)
-            fn()
-            rates["wpc%d off%d" % (w, off)] = round(nbytes / timed_bursts(torch, stream, fn) / 1e9, 3)
+            key = "wpc%d off%d" % (w, off)
+            fns[key] = lambda w=w, off=off: twin(w, off)
+            fns[key]()
+            rates[key] = round(nbytes / timed_bursts(torch, stream, fns[key]) / 1e9, 3)
     best = max(rates, key=rates.get)
-    return {"probe_best_TBps": rates[best], "probe_best_at": best, "sweep_TBps": rates}
+    best0 = max((kk for kk in rates if kk.endswith(" off0")), key=rates.get)
+    # the max over the sweep's noisy medians reads high: the winner (and the best at offset 0, the
+    # kernels' own output placement) are timed again in fresh interleaved bursts, and those rates
+    # are the ones reported
+    again = {kk: [] for kk in dict.fromkeys((best, best0))}
+    for _ in range(3):
+        for kk in again:
+            again[kk].append(timed_bursts(torch, stream, fns[kk]))
+    re_rate = {kk: round(nbytes / sorted(v)[1] / 1e9, 3) for kk, v in again.items()}
+    return {"probe_best_TBps": re_rate[best], "probe_best_at": best, "probe_best_off0_TBps": re_rate[best0],
+            "probe_best_off0_at": best0, "sweep_TBps": rates,
+            "sweep_note": "probe_best_* re-timed after the sweep in 3 interleaved rounds (median); sweep_TBps "
+                          "holds each setting's first median"}
 
 
 def box_probe(torch, codec, b, step, stream, enc_bytes, dec_bytes, rounds=5, burst=4):

@@ -33,7 +33,9 @@
  * Memory kinds (`flags`):
  *   FEC_DEVICE  pointers are device memory of the ctx's device; shard_stride, block
  *               strides and base pointers must be multiples of 16, every shard slot
- *               (shard_stride bytes) must be readable. The call is asynchronous on the
+ *               (shard_stride bytes) must be readable; present_mask and block_status must be
+ *               4-byte aligned (the kernels read masks by 4-byte scalar loads, which drop the
+ *               low two address bits). The call is asynchronous on the
  *               ctx stream; per-block decode failures are reported through `block_status`
  *               (if given) and, sticky, by fec_sync().
  *   FEC_HOST    pointers are host memory with any layout; the ctx stages the batch
@@ -69,7 +71,8 @@ extern "C" {
 #define FEC_ERR_TOO_FEW_SHARDS (-4)  /* klauspost ErrTooFewShards */
 #define FEC_ERR_SHARD_SIZE (-5)      /* klauspost ErrShardSize */
 #define FEC_ERR_SHARD_NO_DATA (-6)   /* klauspost ErrShardNoData: shard_len == 0 */
-#define FEC_ERR_ALIGNMENT (-7)       /* FEC_DEVICE layout not 16-byte aligned */
+#define FEC_ERR_ALIGNMENT (-7)       /* FEC_DEVICE layout not 16-byte aligned, or a mask / status
+                                        array not 4-byte aligned */
 #define FEC_ERR_HIP (-8)             /* HIP runtime failure */
 #define FEC_ERR_NOMEM (-9)
 #define FEC_ERR_NO_DEVICE (-10)

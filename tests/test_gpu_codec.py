@@ -295,6 +295,11 @@ ENC_VARIANTS = {
     "own_wpc2": dict(enc_fixed=1, enc_wpc=2, enc_bwpc=2),
     "generic": dict(enc_fixed=0),
     "generic_wpc2": dict(enc_fixed=0, gen_wpc=2),
+    "glds104": dict(enc_fixed=1, enc_glds=104),
+    "glds208_wpc2": dict(enc_fixed=1, enc_glds=208, enc_wpc=2),
+    "glds316_wpc1": dict(enc_fixed=1, enc_glds=316, enc_wpc=1),
+    "stpol_sc1": dict(enc_fixed=1, st_pol=1),
+    "stpol_ntsc1": dict(enc_fixed=1, st_pol=3),
 }
 
 
@@ -339,6 +344,8 @@ DEC_VARIANTS = {
     "tile": dict(dec_direct=0, dec_wave=0),
     "table": dict(dec_direct=2),
     "wpc2": dict(dir_wpc=2, dec_wpc=2),
+    "defer": dict(dec_defer=1),
+    "stpol_sc1": dict(st_pol=1),
 }
 
 

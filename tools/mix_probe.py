@@ -2,7 +2,7 @@
 """Diagnostics: mixed read/write HBM rates vs output offset, XCD mapping, occupancy, items per
 lane (tools/mix_probe.hip). Prints one JSON object; rates are bytes moved / time in GB/s.
 
-usage: mix_probe.py [sweep1|sweep2|sweep3|persist|ipl] [--rebuild] [--build-only]"""
+usage: mix_probe.py [sweep1|sweep2|sweep3|persist|ipl|pol] [--rebuild] [--build-only]"""
 import ctypes
 import json
 import os
@@ -128,6 +128,36 @@ def main():
                         acc.setdefault("r%d w%d ipl%d wg%d" % (nin, nout, ipl, w), []).append(
                             run(nin, nout, B, nin * ss, nout * ss, 0, ipl=ipl, swz=1, pad=pad))
         res.update({kk: sorted(v)[1] for kk, v in acc.items()})
+    elif mode == "pol":
+        # store cache policy x residency, interleaved rounds (round 6): decode shape (8 reads + 1
+        # store), encode shape (8 + 4) and reads alone, bench layout
+        lib.mix_pol_probe.argtypes = [vp, vp, sz, sz, sz, u, u, i, i, i, sz, vp]
+        B = 1 << 20
+        pads = {2: 64 << 10, 3: 48 << 10}
+        acc = {}
+
+        def runq(nin, nout, pol, pad, iters=6):
+            fn = lambda: lib.mix_pol_probe(base, base + B * nin * ss, nin * ss, max(1, nout) * ss, ss, cps, B, nin,
+                                           nout, pol, pad, st)
+            if fn() != 0:
+                return None
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(iters):
+                fn()
+            e.record()
+            torch.cuda.synchronize()
+            return round(B * cps * 16 * (nin + nout) / (s.elapsed_time(e) / iters / 1e3) / 1e9, 1)
+        names = {0: "nt", 1: "plain", 2: "sc1", 3: "sc0sc1"}
+        for rnd in range(3):
+            for nin, nout, pols in ((8, 1, (0, 1, 2, 3)), (8, 4, (0, 1, 2, 3)), (8, 0, (0,))):
+                for pol in pols:
+                    for w, pad in pads.items():
+                        acc.setdefault("r%d w%d %s wg%d" % (nin, nout, names[pol], w), []).append(
+                            runq(nin, nout, pol, pad))
+            res.update({kk: sorted(v)[len(v) // 2] for kk, v in acc.items()})
+            flush()
     elif mode == "persist":
         B = 1 << 20
         ctr = torch.zeros(1024, dtype=torch.int32, device="cuda")

@@ -7,7 +7,12 @@ tile route (dec_direct=0, dec_wave=0), interleaved in one process; the outputs o
 compared byte for byte. (Round 5 measured with it the direct kernel + multi-erasure worklist that
 multi-slot calls took before: profiles/r05/mixed_route*_r05g.log.)
 
-usage: mixed_route_probe.py [blocks] [rounds] [--code K,M,MULTI ...] [--routes default,wave]"""
+--inplace times fec_rs_reconstruct_batch (in place) instead, whose default route for these codes is
+the deferred one since round 6 (the direct kernel, then plans and rebuilds of the multi-erasure
+windows only; route "nodefer" is round 5's sorted-plan route for every block). MULTI 0: one random
+data shard lost per block (bench.py's erasures).
+
+usage: mixed_route_probe.py [blocks] [rounds] [--code K,M,MULTI ...] [--routes default,wave] [--inplace]"""
 import importlib
 import json
 import os
@@ -16,7 +21,8 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 L, S = 1202, 1216
-ROUTES = {"default": {}, "wave": {"dec_direct": 0}, "tile": {"dec_direct": 0, "dec_wave": 0}}
+ROUTES = {"default": {}, "wave": {"dec_direct": 0}, "tile": {"dec_direct": 0, "dec_wave": 0},
+          "nodefer": {"dec_defer": 0}, "defer": {"dec_defer": 1}}
 
 
 def main():
@@ -30,6 +36,7 @@ def main():
         i = argv.index("--routes")
         routes = argv[i + 1].split(",")
         del argv[i:i + 2]
+    inplace = "--inplace" in argv
     args = [a for a in argv if not a.startswith("--")]
     B = int(args[0]) if args else 1 << 18
     rounds = int(args[1]) if len(args) > 1 else 5
@@ -45,20 +52,36 @@ def main():
         data = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device="cuda", generator=g)
         par = torch.zeros((B, m, S), dtype=torch.uint8, device="cuda")
         codec.rs_encode_raw(k, m, L, B, data.data_ptr(), k * S, par.data_ptr(), m * S, S, fec.FEC_DEVICE)
-        e = torch.randint(1, multi + 1, (B,), device="cuda", generator=g)
-        rank = torch.rand((B, n), device="cuda", generator=g).argsort(dim=1).argsort(dim=1)
-        lost = rank < e[:, None]
+        if multi:
+            e = torch.randint(1, multi + 1, (B,), device="cuda", generator=g)
+            rank = torch.rand((B, n), device="cuda", generator=g).argsort(dim=1).argsort(dim=1)
+            lost = rank < e[:, None]
+        else:
+            which = torch.randint(0, k, (B,), device="cuda", generator=g)
+            lost = torch.zeros((B, n), dtype=torch.bool, device="cuda")
+            lost[torch.arange(B, device="cuda"), which] = True
         w = torch.bitwise_left_shift(torch.ones(n, dtype=torch.int64, device="cuda"), torch.arange(n, device="cuda"))
         masks = ((~lost).to(torch.int64) * w).sum(dim=1).to(torch.int32)
         e_d = lost[:, :k].sum(dim=1)
         slots = m   # as a caller that does not scan the masks first
         nbytes = int(((k + e_d) * (e_d > 0)).sum().item()) * L
-        outs = {r: torch.zeros((B, slots, S), dtype=torch.uint8, device="cuda") for r in routes}
+        if inplace:
+            # each route rebuilds its own copy with the erased shards wiped; the copies are compared
+            # with the original data (and with each other) afterwards
+            wiped = data.clone()
+            wiped[lost[:, :k]] = 0x3C
+            outs = {r: wiped.clone() for r in routes}
+        else:
+            outs = {r: torch.zeros((B, slots, S), dtype=torch.uint8, device="cuda") for r in routes}
 
         def dec(r):
             def fn():
-                rc = codec.rs_recover_raw(k, m, L, B, data.data_ptr(), k * S, par.data_ptr(), m * S, S,
-                                          masks.data_ptr(), outs[r].data_ptr(), slots * S, slots, None)
+                if inplace:
+                    rc = codec.rs_reconstruct_raw(k, m, L, B, outs[r].data_ptr(), k * S, par.data_ptr(), m * S, S,
+                                                  masks.data_ptr(), None, fec.FEC_DEVICE)
+                else:
+                    rc = codec.rs_recover_raw(k, m, L, B, data.data_ptr(), k * S, par.data_ptr(), m * S, S,
+                                              masks.data_ptr(), outs[r].data_ptr(), slots * S, slots, None)
                 assert rc == 0, rc
             return fn
 
@@ -72,7 +95,9 @@ def main():
             torch.cuda.synchronize()
             return s.elapsed_time(e_) / iters
 
-        name = "RS(%d,%d) U{1..%d}" % (k, n, multi)
+        name = ("RS(%d,%d) U{1..%d}" % (k, n, multi)) if multi else "RS(%d,%d) one data shard" % (k, n)
+        if inplace:
+            name += " in place"
         for _ in range(rounds):
             for r in routes:
                 old = codec.set_tuning(**ROUTES[r])
@@ -80,6 +105,8 @@ def main():
                 codec.set_tuning(**old)
         torch.cuda.synchronize()
         same = all(torch.equal(outs[routes[0]], outs[r]) for r in routes)
+        if inplace:
+            same = same and all(torch.equal(outs[r][:, :, :L], data[:, :, :L]) for r in routes)
         med = {r: round(sorted(v)[len(v) // 2], 4) for r, v in res[name].items()}
         print(json.dumps({"code": name, "blocks": B, "routes_agree": same, "median_ms": med,
                           "TBps": {r: round(nbytes / t / 1e9, 3) for r, t in med.items()}}), flush=True)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Diagnostics: does the headline encode run slower inside bench.py's step than alone?
-enc_select.py times RS(8,12) encode back-to-back at 6.4-6.5 TB/s; the bench step (encode, then
-decode, alternating) sees 6.1. This times, in one process and interleaved over rounds, on the
+Round 4's encode A/Bs (profiles/r04/enc_*_r04*.log) timed RS(8,12) encode back-to-back at
+6.4-6.5 TB/s; the bench step (encode, then decode, alternating) sees 6.1. This times, in one process and interleaved over rounds, on the
 bench's own buffers (bench.RankBatch / RankStep):
   enc x5       encode launches back-to-back
   dec x5       decode launches back-to-back
