@@ -84,7 +84,7 @@ constexpr uint64_t kMaxItems = uint64_t(1) << 31;
 struct Work {
     uint8_t* d_plans = nullptr;
     size_t plans_cap = 0;
-    uint32_t* d_wflags = nullptr;   // deferred in-place decode: one word per 64-block window
+    uint32_t* d_wflags = nullptr;   // routed in-place decode: the classify pass's route word
     size_t wflags_cap = 0;
     void release() {
         if (d_plans) (void)hipFree(d_plans);
@@ -365,15 +365,14 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
     //  * shards of 32+ chunks: sorted plans (fec_plan.hip), then the wave-form rebuild
     //    (fec_rebuild.hip for RS(16,24) / RS(20,30) with 64+ chunks, else fec_decode.hip);
     //  * short shards: plans in block order, then the workgroup-tile rebuild.
-    //  * deferred (in-place calls of the small m >= 2 codes): the direct kernel rebuilds the blocks
-    //    with one erased data shard and flags each 64-block window holding a block with more; the
-    //    sorted plans and the wave rebuild then run over the flagged windows only (their launches
-    //    exit at once on single-erasure batches).
+    //  * routed (in-place calls of RS(8,12)): a classify pass reduces the masks to one word; the
+    //    sorted plans run only if some block has two or more erased data shards, and one kernel
+    //    runs the direct body or the wave rebuild by that word (fec_recover.hip).
     const bool single_slot = out && out_slots == 1;
     const bool direct = code->d_single_coef && fk::direct_recon_applies(k, m, cps, single_slot);
     const bool wave = !direct && fk::wave_recon_applies(cps, k, maxe, lay_sorted.stride);
-    const bool defer = wave && !out && code->d_single_coef && fk::defer_recon_applies(k, m, cps) &&
-                       !fk::rebuild_k_applies(k, maxe, cps);
+    const bool routed = wave && !out && code->d_single_coef && !fk::rebuild_k_applies(k, maxe, cps) &&
+                        fk::routed_recon_applies(k, m, cps, maxe, lay_sorted.stride);
     const fk::PlanLayout lay = wave ? lay_sorted : lay_block;
     size_t per_launch = std::min<size_t>(direct ? nblocks : kPlanBytes / lay.stride, (size_t)(kMaxItems / cps));
     per_launch = std::max<size_t>(1, std::min(per_launch, nblocks));
@@ -381,8 +380,8 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         const int rc = grow_plans(ctx, per_launch * lay.stride);
         if (rc) return rc;
     }
-    if (defer) {
-        const int rc = grow_wflags(ctx, (per_launch + 63) / 64);
+    if (routed) {
+        const int rc = grow_wflags(ctx, 1);
         if (rc) return rc;
     }
     const uint32_t G = fk::pick_tile_blocks(cps, k, maxe, lay);
@@ -421,7 +420,7 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         a.sorted = wave ? 1u : 0u;
         a.out = out ? out + b0 * out_bs : nullptr;
         a.out_bs = out_bs;
-        if (direct || defer) {
+        if (direct || routed) {
             a.masks = p.masks;
             a.status = p.status;
             a.err = p.err;
@@ -434,13 +433,11 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
         }
         if (direct) {
             HIP_TRY(fk::launch_rs_recover_direct(a, ctx->stream));
-        } else if (defer) {
-            a.wflags = ctx->work->d_wflags;
-            HIP_TRY(fk::launch_rs_recover_direct(a, ctx->stream));
-            p.wflags = a.wflags;
-            p.min_e = 2;
+        } else if (routed) {
+            a.route = p.route = ctx->work->d_wflags;
+            HIP_TRY(fk::launch_rs_route_classify(a, ctx->work->d_wflags, ctx->stream));
             HIP_TRY(fk::launch_rs_plan_sorted(p, ctx->stream));
-            HIP_TRY(fk::launch_rs_reconstruct_wave(a, ctx->stream));
+            HIP_TRY(fk::launch_rs_reconstruct_routed(a, ctx->stream));
         } else if (wave) {
             HIP_TRY(fk::launch_rs_plan_sorted(p, ctx->stream));
             if (fk::rebuild_k_applies(k, maxe, cps)) HIP_TRY(fk::launch_rs_rebuild_k(a, ctx->stream));
@@ -1219,7 +1216,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
     std::atomic<int>* slots[fk::kTuningKeys] = {&t.enc_wpc,   &t.gen_wpc,    &t.dec_wpc,      &t.dir_wpc,
                                                 &t.enc_bwpc,  &t.enc_fixed,  &t.dec_wave,     &t.dec_direct,
                                                 &t.host_chunk, &t.host_threads, &t.bat_zc,     &t.enc_glds,
-                                                &t.dec_defer,  &t.st_pol};
+                                                &t.dec_route,  &t.st_pol,     &t.dec_lpad,     &t.dst_pol,
+                                                &t.route_wpc};
     if (key < 0 || key >= fk::kTuningKeys) return FEC_ERR_INVALID_ARG;
     return slots[key]->exchange(value);
 }

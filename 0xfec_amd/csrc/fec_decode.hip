@@ -175,72 +175,12 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
     }
 }
 
-// Wave form (shards of 32+ chunks): one wave per 64 consecutive items of the sorted plan order; the
-// wave stages its <= 3 blocks' records and the PermTabs of the rows they rebuild in a wave-private
-// LDS slice (no workgroup barrier), one item per lane. K: compile-time data shard count (0: runtime
-// a.k), all K input loads in flight before the first is folded (recon_item_k).
+// Wave form (shards of 32+ chunks): one wave per 64 consecutive items of the sorted plan order
+// (the body, wave_body, is in fec_recon.hpp).
 template <int MAXE, int K = 0>
 __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t k = a.k, maxe = a.maxe;
-    const PlanLayout lay = a.lay;
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    uint8_t* slice = smem + (size_t)wave * wave_slice_bytes(k, maxe, lay.stride);
-    gf::PermTab* tabs = reinterpret_cast<gf::PermTab*>(slice);                     // 3*maxe*k
-    uint8_t* plans = slice + (size_t)kWaveBlocks * maxe * k * sizeof(gf::PermTab);  // 3*stride
-    const uint32_t total = a.nblocks * a.cps;
-    const uint32_t i0 = xcd_order() * kThreads + (wave << 6);
-    if (i0 >= total) return;
-    const uint32_t bfirst = fdiv(i0, a.div_cps);
-    const uint32_t nb = fdiv(min(i0 + 63u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
-    // deferred form: records of windows the plan kernel skipped (no multi-erasure block: the direct
-    // kernel did them) are not read; a wave with none in a flagged window exits here
-    uint32_t live = 7u;
-    if (a.wflags) {
-        typedef __attribute__((address_space(4))) const uint32_t ConstU32;
-        ConstU32* wf = (ConstU32*)a.wflags;
-        const uint32_t bf = (uint32_t)__builtin_amdgcn_readfirstlane((int)bfirst);
-        const uint32_t bl = (uint32_t)__builtin_amdgcn_readfirstlane((int)(bfirst + nb - 1));
-        const uint32_t f0 = wf[bf >> 6], f1 = wf[bl >> 6];
-        if (!f0 && !f1) return;
-        live = 0;
-        for (uint32_t g = 0; g < nb; ++g) live |= (((bf + g) >> 6) == (bf >> 6) ? f0 : f1) ? 1u << g : 0u;
-    }
-    {
-        const uint32_t nw = nb * lay.stride / 16;
-        const uint4* src = reinterpret_cast<const uint4*>(a.plans + (uint64_t)bfirst * lay.stride);
-        if (lane < nw) reinterpret_cast<uint4*>(plans)[lane] = src[lane];
-        // (LDS writes of one wave land in issue order: the stale record's count is overwritten)
-        if (lane < nb && !((live >> lane) & 1u)) plans[lane * lay.stride + lay.nout_off] = 0;
-    }
-    wave_sync();
-    {
-        // expand only the rows the blocks rebuild: entry i of c0 + c1 + c2 (c_g = nout_g * k)
-        const uint32_t c0 = plans[lay.nout_off] * k;
-        const uint32_t c1 = nb > 1 ? plans[lay.stride + lay.nout_off] * k : 0u;
-        const uint32_t c2 = nb > 2 ? plans[2 * lay.stride + lay.nout_off] * k : 0u;
-        const uint32_t kk = K > 0 ? (uint32_t)K : k;   // compile-time k: the division is a shift
-        for (uint32_t i = lane; i < c0 + c1 + c2; i += 64) {
-            const uint32_t g = (i >= c0) + (i >= c0 + c1);
-            const uint32_t rem = i - (g == 0 ? 0u : g == 1 ? c0 : c0 + c1);
-            const uint32_t r = rem / kk, j = rem - r * kk;
-            const uint8_t* P = plans + g * lay.stride;
-            tabs[g * maxe * k + rem] = gf::make_permtab_fast(P[lay.coef_off + r * k + j]);
-        }
-    }
-    wave_sync();
-    const uint32_t item = i0 + lane;
-    const bool inr = item < total;
-    const uint32_t blk = inr ? fdiv(item, a.div_cps) : bfirst;
-    const uint32_t g = blk - bfirst;
-    const uint32_t c = item - blk * a.cps;
-    const uint8_t* P = plans + g * lay.stride;
-    const uint32_t nout = inr ? P[lay.nout_off] : 0;
-    const uint32_t rows = wave_rows<MAXE>(nout);
-    if (nout == 0) return;
-    const uint32_t rb = a.sorted ? *reinterpret_cast<const uint32_t*>(P + lay.blk_off) : blk;
-    if constexpr (K > 0) recon_item_k<K, MAXE>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
-    else recon_item<MAXE>(a, P, tabs + g * maxe * k, rb, c, rows, nout);
+    wave_body<MAXE, K>(a, smem);
 }
 
 hipError_t launch_rs_plan(const PlanArgs& a, hipStream_t s) {

@@ -59,12 +59,9 @@ struct PlanArgs {
     PlanLayout lay;
     uint32_t max_out;          // recover: output slots per block (0: in place, unlimited)
     const uint8_t* dall;       // sorted plans: per shard index s < n, sum_{t < n, t != s} log(s ^ t) mod 255
-    // deferred form (in-place calls after the direct kernel, fec_recover.hip): one word per 64-block
-    // window, nonzero where a block has two or more erased data shards; windows without one are
-    // skipped (no records written), and blocks with fewer than min_e erasures get no rows. Statuses
-    // and error flags are then the direct kernel's.
-    const uint32_t* wflags;
-    uint32_t min_e;
+    // routed in-place form (fec_recover.hip): the classify pass's word; zero (no block needs more than
+    // the direct body) makes the plan kernel exit at once (null: always plan)
+    const uint32_t* route;
 };
 
 // Sorted plans (fec_plan.hip): lanes per block and blocks per 256-thread workgroup for k.
@@ -101,10 +98,10 @@ struct ReconArgs {
     const uint32_t* single;
     const uint32_t* single_coef;   // the same plans' coefficient bytes: (k*m) rows of ceil(k/4) dwords
     const uint32_t* single_coef_host;   // host copy of single_coef (passed as a kernel argument when small)
-    // deferred form (in place, m >= 2): the direct kernel rebuilds the single-erasure blocks and sets
-    // wflags[w] for each 64-block window holding a block with more erased data shards; the sorted
-    // plans and the wave rebuild then run over those windows only (null: off)
-    uint32_t* wflags;
+    // routed in-place form (fec_recover.hip rs_reconstruct_routed_kernel): the classify pass's word,
+    // zero when no recoverable block has two or more erased data shards (the direct body runs), else
+    // nonzero (the wave rebuild of the sorted plans runs)
+    const uint32_t* route;
 };
 
 
@@ -150,14 +147,19 @@ struct Tuning {
     // RS(8,12) encode by the LDS-DMA ring kernel (fec_encode.hip): 0 off, else D * 100 + T (+ 1000: the
     // twin body, measurement only)
     std::atomic<int> enc_glds{0};
-    // in-place reconstructs of the small m >= 2 codes: direct kernel first, plans and rebuilds of the
-    // multi-erasure windows after it (fec_recover.hip); 0: the sorted-plan route for every block
-    std::atomic<int> dec_defer{0};
-    // store cache policy of the RS(8,12) encode and direct decode (fec_device.hpp st16p): 0 nt, 1 sc1,
-    // 2 sc0 sc1, 3 nt sc1
-    std::atomic<int> st_pol{0};
+    // in-place reconstructs of RS(8,12): routed by a classify pass between the direct body and the
+    // sorted plans (fec_recover.hip); 0: the sorted-plan route for every batch
+    std::atomic<int> dec_route{1};
+    // store cache policy of the RS(8,12) encode (st_pol) and direct decode (dst_pol) (fec_device.hpp
+    // st16p): 0 nt, 1 sc1, 2 sc0 sc1, 3 nt sc1
+    std::atomic<int> st_pol{1};
+    // RS(16,24) / RS(20,30) rebuild: the second block's table rows 4 banks on (fec_rebuild.hip Slice)
+    std::atomic<int> dec_lpad{0};
+    std::atomic<int> dst_pol{3};
+    // resident workgroups per CU of the routed in-place kernel (-1: the direct kernel's, dir_wpc)
+    std::atomic<int> route_wpc{-1};
 };
-constexpr int kTuningKeys = 14;   // fec__set_tuning keys 0..13, in the order above
+constexpr int kTuningKeys = 17;   // fec__set_tuning keys 0..16, in the order above
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):
 // halfway between 160K/(wpc+1) and 160K/wpc, never below what the kernel itself needs.
@@ -195,9 +197,12 @@ bool rebuild_k_applies(uint32_t k, uint32_t maxe, uint32_t cps);
 hipError_t launch_rs_rebuild_k(const ReconArgs& a, hipStream_t s);
 // Direct form (fec_recover.hip): applies when the single-erasure tables of (k, m) fit in LDS.
 bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, bool single_slot);
-// The deferred in-place form (direct kernel + sorted plans and wave rebuild of the multi-erasure
-// windows): small codes with m >= 2 whose plan sort windows are 64 blocks.
-bool defer_recon_applies(uint32_t k, uint32_t m, uint32_t cps);
+// The routed in-place form (fec_recover.hip): RS(8,12)-shaped codes in place, classify pass ->
+// route word -> sorted plans (skipped on a zero word) -> one routed kernel (the direct body on a
+// zero word, the wave rebuild otherwise).
+bool routed_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t maxe, uint32_t stride);
+hipError_t launch_rs_route_classify(const ReconArgs& a, uint32_t* route, hipStream_t s);
+hipError_t launch_rs_reconstruct_routed(const ReconArgs& a, hipStream_t s);
 size_t direct_table_words(uint32_t k, uint32_t m);
 hipError_t launch_rs_recover_direct(const ReconArgs& a, hipStream_t s);
 hipError_t launch_xor_encode(const XorArgs& a, int grid, hipStream_t s);

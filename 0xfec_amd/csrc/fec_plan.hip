@@ -111,10 +111,17 @@ __device__ __forceinline__ void sort_window_out(const PlanArgs& a, uint8_t* smem
     }
 }
 
+// The routed in-place form's word (fec_recover.hip): zero, no block needs a plan (workgroup-uniform).
+__device__ __forceinline__ bool route_skips(const PlanArgs& a) {
+    typedef __attribute__((address_space(4))) const uint32_t ConstU32;
+    return a.route && *(ConstU32*)a.route == 0;
+}
+
 template <uint32_t LPB>
 __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanArgs a, uint32_t segs, uint32_t win) {
     constexpr uint32_t G = kPlanSortThreads / LPB;   // blocks per workgroup segment
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (route_skips(a)) return;
     const PlanLayout lay = a.lay;
     const SortLds L = sort_lds(a.m, a.k, G, lay.stride, win);
     uint8_t* s_exp = smem + kV2Exp;
@@ -154,9 +161,6 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
         const uint32_t bn = b + G;
         mask_next = (sg + 1 < segs && bn < a.nblocks) ? a.masks[bn] : 0u;
         const uint32_t wl = sg % win;   // segment within the sort window
-        // deferred form: a window without a multi-erasure block was done by the direct kernel
-        // (workgroup-uniform; its records are not written, and the rebuild skips them too)
-        if (a.wflags && !a.wflags[(base - wl * G) >> 6]) continue;
         // a window's first segment: tables staged (first pass), the previous window's records
         // copied out; within a window a block group's scratch is its own lanes' (wave-local)
         if (wl == 0) __syncthreads();
@@ -169,18 +173,18 @@ __global__ __launch_bounds__(kPlanSortThreads) void rs_plan_sorted_kernel(PlanAr
         if (e != 0) {
             if ((uint32_t)__popc(mask) < k) {
                 st = -4;   // FEC_ERR_TOO_FEW_SHARDS
-                if (gl == 0 && !a.wflags) wave_flag(a.err, 1);
+                if (gl == 0) wave_flag(a.err, 1);
             } else if (a.max_out && e > a.max_out) {
                 st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
                 if (gl == 0) wave_flag(a.err, 2);
             } else {
-                nout = e >= a.min_e ? e : 0u;
+                nout = e;
             }
         }
         if (gl == 0) {
             P[lay.nout_off] = (uint8_t)nout;
             *reinterpret_cast<uint32_t*>(P + lay.blk_off) = b;
-            if (valid && a.status && !a.wflags) a.status[b] = st;
+            if (valid && a.status) a.status[b] = st;
         }
         if (nout) {
             for (uint32_t t = gl; t < n; t += LPB) {

@@ -20,6 +20,8 @@
 // gained only 2.4 % over it (round 5, profiles/r05/mixed_route_*_r05g.log).
 #include <string.h>
 
+#include <algorithm>
+
 #include "fec_recon.hpp"
 
 namespace fk {
@@ -52,15 +54,11 @@ struct CoefWords {
 // and one coalesced status store per 64 blocks. (Stored by the waves of each block, the 4-byte
 // statuses of neighbouring blocks were scattered partial-line stores from different waves: RS(2,3)
 // 45 -> 57 us with a status array.)
-// In the deferred form (a.wflags, in place) the same pass writes the window's flag: nonzero when a
-// block of the 64 has two or more erased data shards and enough present ones (its rows come from
-// the sorted plans and the wave rebuild that run after this kernel).
 __device__ __forceinline__ void direct_status_pass(const ReconArgs& a, uint32_t k, uint32_t w, uint32_t lane) {
     if (w * 64u >= a.nblocks) return;   // wave-uniform
     const uint32_t all = low_mask(k + a.m), kmask = low_mask(k);
     const uint32_t b = w * 64u + lane;
     uint32_t bad = 0;
-    bool multi = false;
     if (b < a.nblocks) {
         const uint32_t mask = a.masks[b] & all;
         const uint32_t e = k - __popc(mask & kmask);
@@ -71,17 +69,11 @@ __device__ __forceinline__ void direct_status_pass(const ReconArgs& a, uint32_t 
         } else if (a.max_out && e > a.max_out) {
             st = -1;   // FEC_ERR_INVALID_ARG: more erasures than output slots
             bad = 2;
-        } else {
-            multi = e >= 2;
         }
         if (a.status) a.status[b] = st;
     }
     const bool f1 = __ballot(bad == 1) != 0, f2 = __ballot(bad == 2) != 0;
     if (lane == 0 && (f1 || f2)) atomicOr(a.err, (f1 ? 1 : 0) | (f2 ? 2 : 0));
-    if (a.wflags) {
-        const bool any = __ballot(multi) != 0;
-        if (lane == 0) a.wflags[w] = any ? 1u : 0u;
-    }
 }
 
 // K: compile-time data shard count (0: runtime a.k). TAB: how a wave gets the PermTabs of its
@@ -92,9 +84,8 @@ __device__ __forceinline__ void direct_status_pass(const ReconArgs& a, uint32_t 
 // address space: scalar loads), for codes whose rows do not fit the argument (RS(20,30): 1000
 // dwords).
 template <int K, int TAB, int SP = 0>
-__global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a, CoefWords cwords) {
+__device__ __forceinline__ void direct_body(const ReconArgs& a, const CoefWords& cwords, uint8_t* smem) {
     constexpr bool NTL = true, NTS = true;   // non-temporal loads and stores (see launch_rs_recover_direct)
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     {
         const uint32_t vb = blockIdx.x;
         const uint32_t k = K ? (uint32_t)K : a.k, m = a.m;
@@ -118,14 +109,20 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
 
         // Per block (uniform): the table row (E0 * m + R0) of a single-erasure block.
         uint32_t row[kWaveBlocks] = {0, 0, 0};
+        bool any = false;
     #pragma unroll
         for (uint32_t g = 0; g < kWaveBlocks; ++g) {
             if (g >= nb) break;
             const uint32_t mask = mask_of(g) & all;
             const uint32_t e = k - __popc(mask & kmask);
-            if (e == 1 && (uint32_t)__popc(mask) >= k && !(a.max_out && e > a.max_out))
+            if (e == 1 && (uint32_t)__popc(mask) >= k && !(a.max_out && e > a.max_out)) {
                 row[g] = (__ffs(~mask & kmask) - 1) * m + (__ffs(mask >> k) - 1);   // m >= 1 here: k < 32
+                any = true;
+            }
         }
+        // a wave none of whose blocks has one erased data shard (nothing erased, or failed) issues
+        // no loads (wave-uniform: the masks are scalar)
+        if (!any) return;
         // The PermTab rows of the wave's blocks into its LDS slice, prepared while the data loads are
         // in flight (vector loads return in order: LDS writes that wait for a row load wait for that
         // load only, and scalar loads are counted apart).
@@ -252,6 +249,46 @@ __global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a
     }
 }
 
+template <int K, int TAB, int SP = 0>
+__global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a, CoefWords cwords) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    direct_body<K, TAB, SP>(a, cwords, smem);
+}
+
+// ------------------------------------------------------------------ routed in-place reconstruct
+// In-place calls (fec_rs_reconstruct_batch) of RS(8,12) cannot know before the kernels run whether
+// a block has two or more erased data shards: the masks are device memory. A classify pass reduces
+// the masks to one word (route: nonzero if some recoverable block has >= 2 erased data shards); the
+// sorted plan kernel then exits at once when it is zero, and this kernel runs the direct
+// single-erasure body (no plan records) when it is zero and the wave rebuild of the sorted plans
+// when it is not: one launch of the flat grid either way, no empty grid on either route.
+// One workgroup per CU sweeps the masks; a workgroup that finds such a block sets the word with one
+// atomic (an atomic per wave on one address, 8192 of them on a mixed 2^20-block batch, serialised
+// at L2 for ~90 us).
+__global__ __launch_bounds__(256) void rs_route_classify_kernel(const uint32_t* masks, uint32_t nblocks, uint32_t k,
+                                                                 uint32_t m, uint32_t* route) {
+    __shared__ uint32_t found;
+    if (threadIdx.x == 0) found = 0;
+    __syncthreads();
+    const uint32_t all = low_mask(k + m), kmask = low_mask(k);
+    bool multi = false;
+    for (uint32_t b = blockIdx.x * 256u + threadIdx.x; b < nblocks; b += gridDim.x * 256u) {
+        const uint32_t mask = masks[b] & all;
+        multi |= k - __popc(mask & kmask) >= 2 && (uint32_t)__popc(mask) >= k;
+    }
+    if (__ballot(multi) != 0 && __lane_id() == 0) found = 1;   // plain LDS store: any writer wins
+    __syncthreads();
+    if (threadIdx.x == 0 && found) atomicOr(route, 1u);
+}
+
+template <int MAXE, int DK, int TAB, int SP>
+__global__ __launch_bounds__(kThreads) void rs_reconstruct_routed_kernel(ReconArgs a, CoefWords cwords) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    typedef __attribute__((address_space(4))) const uint32_t ConstU32;
+    if (*(ConstU32*)a.route == 0) direct_body<DK, TAB, SP>(a, cwords, smem);
+    else wave_body<MAXE, 0>(a, smem);
+}
+
 // RS(2,3) (k = 2, m = 1): a block is rebuilt from its other data shard and the parity with the
 // two coefficients of its erased shard's row, x_E0 = c[E0][0] * x_other ^ c[E0][1] * p. Both rows'
 // PermTabs (4 x 32 bytes) arrive as a kernel argument, so a lane picks its row's words from scalar
@@ -315,12 +352,44 @@ bool direct_recon_applies(uint32_t k, uint32_t m, uint32_t cps, bool single_slot
     return (small || big) && 4 * direct_wave_bytes(k) <= g_max_lds;
 }
 
-bool defer_recon_applies(uint32_t k, uint32_t m, uint32_t cps) {
-    // the sorted plans' sort windows must be the flags' 64 blocks (plan_lanes(k) >= 4: 64 or fewer
-    // blocks per plan segment); RS(16,24) / RS(20,30) keep the sorted-plan route in place (their
-    // rebuild is fec_rebuild.hip's)
-    if (!g_tune.dec_defer || !g_tune.dec_direct || m < 2 || k < 3 || k + m > 32 || cps < 32) return false;
-    return (size_t)k * m * k * sizeof(gf::PermTab) <= kDirectTableBytes && 4 * direct_wave_bytes(k) <= g_max_lds;
+bool routed_recon_applies(uint32_t k, uint32_t m, uint32_t cps, uint32_t maxe, uint32_t stride) {
+    // RS(8,12)-shaped codes in place (the headline code: the direct body with k at compile time and
+    // its rows from the kernel argument), when the wave rebuild serves their plan route
+    return g_tune.dec_route && g_tune.dec_direct == 1 && k == 8 && m >= 2 && maxe <= 8 &&
+           (size_t)k * m * ((k + 3) / 4) <= kCoefWords && (size_t)k * m * k * sizeof(gf::PermTab) <= kDirectTableBytes &&
+           wave_recon_applies(cps, k, maxe, stride);
+}
+
+hipError_t launch_rs_route_classify(const ReconArgs& a, uint32_t* route, hipStream_t s) {
+    if (a.nblocks == 0) return hipSuccess;
+    if (hipMemsetAsync(route, 0, 4, s) != hipSuccess) return hipGetLastError();
+    const int grid = (int)std::min<uint64_t>(256, ((uint64_t)a.nblocks + 255) / 256);
+    hipLaunchKernelGGL(rs_route_classify_kernel, dim3(grid), dim3(256), 0, s, a.masks, a.nblocks, a.k, a.m, route);
+    return hipGetLastError();
+}
+
+hipError_t launch_rs_reconstruct_routed(const ReconArgs& a, hipStream_t s) {
+    const uint64_t total = (uint64_t)a.nblocks * a.cps;
+    const int flat = (int)((total + kThreads - 1) / kThreads);
+    if (flat == 0) return hipSuccess;
+    CoefWords cw{};
+    memcpy(cw.w, a.single_coef_host, (size_t)a.k * a.m * ((a.k + 3) / 4) * 4);
+    // residency: knob route_wpc, else the direct kernel's (dir_wpc; 3 for k >= 8)
+    const int wpc = g_tune.route_wpc >= 0 ? (int)g_tune.route_wpc : g_tune.dir_wpc >= 0 ? (int)g_tune.dir_wpc : 3;
+    const size_t own = std::max(4 * direct_wave_bytes(a.k), 4 * wave_slice_bytes(a.k, a.maxe, a.lay.stride));
+    const size_t lds = occupancy_lds(wpc, own);
+    const bool sp3 = g_tune.dst_pol == 3;
+#define FEC_ROUTED(MAXE, SP) \
+    hipLaunchKernelGGL((rs_reconstruct_routed_kernel<MAXE, 8, 1, SP>), dim3(flat), dim3(kThreads), lds, s, a, cw)
+    if (a.maxe <= 4) {
+        if (sp3) FEC_ROUTED(4, 3);
+        else FEC_ROUTED(4, 0);
+    } else {
+        if (sp3) FEC_ROUTED(8, 3);
+        else FEC_ROUTED(8, 0);
+    }
+#undef FEC_ROUTED
+    return hipGetLastError();
 }
 
 template <int K, int TAB, int SP = 0>
@@ -353,11 +422,11 @@ hipError_t launch_rs_recover_direct(const ReconArgs& a, hipStream_t s) {
         e = direct_launch<20, 2>(a, cw, s);
     else if (a.k == 16)
         e = direct_launch<16, 2>(a, cw, s);
-    else if (a.k == 8 && by_arg && g_tune.st_pol == 1)
+    else if (a.k == 8 && by_arg && g_tune.dst_pol == 1)
         e = direct_launch<8, 1, 1>(a, cw, s);
-    else if (a.k == 8 && by_arg && g_tune.st_pol == 2)
+    else if (a.k == 8 && by_arg && g_tune.dst_pol == 2)
         e = direct_launch<8, 1, 2>(a, cw, s);
-    else if (a.k == 8 && by_arg && g_tune.st_pol == 3)
+    else if (a.k == 8 && by_arg && g_tune.dst_pol == 3)
         e = direct_launch<8, 1, 3>(a, cw, s);
     else if (a.k == 8)
         e = by_arg ? direct_launch<8, 1>(a, cw, s) : direct_launch<8, 0>(a, cw, s);

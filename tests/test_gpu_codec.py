@@ -298,8 +298,7 @@ ENC_VARIANTS = {
     "glds104": dict(enc_fixed=1, enc_glds=104),
     "glds208_wpc2": dict(enc_fixed=1, enc_glds=208, enc_wpc=2),
     "glds316_wpc1": dict(enc_fixed=1, enc_glds=316, enc_wpc=1),
-    "stpol_sc1": dict(enc_fixed=1, st_pol=1),
-    "stpol_ntsc1": dict(enc_fixed=1, st_pol=3),
+    "stpol_nt": dict(enc_fixed=1, st_pol=0),
 }
 
 
@@ -344,8 +343,9 @@ DEC_VARIANTS = {
     "tile": dict(dec_direct=0, dec_wave=0),
     "table": dict(dec_direct=2),
     "wpc2": dict(dir_wpc=2, dec_wpc=2),
-    "defer": dict(dec_defer=1),
-    "stpol_sc1": dict(st_pol=1),
+    "noroute": dict(dec_route=0),
+    "dstpol_nt": dict(dst_pol=0),
+    "lpad": dict(dec_lpad=1),
 }
 
 

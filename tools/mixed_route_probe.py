@@ -7,9 +7,9 @@ tile route (dec_direct=0, dec_wave=0), interleaved in one process; the outputs o
 compared byte for byte. (Round 5 measured with it the direct kernel + multi-erasure worklist that
 multi-slot calls took before: profiles/r05/mixed_route*_r05g.log.)
 
---inplace times fec_rs_reconstruct_batch (in place) instead, whose default route for these codes is
-the deferred one since round 6 (the direct kernel, then plans and rebuilds of the multi-erasure
-windows only; route "nodefer" is round 5's sorted-plan route for every block). MULTI 0: one random
+--inplace times fec_rs_reconstruct_batch (in place) instead, whose default route for RS(8,12) is the
+routed one since round 6 (a classify pass, then the direct body or the sorted plans + wave rebuild
+in one kernel; route "noroute" is round 5's sorted-plan route for every batch). MULTI 0: one random
 data shard lost per block (bench.py's erasures).
 
 usage: mixed_route_probe.py [blocks] [rounds] [--code K,M,MULTI ...] [--routes default,wave] [--inplace]"""
@@ -22,7 +22,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 L, S = 1202, 1216
 ROUTES = {"default": {}, "wave": {"dec_direct": 0}, "tile": {"dec_direct": 0, "dec_wave": 0},
-          "nodefer": {"dec_defer": 0}, "defer": {"dec_defer": 1}}
+          "noroute": {"dec_route": 0}, "route_wpc3": {"route_wpc": 3},
+          "route_wpc4": {"route_wpc": 4}, "route_wpc5": {"route_wpc": 5}, "route_wpc0": {"route_wpc": 0}}
 
 
 def main():
