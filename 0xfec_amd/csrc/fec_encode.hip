@@ -129,11 +129,6 @@ __device__ __forceinline__ void dy_conv(const Idx (*D)[NC], const gf::PermTab* T
     }
 }
 
-// ------------------------------------------------------------------ RS encode, fixed shape
-// RS(8,12), the headline code, with K and M compile-time and the dyadic body: one lane = one
-// 16-byte column chunk, the K loads issued back to back, no runtime guards; the workgroup stages
-// the leaf tables (dyadic_leaves(), fec_capi.cpp) in LDS. Non-temporal loads and stores. Tail
-// chunks are stored whole with the pad bytes zeroed.
 // The dyadic body: the M parity chunks of one 16-byte column from its K data chunks, the leaf
 // tables at `tabs` (LDS).
 template <int K, int M>
@@ -171,6 +166,15 @@ __device__ __forceinline__ void dy_encode_chunk(const uint4 (&x)[K], const uint8
     }
 }
 
+// ------------------------------------------------------------------ RS encode, fixed shape
+// RS(8,12), the headline code, with K and M compile-time and the dyadic body: one lane = one
+// 16-byte column chunk, the K loads issued back to back, no runtime guards; the workgroup stages
+// the leaf tables (dyadic_leaves(), fec_capi.cpp) in LDS. Non-temporal loads; stores by policy SP
+// (fec_device.hpp st16p; the launch's default sc1). Tail chunks are stored whole with the pad
+// bytes zeroed. (Round 6 measured a form with its loads decoupled from its arithmetic, each wave
+// walking T tiles with the next D tiles' shard chunks in flight as LDS-DMA loads into a ring:
+// 7-17 % slower than this flat grid at every residency, its traffic twin 7.5-9 % below the flat
+// twin; DESIGN.md 3, the kernel is in commit f1dd58a.)
 template <int K, int M, int SP = 0>
 __global__ __launch_bounds__(kThreads) void rs_encode_fixed_kernel(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -193,168 +197,6 @@ __global__ __launch_bounds__(kThreads) void rs_encode_fixed_kernel(EncodeArgs a)
     const uint32_t nb = min(a.len - c * kChunk, (uint32_t)kChunk);
 #pragma unroll
     for (int r = 0; r < M; ++r) st16p<SP>(dst + (uint64_t)r * a.ss, keep_bytes(as_uint4(acc[r]), nb));
-}
-
-// ------------------------------------------------------------------ RS encode, LDS-DMA ring
-// The fixed-shape encode with its loads decoupled from its arithmetic: each wave walks T tiles of
-// 64 items (tile q of its workgroup's 4T, then q + 4, ...) and keeps the next D tiles' K shard
-// chunks in flight as LDS-DMA loads (global_load_lds_dwordx4, non-temporal) into a D-slot ring of
-// its own (K KiB per slot: lane l's chunk of shard j at slot + 1024 j + 16 l), so the field
-// arithmetic of one tile runs while the loads of the next ones land, at a residency where the
-// flat grid's waves could not hide it. Every load and store is unconditional (a lane past the
-// batch re-codes its last item: the same bytes to the same place), so the kernel knows at compile
-// time how many vector-memory operations follow each tile's loads and waits for exactly those
-// (vmcnt counts loads and stores in issue order). TWIN: the XOR of the inputs in place of the
-// products, the access shape alone (measurement only).
-//
-// The LDS-DMA is inline asm: the compiler's own wait-count bookkeeping makes every LDS read wait
-// for all outstanding LDS-DMA it cannot tell apart, which would drain the ring at each tile.
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-__device__ __forceinline__ void glds16_nt(const uint8_t* gsrc, uint32_t lds) {
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(gsrc), "s"(lds)
-        : "memory");
-}
-
-// Vector-memory operations issued after tile t's K loads and before step t waits for them.
-// Program order: the prologue's loads of tiles 0..min(D, T)-1; step s: wait, loads of tile s + D
-// (if s + D < T), M stores of tile s.
-constexpr int glds_after(int K, int M, int D, int T, int t) {
-    int cnt = 0;
-    bool after = false;
-    for (int u = 0; u < (D < T ? D : T); ++u) {
-        if (after) cnt += K;
-        if (u == t) after = true;
-    }
-    for (int s = 0; s < t; ++s) {
-        if (s + D < T) {
-            if (after) cnt += K;
-            if (s + D == t) after = true;
-        }
-        if (after) cnt += M;
-    }
-    return cnt;
-}
-
-struct GldsItem {
-    const uint8_t* src;
-    uint8_t* dst;
-    uint32_t nb;
-};
-__device__ __forceinline__ GldsItem glds_item(const EncodeArgs& a, uint32_t tile, uint32_t lane) {
-    const uint32_t it = min(tile * 64u + lane, a.total - 1u);
-    const uint32_t b = fdiv(it, a.div_cps);
-    const uint32_t c = it - b * a.cps;
-    return {a.in + (uint64_t)b * a.in_bs + (uint64_t)c * kChunk, a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk,
-            min(a.len - c * kChunk, (uint32_t)kChunk)};
-}
-
-template <int K>
-__device__ __forceinline__ void glds_issue(const EncodeArgs& a, uint32_t slot, uint32_t tile, uint32_t lane) {
-    const uint8_t* src = glds_item(a, tile, lane).src;
-#pragma unroll
-    for (int j = 0; j < K; ++j) glds16_nt(src + (uint64_t)j * a.ss, slot + (uint32_t)j * 64u * kChunk);
-}
-
-template <int K, int M, int D, int T, bool TWIN, int t>
-__device__ __forceinline__ void glds_step(const EncodeArgs& a, const uint8_t* smem, const uint8_t* wring,
-                                          uint32_t ring, uint32_t tile0, uint32_t ts, uint32_t lane) {
-    if constexpr (t < T) {
-        constexpr uint32_t kSlot = K * 64 * kChunk;
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(glds_after(K, M, D, T, t)) : "memory");
-        uint4 x[K];
-        const uint8_t* sl = wring + (t % D) * kSlot + lane * kChunk;
-#pragma unroll
-        for (int j = 0; j < K; ++j) x[j] = *reinterpret_cast<const uint4*>(sl + j * 64 * kChunk);
-        if constexpr (t + D < T) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot is read before it is refilled
-            glds_issue<K>(a, ring + (t % D) * kSlot, tile0 + ts * (t + D), lane);
-        }
-        uint32_t acc[M][4];
-        if constexpr (TWIN) {
-#pragma unroll
-            for (int r = 0; r < M; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0;
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                acc[j % M][0] ^= x[j].x;
-                acc[j % M][1] ^= x[j].y;
-                acc[j % M][2] ^= x[j].z;
-                acc[j % M][3] ^= x[j].w;
-            }
-        } else {
-            dy_encode_chunk<K, M>(x, smem, acc);
-        }
-        const GldsItem g = glds_item(a, tile0 + ts * t, lane);
-#pragma unroll
-        for (int r = 0; r < M; ++r) st16<true>(g.dst + (uint64_t)r * a.ss, keep_bytes(as_uint4(acc[r]), g.nb));
-        glds_step<K, M, D, T, TWIN, t + 1>(a, smem, wring, ring, tile0, ts, lane);
-    }
-}
-
-template <int K, int M, int D, int T, bool TWIN>
-__global__ __launch_bounds__(kThreads) void rs_encode_glds_kernel(EncodeArgs a, uint32_t resid) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    constexpr uint32_t kTab = M * K * sizeof(gf::PermTab), kSlot = K * 64 * kChunk;
-    if constexpr (!TWIN) {
-        uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
-        for (uint32_t i = threadIdx.x; i < (uint32_t)(M * K * 8); i += kThreads) dst[i] = a.dytabs[i];
-        __syncthreads();
-    }
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    // Tiles: with resid = 0, workgroup w (XCD-contiguous order) takes tiles [4Tw, 4Tw + 4T), wave q
-    // tiles q, q + 4, ...; with resid = R (workgroups resident per XCD), the workgroups of an XCD
-    // go in groups of R consecutive ones that sweep their group's 4TR tiles together, step t of
-    // workgroup j at tiles 4(tR' + j) + q (R' the group's size): the resident waves of an XCD
-    // then work on one compact window of tiles, as the flat grid's do.
-    uint32_t tile0, ts;
-    const uint32_t G = gridDim.x, full = G & ~7u;
-    if (resid == 0 || blockIdx.x >= full) {
-        tile0 = xcd_order() * (4u * T) + wave;
-        ts = 4;
-    } else {
-        const uint32_t nx = full >> 3, x = blockIdx.x & 7u, j = blockIdx.x >> 3;
-        const uint32_t g0 = j / resid * resid, gs = min(resid, nx - g0);
-        tile0 = (x * nx + g0) * (4u * T) + (j - g0) * 4u + wave;
-        ts = 4u * gs;
-    }
-    const uint8_t* wring = smem + kTab + wave * (D * kSlot);
-    const uint32_t ring = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_addr(wring));
-#pragma unroll
-    for (int u = 0; u < (D < T ? D : T); ++u) glds_issue<K>(a, ring + u * kSlot, tile0 + ts * u, lane);
-    glds_step<K, M, D, T, TWIN, 0>(a, smem, wring, ring, tile0, ts, lane);
-}
-
-// enc_glds knob: D * 100 + T, + 1000 for the twin body, + 10000 for the compact tile order
-template <int D, int T, bool TWIN>
-static hipError_t glds_launch(const EncodeArgs& a, bool compact, hipStream_t s) {
-    const int grid = (int)((a.total + 4u * 64u * T - 1) / (4u * 64u * T));
-    const size_t own = (size_t)a.m * a.k * sizeof(gf::PermTab) + (size_t)4 * D * 8 * 64 * kChunk;
-    if (own > g_max_lds) return hipErrorInvalidValue;
-    const size_t lds = occupancy_lds(g_tune.enc_wpc, own);
-    // resident workgroups per XCD (32 CUs each) for the compact tile order (knob value + 10000)
-    const uint32_t resid = compact ? (uint32_t)(32 * std::max<size_t>(1, 160 * 1024 / lds)) : 0u;
-    hipLaunchKernelGGL((rs_encode_glds_kernel<8, 4, D, T, TWIN>), dim3(grid), dim3(kThreads), lds, s, a, resid);
-    return hipGetLastError();
-}
-template <bool TWIN>
-static hipError_t glds_dispatch(const EncodeArgs& a, int v, hipStream_t s) {
-    const bool compact = v >= 10000;
-    switch (v % 10000) {
-        case 104: return glds_launch<1, 4, TWIN>(a, compact, s);
-        case 108: return glds_launch<1, 8, TWIN>(a, compact, s);
-        case 204: return glds_launch<2, 4, TWIN>(a, compact, s);
-        case 208: return glds_launch<2, 8, TWIN>(a, compact, s);
-        case 216: return glds_launch<2, 16, TWIN>(a, compact, s);
-        case 308: return glds_launch<3, 8, TWIN>(a, compact, s);
-        case 316: return glds_launch<3, 16, TWIN>(a, compact, s);
-        case 416: return glds_launch<4, 16, TWIN>(a, compact, s);
-        default: return hipErrorInvalidValue;
-    }
 }
 
 // ------------------------------------------------------------------ RS encode, bit-sliced
@@ -505,16 +347,15 @@ hipError_t launch_rs_encode_fixed(const EncodeArgs& a, hipStream_t s) {
     if (a.k == 16 && a.m == 8) return enc_bits_dispatch<16, 8>(a, s);
     if (a.k == 20 && a.m == 10) return enc_bits_dispatch<20, 10>(a, s);
     if (a.k == 8 && a.m == 4 && a.dytabs) {
-        if (const int v = g_tune.enc_glds) return v % 10000 >= 1000 ? glds_dispatch<true>(a, v - 1000, s) : glds_dispatch<false>(a, v, s);
         // 3 workgroups per CU (knob enc_wpc; DESIGN.md 3: the flat grid at 3 beats 2, 4 and uncapped)
         const int grid = (int)((a.total + kThreads - 1) / kThreads);
         const size_t lds = occupancy_lds(g_tune.enc_wpc, (size_t)a.m * a.k * sizeof(gf::PermTab));
-        switch (g_tune.st_pol) {
-            case 1: hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4, 1>), dim3(grid), dim3(kThreads), lds, s, a); break;
-            case 2: hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4, 2>), dim3(grid), dim3(kThreads), lds, s, a); break;
-            case 3: hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4, 3>), dim3(grid), dim3(kThreads), lds, s, a); break;
-            default: hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4>), dim3(grid), dim3(kThreads), lds, s, a);
-        }
+        // parity stored with sc1 (st_pol 1: the line leaves the XCD's L2; -1.7 / -2.1 % time against nt
+        // stores on two boxes, profiles/r06/stpol_ab_*.log), or nt (st_pol 0)
+        if (g_tune.st_pol == 1)
+            hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4, 1>), dim3(grid), dim3(kThreads), lds, s, a);
+        else
+            hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4>), dim3(grid), dim3(kThreads), lds, s, a);
         return hipGetLastError();
     }
     return hipErrorInvalidValue;

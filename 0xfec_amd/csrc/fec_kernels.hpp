@@ -144,22 +144,17 @@ struct Tuning {
     std::atomic<int> host_threads{8};   // FEC_HOST (pageable): copy workers for the staging / scatter copies
     std::atomic<int> bat_zc{4 << 20};   // batch encoder / decoder (fec_batch.cpp): sets of at most this many
                                         // input bytes are coded straight from / into their pinned buffers
-    // RS(8,12) encode by the LDS-DMA ring kernel (fec_encode.hip): 0 off, else D * 100 + T (+ 1000: the
-    // twin body, measurement only)
-    std::atomic<int> enc_glds{0};
     // in-place reconstructs of RS(8,12): routed by a classify pass between the direct body and the
     // sorted plans (fec_recover.hip); 0: the sorted-plan route for every batch
     std::atomic<int> dec_route{1};
-    // store cache policy of the RS(8,12) encode (st_pol) and direct decode (dst_pol) (fec_device.hpp
-    // st16p): 0 nt, 1 sc1, 2 sc0 sc1, 3 nt sc1
+    // store cache policy of the RS(8,12) encode (st_pol: 1 sc1, 0 nt) and direct decode (dst_pol: 3 nt
+    // sc1, 0 nt) (fec_device.hpp st16p), and of their traffic twins
     std::atomic<int> st_pol{1};
-    // RS(16,24) / RS(20,30) rebuild: the second block's table rows 4 banks on (fec_rebuild.hip Slice)
-    std::atomic<int> dec_lpad{0};
     std::atomic<int> dst_pol{3};
     // resident workgroups per CU of the routed in-place kernel (-1: the direct kernel's, dir_wpc)
     std::atomic<int> route_wpc{-1};
 };
-constexpr int kTuningKeys = 17;   // fec__set_tuning keys 0..16, in the order above
+constexpr int kTuningKeys = 15;   // fec__set_tuning keys 0..14, in the order above
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):
 // halfway between 160K/(wpc+1) and 160K/wpc, never below what the kernel itself needs.

@@ -2,7 +2,8 @@
 //
 // A twin moves exactly the bytes its kernel moves, with the same launch geometry (flat grid, one
 // 16-byte chunk per lane, XCD-contiguous workgroup order, the same residency cap through dynamic
-// LDS, non-temporal loads and stores, zero-padded tail chunks) and no field arithmetic: the XOR of
+// LDS, the same cache policies: non-temporal loads, and the kernel's store policy, zero-padded tail
+// chunks) and no field arithmetic: the XOR of
 // its inputs stands in for the products. Timed on the same box and buffers right after the
 // kernel, its rate is that box's ceiling for the kernel's access shape, so a bench line can say
 // how much of a kernel's distance to the 8 TB/s spec is the box and how much is the kernel.
@@ -29,7 +30,8 @@
 namespace fk {
 namespace {
 
-template <int K, int M>
+// SP: the store policy of the kernel twinned (fec_device.hpp st16p; RS(8,12): knobs st_pol / dst_pol)
+template <int K, int M, int SP = 0>
 __global__ __launch_bounds__(kThreads) void probe_encode_kernel(EncodeArgs a) {
     extern __shared__ uint8_t smem[];   // residency only, as the encode's staged tables
     const uint32_t it = xcd_order() * kThreads + threadIdx.x;
@@ -53,7 +55,7 @@ __global__ __launch_bounds__(kThreads) void probe_encode_kernel(EncodeArgs a) {
     uint8_t* dst = a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk;
     const uint32_t nb = min(a.len - c * kChunk, (uint32_t)kChunk);
 #pragma unroll
-    for (int r = 0; r < M; ++r) st16<true>(dst + (uint64_t)r * a.ss, keep_bytes(acc[r], nb));
+    for (int r = 0; r < M; ++r) st16p<SP>(dst + (uint64_t)r * a.ss, keep_bytes(acc[r], nb));
     if (a.k == 0x5A5A5A5Au) smem[0] = 1;   // never: keeps the LDS allocation
 }
 
@@ -67,7 +69,7 @@ struct RecoverProbeArgs {
     FastDiv div_cps;
 };
 
-template <int K>
+template <int K, int SP = 0>
 __global__ __launch_bounds__(kThreads) void probe_recover_kernel(RecoverProbeArgs a, uint32_t m) {
     extern __shared__ uint8_t smem[];   // residency only, as the decode's wave slices
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -104,7 +106,7 @@ __global__ __launch_bounds__(kThreads) void probe_recover_kernel(RecoverProbeArg
         acc.w ^= x[j].w;
     }
     const uint32_t nb = min(a.len - c * kChunk, (uint32_t)kChunk);
-    st16<true>(a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk, keep_bytes(acc, nb));
+    st16p<SP>(a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk, keep_bytes(acc, nb));
     if (a.nin == 0x5A5A5A5Au) smem[0] = 1;   // never: keeps the LDS allocation
 }
 
@@ -216,6 +218,8 @@ extern "C" int fec_probe_encode_traffic(fec_ctx* ctx, int k, int m, size_t shard
     if (wpc < 0) wpc = k >= 16 ? (int)g_tune.enc_bwpc : k == 2 ? 0 : (int)g_tune.enc_wpc;
     const size_t lds = occupancy_lds(wpc, k == 8 ? (size_t)m * k * 32 : 0);
     if (k == 2) hipLaunchKernelGGL((probe_encode_kernel<2, 1>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (k == 8 && g_tune.st_pol == 1)
+        hipLaunchKernelGGL((probe_encode_kernel<8, 4, 1>), dim3(grid), dim3(kThreads), lds, s, a);
     else if (k == 8) hipLaunchKernelGGL((probe_encode_kernel<8, 4>), dim3(grid), dim3(kThreads), lds, s, a);
     else if (k == 16) hipLaunchKernelGGL((probe_encode_kernel<16, 8>), dim3(grid), dim3(kThreads), lds, s, a);
     else hipLaunchKernelGGL((probe_encode_kernel<20, 10>), dim3(grid), dim3(kThreads), lds, s, a);
@@ -258,6 +262,8 @@ extern "C" int fec_probe_recover_traffic(fec_ctx* ctx, int k, int m, size_t shar
     const size_t lds = occupancy_lds(wpc, (size_t)4 * 3 * k * 32);
     const uint32_t um = (uint32_t)m;
     if (k == 2) hipLaunchKernelGGL((probe_recover_kernel<2>), dim3(grid), dim3(kThreads), lds, s, a, um);
+    else if (k == 8 && g_tune.dst_pol == 3)
+        hipLaunchKernelGGL((probe_recover_kernel<8, 3>), dim3(grid), dim3(kThreads), lds, s, a, um);
     else if (k == 8) hipLaunchKernelGGL((probe_recover_kernel<8>), dim3(grid), dim3(kThreads), lds, s, a, um);
     else if (k == 16) hipLaunchKernelGGL((probe_recover_kernel<16>), dim3(grid), dim3(kThreads), lds, s, a, um);
     else hipLaunchKernelGGL((probe_recover_kernel<20>), dim3(grid), dim3(kThreads), lds, s, a, um);

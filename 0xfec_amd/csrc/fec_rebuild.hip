@@ -73,14 +73,13 @@ constexpr uint32_t kTabLds = 256 * 16 + 256 * 4;   // the workgroup's copy of kP
 // A wave's LDS slice: PermTab words of R rows x K inputs for each of its WB blocks, the blocks'
 // input offsets, their plan records. (RS(16,24)'s 2048-byte T0|T1 and 512-byte T2 block strides put
 // the two blocks' rows on the same banks, 24 % of its LDS cycles in conflicts; padding them 32 banks
-// apart measured +0.1 % for RS(16,24) and -1.2 % for RS(20,30), r04c: not on the critical path.)
-// PAD (round 6, knob dec_lpad): the second block's T0|T1 and T2 words 16 bytes further on (4 banks),
-// so the two blocks' broadcast table reads of one instruction fall on different banks.
-template <int K, int R, int PAD = 0>
+// apart measured +0.1 % for RS(16,24) and -1.2 % for RS(20,30), r04c, and 4 banks apart -0.03 % and
+// -0.1 %, r06d (profiles/r06/lpad_*_r06d.log): not on the critical path.)
+template <int K, int R>
 struct Slice {
     static constexpr uint32_t WB = 2;
-    static constexpr uint32_t bs01 = R * K * 16 + 16 * PAD;   // bytes per block
-    static constexpr uint32_t bs2 = R * K * 4 + 16 * PAD;
+    static constexpr uint32_t bs01 = R * K * 16;   // bytes per block
+    static constexpr uint32_t bs2 = R * K * 4;
     static constexpr uint32_t t01 = 0;                        // uint4    [WB][R][K], blocks bs01 apart
     static constexpr uint32_t t2 = t01 + WB * bs01;           // uint32_t [WB][R][K], blocks bs2 apart
     static constexpr uint32_t offs = t2 + WB * bs2;           // uint64_t [WB][K]
@@ -183,9 +182,9 @@ __device__ __forceinline__ void rebuild_rows(const ReconArgs& a, const uint8_t* 
 
 // Flat grid, one wave per 64 consecutive items of the (sorted) plan order; R: the code's largest
 // rebuilt row count (min(k, m)); W: loads in flight per lane; RP: row-pipelined table reads.
-template <int K, int R, int W, bool RP, int PAD = 0>
+template <int K, int R, int W, bool RP>
 __global__ __launch_bounds__(kThreads) void rs_rebuild_k_kernel(ReconArgs a) {
-    using S = Slice<K, R, PAD>;
+    using S = Slice<K, R>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint4* g01 = reinterpret_cast<uint4*>(smem);
     uint32_t* g2 = reinterpret_cast<uint32_t*>(smem + 256 * 16);
@@ -274,13 +273,13 @@ __global__ __launch_bounds__(kThreads) void rs_rebuild_k_kernel(ReconArgs a) {
 #undef FEC_RB_ROWS
 }
 
-template <int K, int R, int W, bool RP, int PAD = 0>
+template <int K, int R, int W, bool RP>
 hipError_t rebuild_launch(const ReconArgs& a, hipStream_t s) {
     const uint64_t total = (uint64_t)a.nblocks * a.cps;
     const int grid = (int)((total + kThreads - 1) / kThreads);
     if (grid == 0) return hipSuccess;
-    const size_t lds = occupancy_lds(g_tune.dec_wpc, kTabLds + 4 * Slice<K, R, PAD>::bytes(a.lay.stride));
-    hipLaunchKernelGGL((rs_rebuild_k_kernel<K, R, W, RP, PAD>), dim3(grid), dim3(kThreads), lds, s, a);
+    const size_t lds = occupancy_lds(g_tune.dec_wpc, kTabLds + 4 * Slice<K, R>::bytes(a.lay.stride));
+    hipLaunchKernelGGL((rs_rebuild_k_kernel<K, R, W, RP>), dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 
@@ -293,8 +292,8 @@ bool rebuild_k_applies(uint32_t k, uint32_t maxe, uint32_t cps) {
 hipError_t launch_rs_rebuild_k(const ReconArgs& a, hipStream_t s) {
     // windows by interleaved A/B (r03k): RS(16,24) 8 -> 4 +0.3 % (4 / 6 / 8 within 0.7 %); RS(20,30)
     // 8 -> 6 +6.7 % (137 -> 125 VGPRs: 4 instead of 3 waves per SIMD)
-    if (a.k == 16) return g_tune.dec_lpad ? rebuild_launch<16, 8, 4, false, 1>(a, s) : rebuild_launch<16, 8, 4, false>(a, s);
-    return g_tune.dec_lpad ? rebuild_launch<20, 10, 6, true, 1>(a, s) : rebuild_launch<20, 10, 6, true>(a, s);
+    if (a.k == 16) return rebuild_launch<16, 8, 4, false>(a, s);
+    return rebuild_launch<20, 10, 6, true>(a, s);
 }
 
 }  // namespace fk

@@ -422,11 +422,7 @@ hipError_t launch_rs_recover_direct(const ReconArgs& a, hipStream_t s) {
         e = direct_launch<20, 2>(a, cw, s);
     else if (a.k == 16)
         e = direct_launch<16, 2>(a, cw, s);
-    else if (a.k == 8 && by_arg && g_tune.dst_pol == 1)
-        e = direct_launch<8, 1, 1>(a, cw, s);
-    else if (a.k == 8 && by_arg && g_tune.dst_pol == 2)
-        e = direct_launch<8, 1, 2>(a, cw, s);
-    else if (a.k == 8 && by_arg && g_tune.dst_pol == 3)
+    else if (a.k == 8 && by_arg && g_tune.dst_pol == 3)   // nt sc1 stores (knob dst_pol; 0: nt)
         e = direct_launch<8, 1, 3>(a, cw, s);
     else if (a.k == 8)
         e = by_arg ? direct_launch<8, 1>(a, cw, s) : direct_launch<8, 0>(a, cw, s);

@@ -666,7 +666,10 @@ def main():
                 "stream_reference": probe["stream_reference"],
                 "decode_inplace": {"ms": round(inplace_ms, 4),
                                    "GB/s": round(dec_bytes / (inplace_ms / 1e3) / 1e9, 1),
-                                   "api": "fec_rs_reconstruct_batch (direct kernel, in place), not in the step"},
+                                   "api": "fec_rs_reconstruct_batch in place, not in the step: classify pass (one "
+                                          "word: does a block need a multi-erasure plan?), then rs_reconstruct_routed_kernel, "
+                                          "which on this single-erasure batch runs the direct body (the sorted plan kernel "
+                                          "exits at once)"},
                 "step_frac": round((enc_bytes + dec_bytes) / ((enc_ms + dec_ms) / 1000.0) / HBM_PEAK, 4),
             },
             "check": {"roundtrip_full_batch": ok_roundtrip, "encode_vs_oracle_64_blocks": ok_parity,

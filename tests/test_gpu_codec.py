@@ -295,9 +295,6 @@ ENC_VARIANTS = {
     "own_wpc2": dict(enc_fixed=1, enc_wpc=2, enc_bwpc=2),
     "generic": dict(enc_fixed=0),
     "generic_wpc2": dict(enc_fixed=0, gen_wpc=2),
-    "glds104": dict(enc_fixed=1, enc_glds=104),
-    "glds208_wpc2": dict(enc_fixed=1, enc_glds=208, enc_wpc=2),
-    "glds316_wpc1": dict(enc_fixed=1, enc_glds=316, enc_wpc=1),
     "stpol_nt": dict(enc_fixed=1, st_pol=0),
 }
 
@@ -345,7 +342,6 @@ DEC_VARIANTS = {
     "wpc2": dict(dir_wpc=2, dec_wpc=2),
     "noroute": dict(dec_route=0),
     "dstpol_nt": dict(dst_pol=0),
-    "lpad": dict(dec_lpad=1),
 }
 
 

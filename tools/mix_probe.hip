@@ -88,8 +88,10 @@ __device__ __forceinline__ void st_pol(uint8_t* p, u32x4 v) {
         *reinterpret_cast<u32x4*>(p) = v;
     } else if constexpr (POL == 2) {
         asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-    } else {
+    } else if constexpr (POL == 3) {
         asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    } else {
+        asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
     }
 }
 
@@ -130,6 +132,70 @@ extern "C" int mix_pol_probe(const void* in, void* out, size_t in_bs, size_t out
         return (int)hipGetLastError();                                                                           \
     }
     MQ(8, 1, 0) MQ(8, 1, 1) MQ(8, 1, 2) MQ(8, 1, 3) MQ(8, 4, 0) MQ(8, 4, 1) MQ(8, 4, 2) MQ(8, 4, 3) MQ(8, 0, 0)
+    return -1;
+}
+
+// Load cache policy (round 6): the 8 shard loads of an item as one asm statement with its own wait
+// (the destinations are written at the wait, so the compiler cannot read them early). LP 0 nt,
+// 1 plain, 2 sc1, 3 nt sc1, 4 sc0 sc1. Stores by st_pol<SP>. NIN is 8.
+#define FEC_LD8(MOD)                                                                                       \
+    asm volatile("global_load_dwordx4 %0, %8, off" MOD "\n\t"                                             \
+                 "global_load_dwordx4 %1, %8, off offset:1216" MOD "\n\t"                                 \
+                 "global_load_dwordx4 %2, %8, off offset:2432" MOD "\n\t"                                 \
+                 "global_load_dwordx4 %3, %8, off offset:3648" MOD "\n\t"                                 \
+                 "global_load_dwordx4 %4, %9, off" MOD "\n\t"                                             \
+                 "global_load_dwordx4 %5, %9, off offset:1216" MOD "\n\t"                                 \
+                 "global_load_dwordx4 %6, %9, off offset:2432" MOD "\n\t"                                 \
+                 "global_load_dwordx4 %7, %9, off offset:3648" MOD "\n\t"                                 \
+                 "s_waitcnt vmcnt(0)"                                                                       \
+                 : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3]), "=&v"(x[4]), "=&v"(x[5]), "=&v"(x[6]), \
+                   "=&v"(x[7])                                                                              \
+                 : "v"(src), "v"(src + 4 * 1216)                                                            \
+                 : "memory")
+
+template <int LP, int NOUT, int SP>
+__global__ __launch_bounds__(256) void mix_lp_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                     size_t in_bs, size_t out_bs, size_t ss, uint32_t cps,
+                                                     uint32_t total) {
+    extern __shared__ uint8_t pad[];
+    const uint32_t item = swizzle_wg(blockIdx.x, gridDim.x, 1) * 256 + threadIdx.x;
+    if (item >= total) return;
+    const uint32_t b = item / cps, c = item - b * cps;
+    const uint8_t* src = in + (size_t)b * in_bs + (size_t)c * 16;   // shard stride 1216 (the asm offsets)
+    u32x4 x[8];
+    if constexpr (LP == 0) FEC_LD8(" nt");
+    else if constexpr (LP == 1) FEC_LD8("");
+    else if constexpr (LP == 2) FEC_LD8(" sc1");
+    else if constexpr (LP == 3) FEC_LD8(" nt sc1");
+    else FEC_LD8(" sc0 sc1");
+    u32x4 acc = x[0] ^ x[1] ^ x[2] ^ x[3] ^ x[4] ^ x[5] ^ x[6] ^ x[7];
+    uint8_t* dst = out + (size_t)b * out_bs + (size_t)c * 16;
+#pragma unroll
+    for (int r = 0; r < NOUT; ++r) {
+        u32x4 v = acc;
+        v.x ^= r;
+        st_pol<SP>(dst + (size_t)r * ss, v);
+    }
+    if (pad[0] == 0x5A && acc.x == 0x12345u) out[0] = 1;
+}
+
+extern "C" int mix_lp_probe(const void* in, void* out, size_t in_bs, size_t out_bs, size_t ss, unsigned cps,
+                            unsigned nblocks, int nout, int lp, int sp, size_t lds_pad, void* stream) {
+    if (ss != 1216) return -2;
+    const uint32_t total = cps * nblocks;
+    const int grid = (int)((total + 255) / 256);
+    hipStream_t s = (hipStream_t)stream;
+    const uint8_t* i8 = (const uint8_t*)in;
+    uint8_t* o8 = (uint8_t*)out;
+#define ML(LP, NO, SP)                                                                                          \
+    if (lp == LP && nout == NO && sp == SP) {                                                                   \
+        hipLaunchKernelGGL((mix_lp_kernel<LP, NO, SP>), dim3(grid), dim3(256), lds_pad, s, i8, o8, in_bs, out_bs, \
+                           ss, cps, total);                                                                     \
+        return (int)hipGetLastError();                                                                          \
+    }
+    ML(0, 4, 0) ML(1, 4, 0) ML(2, 4, 0) ML(3, 4, 0) ML(4, 4, 0) ML(0, 4, 2) ML(1, 4, 2) ML(2, 4, 2) ML(3, 4, 2)
+    ML(4, 4, 2) ML(0, 1, 0) ML(1, 1, 0) ML(2, 1, 0) ML(3, 1, 0) ML(4, 1, 0) ML(0, 1, 4) ML(1, 1, 4) ML(2, 1, 4)
+    ML(3, 1, 4) ML(4, 1, 4)
     return -1;
 }
 

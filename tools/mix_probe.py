@@ -2,7 +2,7 @@
 """Diagnostics: mixed read/write HBM rates vs output offset, XCD mapping, occupancy, items per
 lane (tools/mix_probe.hip). Prints one JSON object; rates are bytes moved / time in GB/s.
 
-usage: mix_probe.py [sweep1|sweep2|sweep3|persist|ipl|pol] [--rebuild] [--build-only]"""
+usage: mix_probe.py [sweep1|sweep2|sweep3|persist|ipl|pol|lpol] [--rebuild] [--build-only]"""
 import ctypes
 import json
 import os
@@ -156,6 +156,37 @@ def main():
                     for w, pad in pads.items():
                         acc.setdefault("r%d w%d %s wg%d" % (nin, nout, names[pol], w), []).append(
                             runq(nin, nout, pol, pad))
+            res.update({kk: sorted(v)[len(v) // 2] for kk, v in acc.items()})
+            flush()
+    elif mode == "lpol":
+        # load cache policy x store policy (round 6): encode shape (8 reads + 4 stores: nt / sc1 stores)
+        # and decode shape (8 + 1: nt / nt sc1 stores), at 2 and 3 workgroups/CU, interleaved rounds
+        lib.mix_lp_probe.argtypes = [vp, vp, sz, sz, sz, u, u, i, i, i, sz, vp]
+        B = 1 << 20
+        pads = {2: 64 << 10, 3: 48 << 10}
+        lnames = {0: "nt", 1: "plain", 2: "sc1", 3: "ntsc1", 4: "sc0sc1"}
+        snames = {0: "nt", 2: "sc1", 4: "ntsc1"}
+        acc = {}
+
+        def runl(nout, lp, sp, pad, iters=6):
+            fn = lambda: lib.mix_lp_probe(base, base + B * 8 * ss, 8 * ss, nout * ss, ss, cps, B, nout, lp, sp, pad, st)
+            if fn() != 0:
+                return None
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(iters):
+                fn()
+            e.record()
+            torch.cuda.synchronize()
+            return round(B * cps * 16 * (8 + nout) / (s.elapsed_time(e) / iters / 1e3) / 1e9, 1)
+        for rnd in range(3):
+            for nout, sps in ((4, (0, 2)), (1, (0, 4))):
+                for sp in sps:
+                    for lp in range(5):
+                        for w, pad in pads.items():
+                            acc.setdefault("r8 w%d ld-%s st-%s wg%d" % (nout, lnames[lp], snames[sp], w), []).append(
+                                runl(nout, lp, sp, pad))
             res.update({kk: sorted(v)[len(v) // 2] for kk, v in acc.items()})
             flush()
     elif mode == "persist":
