@@ -151,8 +151,8 @@ struct Tuning {
     // sc1, 0 nt) (fec_device.hpp st16p), and of their traffic twins
     std::atomic<int> st_pol{1};
     std::atomic<int> dst_pol{3};
-    // resident workgroups per CU of the routed in-place kernel (-1: the direct kernel's, dir_wpc)
-    std::atomic<int> route_wpc{-1};
+    // resident workgroups per CU of the routed in-place kernel (0: as many as fit)
+    std::atomic<int> route_wpc{0};
 };
 constexpr int kTuningKeys = 15;   // fec__set_tuning keys 0..14, in the order above
 

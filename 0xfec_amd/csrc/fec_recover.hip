@@ -374,8 +374,10 @@ hipError_t launch_rs_reconstruct_routed(const ReconArgs& a, hipStream_t s) {
     if (flat == 0) return hipSuccess;
     CoefWords cw{};
     memcpy(cw.w, a.single_coef_host, (size_t)a.k * a.m * ((a.k + 3) / 4) * 4);
-    // residency: knob route_wpc, else the direct kernel's (dir_wpc; 3 for k >= 8)
-    const int wpc = g_tune.route_wpc >= 0 ? (int)g_tune.route_wpc : g_tune.dir_wpc >= 0 ? (int)g_tune.dir_wpc : 3;
+    // residency (knob route_wpc): uncapped, i.e. the wave body's 95 VGPRs (5 workgroups per CU). The
+    // direct body alone runs best at 3, the wave body at 5: at 3 the plan route lost 9-14 % on mixed
+    // batches, at 5 / uncapped the direct route gives up 1.2-2.3 % (profiles/r06/inplace_route_*.log)
+    const int wpc = g_tune.route_wpc;
     const size_t own = std::max(4 * direct_wave_bytes(a.k), 4 * wave_slice_bytes(a.k, a.maxe, a.lay.stride));
     const size_t lds = occupancy_lds(wpc, own);
     const bool sp3 = g_tune.dst_pol == 3;
