@@ -175,15 +175,15 @@ __device__ __forceinline__ void dy_encode_chunk(const uint4 (&x)[K], const uint8
 // walking T tiles with the next D tiles' shard chunks in flight as LDS-DMA loads into a ring:
 // 7-17 % slower than this flat grid at every residency, its traffic twin 7.5-9 % below the flat
 // twin; DESIGN.md 3, the kernel is in commit f1dd58a.)
-template <int K, int M, int SP = 0>
-__global__ __launch_bounds__(kThreads) void rs_encode_fixed_kernel(EncodeArgs a) {
+template <int K, int M, int SP = 0, int NT = kThreads>
+__global__ __launch_bounds__(NT) void rs_encode_fixed_kernel(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     {
         uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
-        for (uint32_t i = threadIdx.x; i < (uint32_t)(M * K * 8); i += kThreads) dst[i] = a.dytabs[i];
+        for (uint32_t i = threadIdx.x; i < (uint32_t)(M * K * 8); i += NT) dst[i] = a.dytabs[i];
         __syncthreads();
     }
-    const uint32_t it = xcd_order() * kThreads + threadIdx.x;
+    const uint32_t it = xcd_order() * NT + threadIdx.x;
     if (it >= a.total) return;
     const uint32_t b = fdiv(it, a.div_cps);
     const uint32_t c = it - b * a.cps;
@@ -264,9 +264,9 @@ __device__ __forceinline__ void bs_stream(const uint8_t* s0, const uint8_t* s1, 
     }
 }
 
-template <int K, int M>
+template <int K, int M, int SP>
 __global__ __launch_bounds__(kThreads) void rs_encode_bits_kernel(EncodeArgs a) {
-    constexpr bool NTL = true, NTS = true;
+    constexpr bool NTL = true;
     // A wave takes 128 consecutive (block, chunk) items: lane l items w*128 + l and w*128 + 64 + l,
     // so each load and store instruction covers 64 consecutive chunks, as in the one-chunk
     // kernels. The two chunks of a lane may belong to different blocks: the network treats every
@@ -297,8 +297,8 @@ __global__ __launch_bounds__(kThreads) void rs_encode_bits_kernel(EncodeArgs a) 
 #pragma unroll
     for (int r = 0; r < M; ++r) {
         bit_transpose8(y[r]);
-        st16<NTS>(d0 + (uint64_t)r * a.ss, keep_bytes(make_uint4(y[r][0], y[r][1], y[r][2], y[r][3]), nb0));
-        if (two) st16<NTS>(d1 + (uint64_t)r * a.ss, keep_bytes(make_uint4(y[r][4], y[r][5], y[r][6], y[r][7]), nb1));
+        st16p<SP>(d0 + (uint64_t)r * a.ss, keep_bytes(make_uint4(y[r][0], y[r][1], y[r][2], y[r][3]), nb0));
+        if (two) st16p<SP>(d1 + (uint64_t)r * a.ss, keep_bytes(make_uint4(y[r][4], y[r][5], y[r][6], y[r][7]), nb1));
     }
 }
 
@@ -306,8 +306,9 @@ template <int K, int M>
 static hipError_t enc_bits_dispatch(const EncodeArgs& a, hipStream_t s) {
     const int grid = (int)((a.total + 2 * kThreads - 1) / (2 * kThreads));
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((rs_encode_bits_kernel<K, M>), dim3(grid), dim3(kThreads), occupancy_lds(g_tune.enc_bwpc, 0), s,
-                       a);
+    const size_t lds = occupancy_lds(g_tune.enc_bwpc, 0);
+    if (g_tune.st_pol == 1) hipLaunchKernelGGL((rs_encode_bits_kernel<K, M, 1>), dim3(grid), dim3(kThreads), lds, s, a);
+    else hipLaunchKernelGGL((rs_encode_bits_kernel<K, M, 0>), dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 
@@ -352,10 +353,17 @@ hipError_t launch_rs_encode_fixed(const EncodeArgs& a, hipStream_t s) {
         const size_t lds = occupancy_lds(g_tune.enc_wpc, (size_t)a.m * a.k * sizeof(gf::PermTab));
         // parity stored with sc1 (st_pol 1: the line leaves the XCD's L2; -1.7 / -2.1 % time against nt
         // stores on two boxes, profiles/r06/stpol_ab_*.log), or nt (st_pol 0)
-        if (g_tune.st_pol == 1)
+        if (g_tune.enc_nt == 128 || g_tune.enc_nt == 64) {
+            // workgroups of 2 (1) waves: residency in steps of 2 (1) waves per CU (knob enc_nt)
+            const int nt = g_tune.enc_nt;
+            const int g2 = (int)((a.total + nt - 1) / nt);
+            if (nt == 128) hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4, 1, 128>), dim3(g2), dim3(128), lds, s, a);
+            else hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4, 1, 64>), dim3(g2), dim3(64), lds, s, a);
+        } else if (g_tune.st_pol == 1) {
             hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4, 1>), dim3(grid), dim3(kThreads), lds, s, a);
-        else
+        } else {
             hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4>), dim3(grid), dim3(kThreads), lds, s, a);
+        }
         return hipGetLastError();
     }
     return hipErrorInvalidValue;

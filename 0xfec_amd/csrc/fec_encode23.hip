@@ -24,11 +24,12 @@ __device__ __forceinline__ uint32_t gf_dbl4(uint32_t v) {
 
 __device__ __forceinline__ uint32_t parity23(uint32_t x0, uint32_t x1) { return x0 ^ gf_dbl4(x0 ^ x1); }
 
-// Non-temporal loads and stores: with plain loads back-to-back launches re-read the config's whole
-// batch (239 MB) from the 256 MiB Infinity Cache, +11 % that a stream of fresh inputs never sees
-// 
+// Non-temporal loads (with plain loads back-to-back launches re-read the config's whole batch, 239
+// MB, from the 256 MiB Infinity Cache, +11 % that a stream of fresh inputs never sees: DESIGN.md 3,
+// r04); stores by policy SP (fec_device.hpp st16p)
+template <int SP>
 __global__ __launch_bounds__(kThreads) void rs_encode23_kernel(EncodeArgs a) {
-    constexpr bool NTL = true, NTS = true;
+    constexpr bool NTL = true;
     const uint32_t it = xcd_order() * kThreads + threadIdx.x;
     if (it >= a.total) return;
     const uint32_t b = fdiv(it, a.div_cps);
@@ -38,7 +39,7 @@ __global__ __launch_bounds__(kThreads) void rs_encode23_kernel(EncodeArgs a) {
     const uint4 p = make_uint4(parity23(x0.x, x1.x), parity23(x0.y, x1.y), parity23(x0.z, x1.z),
                                parity23(x0.w, x1.w));
     const uint32_t nb = min(a.len - c * kChunk, (uint32_t)kChunk);
-    st16<NTS>(a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk, keep_bytes(p, nb));
+    st16p<SP>(a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk, keep_bytes(p, nb));
 }
 
 bool row_is_3_2() {
@@ -59,7 +60,9 @@ bool rs_encode23_applies(uint32_t k, uint32_t m) { return k == 2 && m == 1 && ro
 hipError_t launch_rs_encode23(const EncodeArgs& a, hipStream_t s) {
     const uint32_t chunks = (a.total + kThreads - 1) / kThreads;
     if (chunks == 0) return hipSuccess;
-    hipLaunchKernelGGL(rs_encode23_kernel, dim3(chunks), dim3(kThreads), 0, s, a);
+    // stores by the encodes' policy (knob st_pol: 1 sc1, 0 nt; fec_device.hpp st16p)
+    if (g_tune.st_pol == 1) hipLaunchKernelGGL(rs_encode23_kernel<1>, dim3(chunks), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL(rs_encode23_kernel<0>, dim3(chunks), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }
 

@@ -147,14 +147,19 @@ struct Tuning {
     // in-place reconstructs of RS(8,12): routed by a classify pass between the direct body and the
     // sorted plans (fec_recover.hip); 0: the sorted-plan route for every batch
     std::atomic<int> dec_route{1};
-    // store cache policy of the RS(8,12) encode (st_pol: 1 sc1, 0 nt) and direct decode (dst_pol: 3 nt
-    // sc1, 0 nt) (fec_device.hpp st16p), and of their traffic twins
+    // store cache policy of the fixed-shape encodes (st_pol: 1 sc1, 0 nt: RS(2,3), RS(8,12), RS(16,24),
+    // RS(20,30)) and of the RS(8,12) direct decode (dst_pol: 3 nt sc1, 0 nt) (fec_device.hpp st16p),
+    // and of their traffic twins
     std::atomic<int> st_pol{1};
     std::atomic<int> dst_pol{3};
     // resident workgroups per CU of the routed in-place kernel (0: as many as fit)
     std::atomic<int> route_wpc{0};
+    // threads per workgroup of the RS(8,12) encode and direct decode (256; 128 / 64: residency in
+    // finer steps)
+    std::atomic<int> enc_nt{256};
+    std::atomic<int> dir_nt{256};
 };
-constexpr int kTuningKeys = 15;   // fec__set_tuning keys 0..14, in the order above
+constexpr int kTuningKeys = 17;   // fec__set_tuning keys 0..16, in the order above
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):
 // halfway between 160K/(wpc+1) and 160K/wpc, never below what the kernel itself needs.

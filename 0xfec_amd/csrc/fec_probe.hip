@@ -217,12 +217,19 @@ extern "C" int fec_probe_encode_traffic(fec_ctx* ctx, int k, int m, size_t shard
     // bit-sliced kernel takes two chunks a lane, the twin one)
     if (wpc < 0) wpc = k >= 16 ? (int)g_tune.enc_bwpc : k == 2 ? 0 : (int)g_tune.enc_wpc;
     const size_t lds = occupancy_lds(wpc, k == 8 ? (size_t)m * k * 32 : 0);
-    if (k == 2) hipLaunchKernelGGL((probe_encode_kernel<2, 1>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (k == 8 && g_tune.st_pol == 1)
-        hipLaunchKernelGGL((probe_encode_kernel<8, 4, 1>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (k == 8) hipLaunchKernelGGL((probe_encode_kernel<8, 4>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (k == 16) hipLaunchKernelGGL((probe_encode_kernel<16, 8>), dim3(grid), dim3(kThreads), lds, s, a);
-    else hipLaunchKernelGGL((probe_encode_kernel<20, 10>), dim3(grid), dim3(kThreads), lds, s, a);
+    // the encodes' store policy (knob st_pol: 1 sc1, 0 nt)
+#define FEC_ENC_TWIN(K, M)                                                                              \
+    do {                                                                                                \
+        if (g_tune.st_pol == 1)                                                                         \
+            hipLaunchKernelGGL((probe_encode_kernel<K, M, 1>), dim3(grid), dim3(kThreads), lds, s, a); \
+        else                                                                                            \
+            hipLaunchKernelGGL((probe_encode_kernel<K, M, 0>), dim3(grid), dim3(kThreads), lds, s, a); \
+    } while (0)
+    if (k == 2) FEC_ENC_TWIN(2, 1);
+    else if (k == 8) FEC_ENC_TWIN(8, 4);
+    else if (k == 16) FEC_ENC_TWIN(16, 8);
+    else FEC_ENC_TWIN(20, 10);
+#undef FEC_ENC_TWIN
     return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
 }
 
