@@ -337,6 +337,7 @@ static int rs_encode_device(fec_ctx* ctx, Code* code, size_t len, size_t nblocks
             a.div_cps = fk::make_fastdiv(cps);
             a.tabs = code->d_tabs + (size_t)r0 * k * 8;
             a.dytabs = (r0 == 0 && mr == code->m) ? code->d_dytabs : nullptr;
+            a.sp = fk::encode_store_policy(fk::g_tune.st_pol, data, dbs, parity, pbs, nblocks);
             if (fk::fixed_encode_applies((uint32_t)k, (uint32_t)mr, a.dytabs != nullptr)) {
                 HIP_TRY(fk::launch_rs_encode_fixed(a, ctx->stream));
                 continue;
@@ -430,6 +431,7 @@ static int rs_reconstruct_device(fec_ctx* ctx, Code* code, size_t len, size_t nb
             a.single = code->d_single;
             a.single_coef = code->d_single_coef;
             a.single_coef_host = code->single_coef.data();
+            a.sp = fk::decode_store_policy(fk::g_tune.dst_pol, data, dbs, parity, pbs, out, out_bs, nblocks);
         }
         if (direct) {
             HIP_TRY(fk::launch_rs_recover_direct(a, ctx->stream));
@@ -1216,8 +1218,7 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
     std::atomic<int>* slots[fk::kTuningKeys] = {&t.enc_wpc,   &t.gen_wpc,    &t.dec_wpc,      &t.dir_wpc,
                                                 &t.enc_bwpc,  &t.enc_fixed,  &t.dec_wave,     &t.dec_direct,
                                                 &t.host_chunk, &t.host_threads, &t.bat_zc,     &t.dec_route,
-                                                &t.st_pol,     &t.dst_pol,    &t.route_wpc,    &t.enc_nt,
-                                                &t.dir_nt};
+                                                &t.st_pol,     &t.dst_pol,    &t.route_wpc};
     if (key < 0 || key >= fk::kTuningKeys) return FEC_ERR_INVALID_ARG;
     return slots[key]->exchange(value);
 }

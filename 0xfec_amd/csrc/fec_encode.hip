@@ -175,15 +175,15 @@ __device__ __forceinline__ void dy_encode_chunk(const uint4 (&x)[K], const uint8
 // walking T tiles with the next D tiles' shard chunks in flight as LDS-DMA loads into a ring:
 // 7-17 % slower than this flat grid at every residency, its traffic twin 7.5-9 % below the flat
 // twin; DESIGN.md 3, the kernel is in commit f1dd58a.)
-template <int K, int M, int SP = 0, int NT = kThreads>
-__global__ __launch_bounds__(NT) void rs_encode_fixed_kernel(EncodeArgs a) {
+template <int K, int M, int SP = 0>
+__global__ __launch_bounds__(kThreads) void rs_encode_fixed_kernel(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     {
         uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
-        for (uint32_t i = threadIdx.x; i < (uint32_t)(M * K * 8); i += NT) dst[i] = a.dytabs[i];
+        for (uint32_t i = threadIdx.x; i < (uint32_t)(M * K * 8); i += kThreads) dst[i] = a.dytabs[i];
         __syncthreads();
     }
-    const uint32_t it = xcd_order() * NT + threadIdx.x;
+    const uint32_t it = xcd_order() * kThreads + threadIdx.x;
     if (it >= a.total) return;
     const uint32_t b = fdiv(it, a.div_cps);
     const uint32_t c = it - b * a.cps;
@@ -307,7 +307,7 @@ static hipError_t enc_bits_dispatch(const EncodeArgs& a, hipStream_t s) {
     const int grid = (int)((a.total + 2 * kThreads - 1) / (2 * kThreads));
     if (grid == 0) return hipSuccess;
     const size_t lds = occupancy_lds(g_tune.enc_bwpc, 0);
-    if (g_tune.st_pol == 1) hipLaunchKernelGGL((rs_encode_bits_kernel<K, M, 1>), dim3(grid), dim3(kThreads), lds, s, a);
+    if (a.sp == 1) hipLaunchKernelGGL((rs_encode_bits_kernel<K, M, 1>), dim3(grid), dim3(kThreads), lds, s, a);
     else hipLaunchKernelGGL((rs_encode_bits_kernel<K, M, 0>), dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
@@ -351,15 +351,11 @@ hipError_t launch_rs_encode_fixed(const EncodeArgs& a, hipStream_t s) {
         // 3 workgroups per CU (knob enc_wpc; DESIGN.md 3: the flat grid at 3 beats 2, 4 and uncapped)
         const int grid = (int)((a.total + kThreads - 1) / kThreads);
         const size_t lds = occupancy_lds(g_tune.enc_wpc, (size_t)a.m * a.k * sizeof(gf::PermTab));
-        // parity stored with sc1 (st_pol 1: the line leaves the XCD's L2; -1.7 / -2.1 % time against nt
-        // stores on two boxes, profiles/r06/stpol_ab_*.log), or nt (st_pol 0)
-        if (g_tune.enc_nt == 128 || g_tune.enc_nt == 64) {
-            // workgroups of 2 (1) waves: residency in steps of 2 (1) waves per CU (knob enc_nt)
-            const int nt = g_tune.enc_nt;
-            const int g2 = (int)((a.total + nt - 1) / nt);
-            if (nt == 128) hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4, 1, 128>), dim3(g2), dim3(128), lds, s, a);
-            else hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4, 1, 64>), dim3(g2), dim3(64), lds, s, a);
-        } else if (g_tune.st_pol == 1) {
+        // parity stored with sc1 (a.sp 1, encode_store_policy: the line leaves the XCD's L2; -1.4 to
+        // -2.1 % time against nt stores on three boxes, profiles/r06/stpol_ab_*.log), or nt
+        // (workgroups of 2 or 1 waves, residency in steps of 8 / 4 waves per CU: 2.49-2.67 ms against
+        // 2.43 at 3 workgroups of 4 waves, profiles/r06/enc_nt_ab_r06h.log)
+        if (a.sp == 1) {
             hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4, 1>), dim3(grid), dim3(kThreads), lds, s, a);
         } else {
             hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4>), dim3(grid), dim3(kThreads), lds, s, a);

@@ -60,8 +60,8 @@ bool rs_encode23_applies(uint32_t k, uint32_t m) { return k == 2 && m == 1 && ro
 hipError_t launch_rs_encode23(const EncodeArgs& a, hipStream_t s) {
     const uint32_t chunks = (a.total + kThreads - 1) / kThreads;
     if (chunks == 0) return hipSuccess;
-    // stores by the encodes' policy (knob st_pol: 1 sc1, 0 nt; fec_device.hpp st16p)
-    if (g_tune.st_pol == 1) hipLaunchKernelGGL(rs_encode23_kernel<1>, dim3(chunks), dim3(kThreads), 0, s, a);
+    // stores by the call's policy (a.sp: fec_kernels.hpp encode_store_policy)
+    if (a.sp == 1) hipLaunchKernelGGL(rs_encode23_kernel<1>, dim3(chunks), dim3(kThreads), 0, s, a);
     else hipLaunchKernelGGL(rs_encode23_kernel<0>, dim3(chunks), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }

@@ -32,7 +32,32 @@ struct EncodeArgs {
     const uint32_t* tabs;      // m * k PermTabs (8 dwords each), device memory
     const uint32_t* dytabs;    // dyadic codes (nullable): leaf PermTabs of the split-recursive
                                // form (fec_capi.cpp dyadic_leaves), padded to m * k entries
+    uint32_t sp;               // store policy of the fixed-shape encodes (fec_device.hpp st16p): 1 sc1
+                               // where the parity region is apart from the data region, else 0 nt
 };
+
+// The encodes' store policy for a call (knob st_pol): sc1 stores let parity lines leave the XCD's L2
+// (-1.4 to -2.1 % RS(8,12) encode time on split buffers), but into parity slots interleaved with the
+// data being read ([B][k+m][S]) they cost 26 % (the XOR layout's twin, r06h): so sc1 only when the
+// [lo, hi) ranges of the two regions do not meet.
+inline bool regions_apart(const void* a, uint64_t abs, const void* b, uint64_t bbs, uint64_t nblocks) {
+    const uintptr_t a0 = (uintptr_t)a, a1 = a0 + abs * nblocks, b0 = (uintptr_t)b, b1 = b0 + bbs * nblocks;
+    return b1 <= a0 || a1 <= b0;
+}
+inline uint32_t encode_store_policy(int st_pol, const void* data, uint64_t dbs, const void* parity, uint64_t pbs,
+                                    uint64_t nblocks) {
+    // (st_pol 2: sc1 whatever the layout, measurement only)
+    return st_pol == 2 || (st_pol == 1 && nblocks && regions_apart(data, dbs, parity, pbs, nblocks)) ? 1u : 0u;
+}
+// The RS(8,12) direct decode's (knob dst_pol): nt sc1 only into an output region apart from the
+// shards it reads (recover calls), else nt (in place: the rebuilt shard lands among the data).
+inline uint32_t decode_store_policy(int dst_pol, const void* data, uint64_t dbs, const void* parity, uint64_t pbs,
+                                    const void* out, uint64_t obs, uint64_t nblocks) {
+    return dst_pol == 3 && out && nblocks && regions_apart(data, dbs, out, obs, nblocks) &&
+                   regions_apart(parity, pbs, out, obs, nblocks)
+               ? 3u
+               : 0u;
+}
 
 // Bits [0, n) set, for n in [0, 32] (a present mask over n shards; 1u << 32 is undefined).
 __host__ __device__ inline uint32_t low_mask(uint32_t n) { return n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u); }
@@ -102,6 +127,7 @@ struct ReconArgs {
     // zero when no recoverable block has two or more erased data shards (the direct body runs), else
     // nonzero (the wave rebuild of the sorted plans runs)
     const uint32_t* route;
+    uint32_t sp;               // store policy of the RS(8,12) direct decode (decode_store_policy)
 };
 
 
@@ -154,12 +180,8 @@ struct Tuning {
     std::atomic<int> dst_pol{3};
     // resident workgroups per CU of the routed in-place kernel (0: as many as fit)
     std::atomic<int> route_wpc{0};
-    // threads per workgroup of the RS(8,12) encode and direct decode (256; 128 / 64: residency in
-    // finer steps)
-    std::atomic<int> enc_nt{256};
-    std::atomic<int> dir_nt{256};
 };
-constexpr int kTuningKeys = 17;   // fec__set_tuning keys 0..16, in the order above
+constexpr int kTuningKeys = 15;   // fec__set_tuning keys 0..14, in the order above
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):
 // halfway between 160K/(wpc+1) and 160K/wpc, never below what the kernel itself needs.

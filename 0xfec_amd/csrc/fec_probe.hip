@@ -217,10 +217,11 @@ extern "C" int fec_probe_encode_traffic(fec_ctx* ctx, int k, int m, size_t shard
     // bit-sliced kernel takes two chunks a lane, the twin one)
     if (wpc < 0) wpc = k >= 16 ? (int)g_tune.enc_bwpc : k == 2 ? 0 : (int)g_tune.enc_wpc;
     const size_t lds = occupancy_lds(wpc, k == 8 ? (size_t)m * k * 32 : 0);
-    // the encodes' store policy (knob st_pol: 1 sc1, 0 nt)
+    // the encodes' store policy for this layout (encode_store_policy)
+    a.sp = encode_store_policy(g_tune.st_pol, data, dbs, parity, pbs, nblocks);
 #define FEC_ENC_TWIN(K, M)                                                                              \
     do {                                                                                                \
-        if (g_tune.st_pol == 1)                                                                         \
+        if (a.sp == 1)                                                                                  \
             hipLaunchKernelGGL((probe_encode_kernel<K, M, 1>), dim3(grid), dim3(kThreads), lds, s, a); \
         else                                                                                            \
             hipLaunchKernelGGL((probe_encode_kernel<K, M, 0>), dim3(grid), dim3(kThreads), lds, s, a); \
@@ -269,7 +270,7 @@ extern "C" int fec_probe_recover_traffic(fec_ctx* ctx, int k, int m, size_t shar
     const size_t lds = occupancy_lds(wpc, (size_t)4 * 3 * k * 32);
     const uint32_t um = (uint32_t)m;
     if (k == 2) hipLaunchKernelGGL((probe_recover_kernel<2>), dim3(grid), dim3(kThreads), lds, s, a, um);
-    else if (k == 8 && g_tune.dst_pol == 3)
+    else if (k == 8 && decode_store_policy(g_tune.dst_pol, data, dbs, parity, pbs, out, out_bs, nblocks) == 3)
         hipLaunchKernelGGL((probe_recover_kernel<8, 3>), dim3(grid), dim3(kThreads), lds, s, a, um);
     else if (k == 8) hipLaunchKernelGGL((probe_recover_kernel<8>), dim3(grid), dim3(kThreads), lds, s, a, um);
     else if (k == 16) hipLaunchKernelGGL((probe_recover_kernel<16>), dim3(grid), dim3(kThreads), lds, s, a, um);

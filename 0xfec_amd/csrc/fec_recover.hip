@@ -83,7 +83,7 @@ __device__ __forceinline__ void direct_status_pass(const ReconArgs& a, uint32_t 
 // read from the code's coefficient table in device memory (a.single_coef, through the constant
 // address space: scalar loads), for codes whose rows do not fit the argument (RS(20,30): 1000
 // dwords).
-template <int K, int TAB, int SP = 0, int WGT = kThreads>
+template <int K, int TAB, int SP = 0>
 __device__ __forceinline__ void direct_body(const ReconArgs& a, const CoefWords& cwords, uint8_t* smem) {
     constexpr bool NTL = true, NTS = true;   // non-temporal loads and stores (see launch_rs_recover_direct)
     {
@@ -93,8 +93,8 @@ __device__ __forceinline__ void direct_body(const ReconArgs& a, const CoefWords&
         uint8_t* slice = smem + (size_t)wave * direct_wave_bytes(k);
         const uint32_t total = a.nblocks * a.cps;
         const uint32_t all = low_mask(k + m), kmask = low_mask(k);
-        direct_status_pass(a, k, vb * (WGT / 64) + wave, lane);
-        const uint32_t i0 = xcd_order() * WGT + (wave << 6);
+        direct_status_pass(a, k, vb * (kThreads / 64) + wave, lane);
+        const uint32_t i0 = xcd_order() * kThreads + (wave << 6);
         if (i0 >= total) return;
         const uint32_t bfirst = fdiv(i0, a.div_cps);
         const uint32_t nb = fdiv(min(i0 + 63u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
@@ -249,10 +249,10 @@ __device__ __forceinline__ void direct_body(const ReconArgs& a, const CoefWords&
     }
 }
 
-template <int K, int TAB, int SP = 0, int NT = kThreads>
-__global__ __launch_bounds__(NT) void rs_recover_direct_kernel(ReconArgs a, CoefWords cwords) {
+template <int K, int TAB, int SP = 0>
+__global__ __launch_bounds__(kThreads) void rs_recover_direct_kernel(ReconArgs a, CoefWords cwords) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    direct_body<K, TAB, SP, NT>(a, cwords, smem);
+    direct_body<K, TAB, SP>(a, cwords, smem);
 }
 
 // ------------------------------------------------------------------ routed in-place reconstruct
@@ -380,7 +380,7 @@ hipError_t launch_rs_reconstruct_routed(const ReconArgs& a, hipStream_t s) {
     const int wpc = g_tune.route_wpc;
     const size_t own = std::max(4 * direct_wave_bytes(a.k), 4 * wave_slice_bytes(a.k, a.maxe, a.lay.stride));
     const size_t lds = occupancy_lds(wpc, own);
-    const bool sp3 = g_tune.dst_pol == 3;
+    const bool sp3 = false;   // in place: nt stores (decode_store_policy)
 #define FEC_ROUTED(MAXE, SP) \
     hipLaunchKernelGGL((rs_reconstruct_routed_kernel<MAXE, 8, 1, SP>), dim3(flat), dim3(kThreads), lds, s, a, cw)
     if (a.maxe <= 4) {
@@ -394,18 +394,19 @@ hipError_t launch_rs_reconstruct_routed(const ReconArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int K, int TAB, int SP = 0, int NT = kThreads>
+template <int K, int TAB, int SP = 0>
 static hipError_t direct_launch(const ReconArgs& a0, const CoefWords& cw, hipStream_t s) {
     const uint64_t total = (uint64_t)a0.nblocks * a0.cps;
-    const int flat = (int)((total + NT - 1) / NT);
+    const int flat = (int)((total + kThreads - 1) / kThreads);
     if (flat == 0) return hipSuccess;
     // residency by shape: 3 workgroups/CU for k >= 8 (RS(8,12) with the masks by scalar loads,
     // profiles/r05/dec_twin_r05c.log: 5.88 TB/s at 3 against 5.82 at 4, 5.76 at 5, 5.37 at 2; with
     // a vector mask load 4 had been best, +3.6 % over uncapped; RS(16,24) / RS(20,30) 3, +1 %, r03i),
     // small codes uncapped
     const int wpc = g_tune.dir_wpc >= 0 ? (int)g_tune.dir_wpc : (a0.k >= 8 ? 3 : 0);
-    const size_t lds = occupancy_lds(wpc, (NT / 64) * direct_wave_bytes(a0.k));
-    hipLaunchKernelGGL((rs_recover_direct_kernel<K, TAB, SP, NT>), dim3(flat), dim3(NT), lds, s, a0, cw);
+    // (workgroups of 2 waves at 5 / 6 / 7 per CU: +2.1 / +0.5 / +1.1 % time, r06i)
+    const size_t lds = occupancy_lds(wpc, 4 * direct_wave_bytes(a0.k));
+    hipLaunchKernelGGL((rs_recover_direct_kernel<K, TAB, SP>), dim3(flat), dim3(kThreads), lds, s, a0, cw);
     return hipGetLastError();
 }
 
@@ -424,9 +425,7 @@ hipError_t launch_rs_recover_direct(const ReconArgs& a, hipStream_t s) {
         e = direct_launch<20, 2>(a, cw, s);
     else if (a.k == 16)
         e = direct_launch<16, 2>(a, cw, s);
-    else if (a.k == 8 && by_arg && g_tune.dst_pol == 3 && g_tune.dir_nt == 128)   // 2-wave workgroups (knob dir_nt)
-        e = direct_launch<8, 1, 3, 128>(a, cw, s);
-    else if (a.k == 8 && by_arg && g_tune.dst_pol == 3)   // nt sc1 stores (knob dst_pol; 0: nt)
+    else if (a.k == 8 && by_arg && a.sp == 3)   // nt sc1 stores (decode_store_policy; else nt)
         e = direct_launch<8, 1, 3>(a, cw, s);
     else if (a.k == 8)
         e = by_arg ? direct_launch<8, 1>(a, cw, s) : direct_launch<8, 0>(a, cw, s);

@@ -296,8 +296,6 @@ ENC_VARIANTS = {
     "generic": dict(enc_fixed=0),
     "generic_wpc2": dict(enc_fixed=0, gen_wpc=2),
     "stpol_nt": dict(enc_fixed=1, st_pol=0),
-    "nt128_wpc5": dict(enc_fixed=1, enc_nt=128, enc_wpc=5),
-    "nt64_wpc10": dict(enc_fixed=1, enc_nt=64, enc_wpc=10),
 }
 
 
@@ -344,7 +342,6 @@ DEC_VARIANTS = {
     "wpc2": dict(dir_wpc=2, dec_wpc=2),
     "noroute": dict(dec_route=0),
     "dstpol_nt": dict(dst_pol=0),
-    "dirnt128": dict(dir_nt=128, dir_wpc=5),
 }
 
 

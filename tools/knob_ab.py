@@ -6,7 +6,8 @@ stride) and compares every setting's output bytes with the first's.
 
 usage: knob_ab.py --k 8 --m 4 [--blocks N] [--multi E (e ~ U{1..E} of n lost; 0: one data
        shard)] [--slots S (output slots; 0: the largest data-loss count)] [--rounds R]
-       SETTING [SETTING ...]      a SETTING is knob=value[,knob=value...] or "default"
+       [--interleaved (one [B][k+m][S] array: parity slots among the data, the batch layer's
+       staging layout)] SETTING [SETTING ...]   a SETTING is knob=value[,knob=value...] or "default"
 """
 import argparse
 import importlib
@@ -32,6 +33,7 @@ def main():
     ap.add_argument("--slots", type=int, default=0)
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--interleaved", action="store_true")
     ap.add_argument("settings", nargs="+")
     args = ap.parse_args()
     import torch
@@ -42,9 +44,16 @@ def main():
     codec.prepare(k, m)
     g = torch.Generator(device="cuda")
     g.manual_seed(0x0FEC)
-    data = torch.empty((B, k, S), dtype=torch.uint8, device="cuda")
-    codec.synth_data(0x0FEC, 0, B, k, 1200, data.data_ptr(), k * S, S)
-    par = torch.zeros((B, m, S), dtype=torch.uint8, device="cuda")
+    if args.interleaved:
+        whole = torch.zeros((B, n, S), dtype=torch.uint8, device="cuda")
+        codec.synth_data(0x0FEC, 0, B, k, 1200, whole.data_ptr(), n * S, S)
+        dptr, pptr, dbs, pbs = whole.data_ptr(), whole.data_ptr() + k * S, n * S, n * S
+        data, par = whole, whole[:, k:]
+    else:
+        data = torch.empty((B, k, S), dtype=torch.uint8, device="cuda")
+        codec.synth_data(0x0FEC, 0, B, k, 1200, data.data_ptr(), k * S, S)
+        par = torch.zeros((B, m, S), dtype=torch.uint8, device="cuda")
+        dptr, pptr, dbs, pbs = data.data_ptr(), par.data_ptr(), k * S, m * S
     if args.multi:
         e = torch.randint(1, args.multi + 1, (B,), generator=g, device="cuda")
         rank = torch.rand((B, n), generator=g, device="cuda").argsort(dim=1).argsort(dim=1)
@@ -60,10 +69,10 @@ def main():
     settings = [parse(s) for s in args.settings]
 
     def enc():
-        codec.rs_encode_raw(k, m, L, B, data.data_ptr(), k * S, par.data_ptr(), m * S, S, fec.FEC_DEVICE)
+        codec.rs_encode_raw(k, m, L, B, dptr, dbs, pptr, pbs, S, fec.FEC_DEVICE)
 
     def rec():
-        rc = codec.rs_recover_raw(k, m, L, B, data.data_ptr(), k * S, par.data_ptr(), m * S, S, masks.data_ptr(),
+        rc = codec.rs_recover_raw(k, m, L, B, dptr, dbs, pptr, pbs, S, masks.data_ptr(),
                                   out.data_ptr(), slots * S, slots, None)
         assert rc == 0, rc
 

@@ -22,8 +22,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 L, S = 1202, 1216
 ROUTES = {"default": {}, "wave": {"dec_direct": 0}, "tile": {"dec_direct": 0, "dec_wave": 0},
-          "noroute": {"dec_route": 0}, "route_wpc3": {"route_wpc": 3},
-          "route_wpc4": {"route_wpc": 4}, "route_wpc5": {"route_wpc": 5}, "route_wpc0": {"route_wpc": 0}}
+          "noroute": {"dec_route": 0}, "direct_oop": {}, "route_wpc3": {"route_wpc": 3},
+          "route_wpc4": {"route_wpc": 4}, "route_wpc5": {"route_wpc": 5}, "route_wpc0": {"route_wpc": 0},
+          "route_wpc4_ntsc1": {"route_wpc": 4, "dst_pol": 5}}
 
 
 def main():
@@ -71,13 +72,18 @@ def main():
             # with the original data (and with each other) afterwards
             wiped = data.clone()
             wiped[lost[:, :k]] = 0x3C
-            outs = {r: wiped.clone() for r in routes}
+            outs = {r: wiped.clone() for r in routes if r != "direct_oop"}
         else:
-            outs = {r: torch.zeros((B, slots, S), dtype=torch.uint8, device="cuda") for r in routes}
+            outs = {r: torch.zeros((B, slots, S), dtype=torch.uint8, device="cuda") for r in routes if r != "direct_oop"}
+
+        oop = torch.zeros((B, 1, S), dtype=torch.uint8, device="cuda") if "direct_oop" in routes else None
 
         def dec(r):
             def fn():
-                if inplace:
+                if r == "direct_oop":   # reference: the out-of-place single-slot recover (bench.py's decode)
+                    rc = codec.rs_recover_raw(k, m, L, B, data.data_ptr(), k * S, par.data_ptr(), m * S, S,
+                                              masks.data_ptr(), oop.data_ptr(), S, 1, None)
+                elif inplace:
                     rc = codec.rs_reconstruct_raw(k, m, L, B, outs[r].data_ptr(), k * S, par.data_ptr(), m * S, S,
                                                   masks.data_ptr(), None, fec.FEC_DEVICE)
                 else:
@@ -105,9 +111,10 @@ def main():
                 res.setdefault(name, {}).setdefault(r, []).append(timed(dec(r)))
                 codec.set_tuning(**old)
         torch.cuda.synchronize()
-        same = all(torch.equal(outs[routes[0]], outs[r]) for r in routes)
+        cmp = [r for r in routes if r != "direct_oop"]
+        same = all(torch.equal(outs[cmp[0]], outs[r]) for r in cmp)
         if inplace:
-            same = same and all(torch.equal(outs[r][:, :, :L], data[:, :, :L]) for r in routes)
+            same = same and all(torch.equal(outs[r][:, :, :L], data[:, :, :L]) for r in cmp)
         med = {r: round(sorted(v)[len(v) // 2], 4) for r, v in res[name].items()}
         print(json.dumps({"code": name, "blocks": B, "routes_agree": same, "median_ms": med,
                           "TBps": {r: round(nbytes / t / 1e9, 3) for r, t in med.items()}}), flush=True)
