@@ -179,7 +179,7 @@ struct Tuning {
     std::atomic<int> st_pol{1};
     std::atomic<int> dst_pol{3};
     // resident workgroups per CU of the routed in-place kernel (0: as many as fit)
-    std::atomic<int> route_wpc{0};
+    std::atomic<int> route_wpc{4};
 };
 constexpr int kTuningKeys = 15;   // fec__set_tuning keys 0..14, in the order above
 

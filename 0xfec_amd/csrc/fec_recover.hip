@@ -374,9 +374,11 @@ hipError_t launch_rs_reconstruct_routed(const ReconArgs& a, hipStream_t s) {
     if (flat == 0) return hipSuccess;
     CoefWords cw{};
     memcpy(cw.w, a.single_coef_host, (size_t)a.k * a.m * ((a.k + 3) / 4) * 4);
-    // residency (knob route_wpc): uncapped, i.e. the wave body's 95 VGPRs (5 workgroups per CU). The
-    // direct body alone runs best at 3, the wave body at 5: at 3 the plan route lost 9-14 % on mixed
-    // batches, at 5 / uncapped the direct route gives up 1.2-2.3 % (profiles/r06/inplace_route_*.log)
+    // residency (knob route_wpc): 4 workgroups per CU. The direct body alone runs best at 3, the wave
+    // body at its VGPR limit of 5: at 3 the plan route lost 8-10 % on mixed batches, at 5 / uncapped
+    // the direct route kept only 0.4-2.9 % of its gain; at 4 single-erasure batches run 2.2-3.9 %
+    // faster than round 5's sorted-plan route and mixed ones within +-3 % of it
+    // (profiles/r06/inplace_route_r06g.log, _r06j)
     const int wpc = g_tune.route_wpc;
     const size_t own = std::max(4 * direct_wave_bytes(a.k), 4 * wave_slice_bytes(a.k, a.maxe, a.lay.stride));
     const size_t lds = occupancy_lds(wpc, own);
