@@ -382,17 +382,11 @@ hipError_t launch_rs_reconstruct_routed(const ReconArgs& a, hipStream_t s) {
     const int wpc = g_tune.route_wpc;
     const size_t own = std::max(4 * direct_wave_bytes(a.k), 4 * wave_slice_bytes(a.k, a.maxe, a.lay.stride));
     const size_t lds = occupancy_lds(wpc, own);
-    const bool sp3 = false;   // in place: nt stores (decode_store_policy)
-#define FEC_ROUTED(MAXE, SP) \
-    hipLaunchKernelGGL((rs_reconstruct_routed_kernel<MAXE, 8, 1, SP>), dim3(flat), dim3(kThreads), lds, s, a, cw)
-    if (a.maxe <= 4) {
-        if (sp3) FEC_ROUTED(4, 3);
-        else FEC_ROUTED(4, 0);
-    } else {
-        if (sp3) FEC_ROUTED(8, 3);
-        else FEC_ROUTED(8, 0);
-    }
-#undef FEC_ROUTED
+    // in place: nt stores (decode_store_policy)
+    if (a.maxe <= 4)
+        hipLaunchKernelGGL((rs_reconstruct_routed_kernel<4, 8, 1, 0>), dim3(flat), dim3(kThreads), lds, s, a, cw);
+    else
+        hipLaunchKernelGGL((rs_reconstruct_routed_kernel<8, 8, 1, 0>), dim3(flat), dim3(kThreads), lds, s, a, cw);
     return hipGetLastError();
 }
 

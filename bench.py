@@ -51,9 +51,14 @@ TRAFFIC_JSON = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
 
 def encode_kernel_name(k, m):
     """The kernel fec_rs_encode_batch runs for (k, m) at the library's default tuning
-    (fec_kernels.hpp Tuning: the fixed shapes run the flat fixed-shape kernel)."""
-    if (k, m) in ((2, 1), (8, 4), (16, 8)):
-        return "rs_encode_fixed_kernel<%d, %d" % (k, m)
+    (fec_encode.hip launch_rs_encode_fixed: RS(8,12) the dyadic fixed-shape kernel, RS(2,3) its
+    parity-row kernel, RS(16,24) / RS(20,30) the bit-sliced one, other shapes the generic kernel)."""
+    if (k, m) == (8, 4):
+        return "rs_encode_fixed_kernel<8, 4"
+    if (k, m) == (2, 1):
+        return "rs_encode23_kernel<"
+    if (k, m) in ((16, 8), (20, 10)):
+        return "rs_encode_bits_kernel<%d, %d" % (k, m)
     return "rs_encode_kernel<"
 
 
@@ -611,6 +616,8 @@ def main():
         dom_name = "decode"
         dominant, dom_bw, dom_bytes = "rs_recover_direct_kernel<%d" % k, dec_bw, dec_bytes
         traffic, traffic_src = committed_traffic("rs_recover_direct_kernel", "fec_recover.hip")
+    if traffic_src.get("kernel"):   # the instance the profile names (store policy in its template list)
+        dominant = traffic_src["kernel"].replace("void fk::", "").split("(")[0]
 
     if rank == 0:
         out = {
