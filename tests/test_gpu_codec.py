@@ -218,6 +218,81 @@ def test_argument_errors(codec, torch, fec):
     codec.sync()
 
 
+# FEC_DEVICE masks and statuses are read and written as 4-byte words (the kernels read the masks by
+# scalar loads, which drop the low two address bits): every reconstruct / recover entry point
+# refuses a mask or status array that is not 4-byte aligned (fec_hip.h), on every route, before
+# anything is enqueued.
+@pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8)])
+def test_misaligned_masks_and_status_refused(codec, torch, fec, k, m):
+    B, S, L = 8, 1216, 1202
+    n = k + m
+    sh = torch.zeros((B, n, S), dtype=torch.uint8, device="cuda")
+    mk = torch.zeros(B + 2, dtype=torch.int32, device="cuda")
+    st = torch.zeros(B + 2, dtype=torch.int32, device="cuda")
+    out = torch.zeros((B, 1, S), dtype=torch.uint8, device="cuda")
+    d, p = sh.data_ptr(), sh.data_ptr() + k * S
+    for ma, sa in ((mk.data_ptr() + 2, None), (mk.data_ptr(), st.data_ptr() + 1)):
+        assert codec.rs_reconstruct_raw(k, m, L, B, d, n * S, p, n * S, S, ma, sa, fec.FEC_DEVICE) == \
+            fec.FEC_ERR_ALIGNMENT
+        assert codec.rs_recover_raw(k, m, L, B, d, n * S, p, n * S, S, ma, out.data_ptr(), S, 1, sa) == \
+            fec.FEC_ERR_ALIGNMENT
+    assert fec.lib.fec_xor_reconstruct_batch(codec.handle, 2, L, B, d, 3 * S, d + 2 * S, 3 * S, S,
+                                             mk.data_ptr() + 1, None, fec.FEC_DEVICE) == fec.FEC_ERR_ALIGNMENT
+    codec.sync()
+
+
+# In-place RS(8,12) reconstructs take the routed form (fec_recover.hip): a classify pass, then the
+# direct single-erasure body when no recoverable block has two or more erased data shards, else the
+# sorted plans and the wave rebuild. Batches on either side of that line, with intact blocks,
+# parity-only losses and too-few-shards blocks mixed in, sizes around the classify pass's 256-block
+# sweep and the 64-block plan windows, against the oracle (data and statuses), on the routed form
+# and on round 5's sorted-plan route (dec_route 0).
+@pytest.mark.parametrize("route", [1, 0])
+@pytest.mark.parametrize("B", [1, 63, 257, 1031])
+@pytest.mark.parametrize("multi", [False, True])
+def test_rs_inplace_routed_matches_oracle(codec, oracle, torch, fec, tune, route, B, multi):
+    k, m, L, S = 8, 4, 1202, 1216
+    n = k + m
+    rng = np.random.default_rng(B * 7 + int(multi) + 10 * route)
+    sh = _rand_shards(rng, B, n, S, L)
+    oracle.rs_encode(k, m, sh)
+    masks = np.empty(B, dtype=np.uint32)
+    for b in range(B):
+        kind = int(rng.integers(0, 5))
+        if kind == 0:
+            lost = []                                                      # intact
+        elif kind == 1:
+            lost = [int(rng.integers(k, n))]                               # one parity shard
+        elif kind == 2 or (kind == 3 and not multi):
+            lost = [int(rng.integers(0, k))]                               # one data shard
+        elif kind == 3:
+            lost = list(rng.choice(n, size=int(rng.integers(2, m + 1)), replace=False))   # up to m shards
+        else:
+            lost = list(rng.choice(k, size=m + 1, replace=False))          # too few shards
+        masks[b] = ((1 << n) - 1) & ~sum(1 << int(i) for i in lost)
+    if multi:   # at least one block with two erased data shards (the plan route)
+        masks[B // 2] = ((1 << n) - 1) & ~0b101
+    dmg = sh.copy()
+    for b in range(B):
+        for i in range(n):
+            if not (masks[b] >> i) & 1:
+                dmg[b, i] = 0x3C
+    want = dmg.copy()
+    st_ref = oracle.rs_reconstruct(k, m, want, masks, length=L)
+    tune(dec_route=route)
+    d = torch.from_numpy(np.ascontiguousarray(dmg[:, :k])).cuda()
+    par = torch.from_numpy(np.ascontiguousarray(dmg[:, k:])).cuda()
+    st = torch.full((B,), 99, dtype=torch.int32, device="cuda")
+    codec.rs_reconstruct_split(k, m, d, par, torch.from_numpy(masks.view(np.int32)).cuda(), status=st,
+                               shard_len=L)
+    rc = codec.lib_sync_rc()
+    assert rc == (fec.FEC_ERR_TOO_FEW_SHARDS if (st_ref != 0).any() else fec.FEC_OK)
+    assert np.array_equal(st.cpu().numpy() == 0, st_ref == 0)
+    got = d.cpu().numpy()
+    ok = st_ref == 0
+    assert np.array_equal(got[ok][:, :, :L], sh[ok][:, :k, :L])
+
+
 @pytest.mark.parametrize("k,m", [(2, 1), (8, 4), (16, 8), (20, 10)])
 def test_rs_split_layout_matches_interleaved(codec, oracle, torch, k, m):
     """Data and parity in separate buffers (the bench layout) give the same bytes."""
