@@ -106,7 +106,11 @@ __global__ __launch_bounds__(kThreads) void probe_recover_kernel(RecoverProbeArg
         acc.w ^= x[j].w;
     }
     const uint32_t nb = min(a.len - c * kChunk, (uint32_t)kChunk);
-    st16p<SP>(a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk, keep_bytes(acc, nb));
+    // out == data: in place, into the erased shard's own slot (the routed in-place reconstruct's
+    // store); else the separate output (the recover's)
+    uint8_t* dst = a.out == a.data ? const_cast<uint8_t*>(d0) + (uint64_t)E0 * a.ss
+                                   : a.out + (uint64_t)blk * a.out_bs + (uint64_t)c * kChunk;
+    st16p<SP>(dst, keep_bytes(acc, nb));
     if (a.nin == 0x5A5A5A5Au) smem[0] = 1;   // never: keeps the LDS allocation
 }
 

@@ -13,7 +13,8 @@
  *   fec_probe_recover_traffic   the bytes and launch shape of fec_rs_recover_batch's direct
  *                               single-erasure kernel: per block the k-1 other data shards and the
  *                               first present parity, one store to out; blocks whose mask is not
- *                               a single data erasure move nothing
+ *                               a single data erasure move nothing. out == data: the store goes
+ *                               into the erased shard's own slot (the in-place reconstruct's)
  *   fec_probe_rebuild_traffic   the bytes of the multi-erasure decode of RS(16,24) / RS(20,30)
  *                               (sorted plans + rebuild): per block the first k present shards
  *                               and one store per erased data shard into out (block b, row r at
