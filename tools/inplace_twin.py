@@ -75,8 +75,9 @@ def main():
     for r in range(args.rounds):
         for name, fn in forms.items():
             res.setdefault(name, []).append(timed(fn))
-    # the in-place kernel rewrites every erased slot the in-place twin overwrote
+    # the kernels rewrite what the twins overwrote: every erased slot in place, and the output
     kern_inplace(4)()
+    kern_oop()
     codec.sync()
     rows = torch.arange(B, device="cuda")
     er = erased.long()
