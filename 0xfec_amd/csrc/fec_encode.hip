@@ -174,7 +174,9 @@ __device__ __forceinline__ void dy_encode_chunk(const uint4 (&x)[K], const uint8
 // bytes zeroed. (Round 6 measured a form with its loads decoupled from its arithmetic, each wave
 // walking T tiles with the next D tiles' shard chunks in flight as LDS-DMA loads into a ring:
 // 7-17 % slower than this flat grid at every residency, its traffic twin 7.5-9 % below the flat
-// twin; DESIGN.md 3, the kernel is in commit f1dd58a.)
+// twin; the kernel is in commit f1dd58a. A body with half the VALU ran no faster at 2 workgroups/CU
+// and slower at 3; leaf tables by scalar loads, with no LDS staging and no barrier, ran 5 % faster
+// at 2 and level at 3, where this kernel runs: DESIGN.md 3, r6 rows.)
 template <int K, int M, int SP = 0>
 __global__ __launch_bounds__(kThreads) void rs_encode_fixed_kernel(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];

@@ -5,6 +5,9 @@ Says whether the encode's access shape moves more at another residency than the 
 runs at, i.e. whether a form of the encode with more work per lane at lower residency could beat
 the ceiling the bench reports.
 
+(Round 6 ran it with two measurement-only forms beside the encode, knobs enc_lite and enc_scal,
+removed after: profiles/r06/twin_sweep_lite_r06n.log, twin_sweep_scal_r06o.log.)
+
 usage: twin_sweep.py [blocks]   (2^20 default)"""
 import importlib
 import json
@@ -18,7 +21,8 @@ def main():
     import torch
     fec = importlib.import_module("0xfec_amd")
     k, m, L, S = 8, 4, 1202, 1216
-    B = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+    pos = [x for x in sys.argv[1:] if not x.startswith("--")]
+    B = int(pos[0]) if pos else 1 << 20
     codec = fec.Codec(0).use_torch_stream()
     data = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device="cuda")
     par = torch.zeros((B, m, S), dtype=torch.uint8, device="cuda")
