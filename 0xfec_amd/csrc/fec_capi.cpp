@@ -1218,7 +1218,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
     std::atomic<int>* slots[fk::kTuningKeys] = {&t.enc_wpc,   &t.gen_wpc,    &t.dec_wpc,      &t.dir_wpc,
                                                 &t.enc_bwpc,  &t.enc_fixed,  &t.dec_wave,     &t.dec_direct,
                                                 &t.host_chunk, &t.host_threads, &t.bat_zc,     &t.dec_route,
-                                                &t.st_pol,     &t.dst_pol,    &t.route_wpc};
+                                                &t.st_pol,     &t.dst_pol,    &t.route_wpc,
+                                                &t.route_ww};
     if (key < 0 || key >= fk::kTuningKeys) return FEC_ERR_INVALID_ARG;
     return slots[key]->exchange(value);
 }

@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kThreads) void rs_reconstruct_kernel(ReconArgs a) {
 template <int MAXE, int K = 0>
 __global__ __launch_bounds__(kThreads) void rs_reconstruct_wave_kernel(ReconArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    wave_body<MAXE, K>(a, smem);
+    wave_body<MAXE, K>(a, smem, xcd_order());
 }
 
 hipError_t launch_rs_plan(const PlanArgs& a, hipStream_t s) {

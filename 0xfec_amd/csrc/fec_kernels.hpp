@@ -180,8 +180,12 @@ struct Tuning {
     std::atomic<int> dst_pol{3};
     // resident workgroups per CU of the routed in-place kernel (0: as many as fit)
     std::atomic<int> route_wpc{4};
+    // waves per workgroup that run the routed kernel's direct body (3: the fourth wave of each
+    // workgroup exits at once, so the direct route runs 12 of the 16 resident waves per CU, the
+    // direct body's best residency, while the plan route keeps 16; 4: all)
+    std::atomic<int> route_ww{3};
 };
-constexpr int kTuningKeys = 15;   // fec__set_tuning keys 0..14, in the order above
+constexpr int kTuningKeys = 16;   // fec__set_tuning keys 0..15, in the order above
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):
 // halfway between 160K/(wpc+1) and 160K/wpc, never below what the kernel itself needs.

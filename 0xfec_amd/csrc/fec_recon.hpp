@@ -185,8 +185,10 @@ __device__ __forceinline__ void wave_sync() {
 // LDS slice (no workgroup barrier), one item per lane. K: compile-time data shard count (0: runtime
 // a.k), all K input loads in flight before the first is folded (recon_item_k). The body of
 // rs_reconstruct_wave_kernel (fec_decode.hip) and of the routed kernel's plan route (fec_recover.hip).
+// order: the workgroup's place in the grid's item order (xcd_order() for a grid of exactly the
+// plan items' workgroups).
 template <int MAXE, int K = 0>
-__device__ __forceinline__ void wave_body(const ReconArgs& a, uint8_t* smem) {
+__device__ __forceinline__ void wave_body(const ReconArgs& a, uint8_t* smem, uint32_t order) {
     const uint32_t k = a.k, maxe = a.maxe;
     const PlanLayout lay = a.lay;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -194,7 +196,7 @@ __device__ __forceinline__ void wave_body(const ReconArgs& a, uint8_t* smem) {
     gf::PermTab* tabs = reinterpret_cast<gf::PermTab*>(slice);                     // 3*maxe*k
     uint8_t* plans = slice + (size_t)kWaveBlocks * maxe * k * sizeof(gf::PermTab);  // 3*stride
     const uint32_t total = a.nblocks * a.cps;
-    const uint32_t i0 = xcd_order() * kThreads + (wave << 6);
+    const uint32_t i0 = order * kThreads + (wave << 6);
     if (i0 >= total) return;
     const uint32_t bfirst = fdiv(i0, a.div_cps);
     const uint32_t nb = fdiv(min(i0 + 63u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3

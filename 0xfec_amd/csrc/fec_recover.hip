@@ -83,18 +83,21 @@ __device__ __forceinline__ void direct_status_pass(const ReconArgs& a, uint32_t 
 // read from the code's coefficient table in device memory (a.single_coef, through the constant
 // address space: scalar loads), for codes whose rows do not fit the argument (RS(20,30): 1000
 // dwords).
-template <int K, int TAB, int SP = 0>
+// WW: waves of the workgroup that take items (4: all; fewer: the others exit at once and the
+// workgroup covers WW * 64 items).
+template <int K, int TAB, int SP = 0, int WW = 4>
 __device__ __forceinline__ void direct_body(const ReconArgs& a, const CoefWords& cwords, uint8_t* smem) {
     constexpr bool NTL = true, NTS = true;   // non-temporal loads and stores (see launch_rs_recover_direct)
     {
         const uint32_t vb = blockIdx.x;
         const uint32_t k = K ? (uint32_t)K : a.k, m = a.m;
         const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        if (WW < kThreads / 64 && wave >= (uint32_t)WW) return;
         uint8_t* slice = smem + (size_t)wave * direct_wave_bytes(k);
         const uint32_t total = a.nblocks * a.cps;
         const uint32_t all = low_mask(k + m), kmask = low_mask(k);
-        direct_status_pass(a, k, vb * (kThreads / 64) + wave, lane);
-        const uint32_t i0 = xcd_order() * kThreads + (wave << 6);
+        direct_status_pass(a, k, vb * WW + wave, lane);
+        const uint32_t i0 = xcd_order() * (WW * 64u) + (wave << 6);
         if (i0 >= total) return;
         const uint32_t bfirst = fdiv(i0, a.div_cps);
         const uint32_t nb = fdiv(min(i0 + 63u, total - 1u), a.div_cps) - bfirst + 1;   // <= 3
@@ -281,12 +284,22 @@ __global__ __launch_bounds__(256) void rs_route_classify_kernel(const uint32_t* 
     if (threadIdx.x == 0 && found) atomicOr(route, 1u);
 }
 
-template <int MAXE, int DK, int TAB, int SP>
+// WW < 4 (knob route_ww): the direct route runs WW waves of each workgroup over a grid of
+// total / (WW * 64) workgroups; the plan route runs the first total / 256 of them, all four waves
+// each, in XCD order among themselves, and the rest exit at once.
+template <int MAXE, int DK, int TAB, int SP, int WW = 4>
 __global__ __launch_bounds__(kThreads) void rs_reconstruct_routed_kernel(ReconArgs a, CoefWords cwords) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     typedef __attribute__((address_space(4))) const uint32_t ConstU32;
-    if (*(ConstU32*)a.route == 0) direct_body<DK, TAB, SP>(a, cwords, smem);
-    else wave_body<MAXE, 0>(a, smem);
+    if (*(ConstU32*)a.route == 0) {
+        direct_body<DK, TAB, SP, WW>(a, cwords, smem);
+    } else if constexpr (WW == kThreads / 64) {
+        wave_body<MAXE, 0>(a, smem, xcd_order());
+    } else {
+        const uint32_t g4 = (a.nblocks * a.cps + kThreads - 1) / kThreads;
+        if (blockIdx.x >= g4) return;
+        wave_body<MAXE, 0>(a, smem, xcd_order_of(blockIdx.x, g4));
+    }
 }
 
 // RS(2,3) (k = 2, m = 1): a block is rebuilt from its other data shard and the parity with the
@@ -370,7 +383,8 @@ hipError_t launch_rs_route_classify(const ReconArgs& a, uint32_t* route, hipStre
 
 hipError_t launch_rs_reconstruct_routed(const ReconArgs& a, hipStream_t s) {
     const uint64_t total = (uint64_t)a.nblocks * a.cps;
-    const int flat = (int)((total + kThreads - 1) / kThreads);
+    const bool w3 = g_tune.route_ww == 3;
+    const int flat = (int)((total + (w3 ? 191 : kThreads - 1)) / (w3 ? 192 : kThreads));
     if (flat == 0) return hipSuccess;
     CoefWords cw{};
     memcpy(cw.w, a.single_coef_host, (size_t)a.k * a.m * ((a.k + 3) / 4) * 4);
@@ -378,15 +392,24 @@ hipError_t launch_rs_reconstruct_routed(const ReconArgs& a, hipStream_t s) {
     // body at its VGPR limit of 5: at 3 the plan route lost 8-10 % on mixed batches, at 5 / uncapped
     // the direct route kept only 0.4-2.9 % of its gain; at 4 single-erasure batches run 2.2-3.9 %
     // faster than round 5's sorted-plan route and mixed ones within +-3 % of it
-    // (profiles/r06/inplace_route_r06g.log, _r06j)
+    // (profiles/r06/inplace_route_r06g.log, _r06j). With three of each workgroup's waves on the
+    // direct route (knob route_ww 3, the default) the direct route runs at its own best residency
+    // (12 waves per CU) and the plan route keeps 16: one data shard lost 1.971 -> 1.930 ms (the
+    // out-of-place decode 1.896), U{1..4} 2.107 -> 2.063, U{1..2} level (inplace_ww3_r06r.log)
     const int wpc = g_tune.route_wpc;
     const size_t own = std::max(4 * direct_wave_bytes(a.k), 4 * wave_slice_bytes(a.k, a.maxe, a.lay.stride));
     const size_t lds = occupancy_lds(wpc, own);
     // in place: nt stores (decode_store_policy)
-    if (a.maxe <= 4)
+    if (w3) {
+        if (a.maxe <= 4)
+            hipLaunchKernelGGL((rs_reconstruct_routed_kernel<4, 8, 1, 0, 3>), dim3(flat), dim3(kThreads), lds, s, a, cw);
+        else
+            hipLaunchKernelGGL((rs_reconstruct_routed_kernel<8, 8, 1, 0, 3>), dim3(flat), dim3(kThreads), lds, s, a, cw);
+    } else if (a.maxe <= 4) {
         hipLaunchKernelGGL((rs_reconstruct_routed_kernel<4, 8, 1, 0>), dim3(flat), dim3(kThreads), lds, s, a, cw);
-    else
+    } else {
         hipLaunchKernelGGL((rs_reconstruct_routed_kernel<8, 8, 1, 0>), dim3(flat), dim3(kThreads), lds, s, a, cw);
+    }
     return hipGetLastError();
 }
 

@@ -675,8 +675,8 @@ def main():
                                    "GB/s": round(dec_bytes / (inplace_ms / 1e3) / 1e9, 1),
                                    "api": "fec_rs_reconstruct_batch in place, not in the step: classify pass (one "
                                           "word: does a block need a multi-erasure plan?), then rs_reconstruct_routed_kernel, "
-                                          "which on this single-erasure batch runs the direct body (the sorted plan kernel "
-                                          "exits at once)"},
+                                          "which on this single-erasure batch runs the direct body on three waves of each "
+                                          "workgroup (the sorted plan kernel exits at once)"},
                 "step_frac": round((enc_bytes + dec_bytes) / ((enc_ms + dec_ms) / 1000.0) / HBM_PEAK, 4),
             },
             "check": {"roundtrip_full_batch": ok_roundtrip, "encode_vs_oracle_64_blocks": ok_parity,

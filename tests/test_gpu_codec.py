@@ -246,8 +246,13 @@ def test_misaligned_masks_and_status_refused(codec, torch, fec, k, m):
 # sorted plans and the wave rebuild. Batches on either side of that line, with intact blocks,
 # parity-only losses and too-few-shards blocks mixed in, sizes around the classify pass's 256-block
 # sweep and the 64-block plan windows, against the oracle (data and statuses), on the routed form
-# and on round 5's sorted-plan route (dec_route 0).
-@pytest.mark.parametrize("route", [1, 0])
+# on round 5's sorted-plan route (dec_route 0), and on the routed form whose direct route runs all
+# four waves of each workgroup (route_ww 4; the default runs three over a larger grid, the plan
+# route on its first total / 256 workgroups).
+ROUTE_FORMS = {0: dict(dec_route=0), 1: dict(dec_route=1), 2: dict(dec_route=1, route_ww=4)}
+
+
+@pytest.mark.parametrize("route", [1, 0, 2])
 @pytest.mark.parametrize("B", [1, 63, 257, 1031])
 @pytest.mark.parametrize("multi", [False, True])
 def test_rs_inplace_routed_matches_oracle(codec, oracle, torch, fec, tune, route, B, multi):
@@ -279,7 +284,7 @@ def test_rs_inplace_routed_matches_oracle(codec, oracle, torch, fec, tune, route
                 dmg[b, i] = 0x3C
     want = dmg.copy()
     st_ref = oracle.rs_reconstruct(k, m, want, masks, length=L)
-    tune(dec_route=route)
+    tune(**ROUTE_FORMS[route])
     d = torch.from_numpy(np.ascontiguousarray(dmg[:, :k])).cuda()
     par = torch.from_numpy(np.ascontiguousarray(dmg[:, k:])).cuda()
     st = torch.full((B,), 99, dtype=torch.int32, device="cuda")

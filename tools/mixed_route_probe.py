@@ -23,7 +23,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 L, S = 1202, 1216
 ROUTES = {"default": {}, "wave": {"dec_direct": 0}, "tile": {"dec_direct": 0, "dec_wave": 0},
           "noroute": {"dec_route": 0}, "direct_oop": {}, "route_wpc3": {"route_wpc": 3},
-          "route_wpc4": {"route_wpc": 4}, "route_wpc5": {"route_wpc": 5}, "route_wpc0": {"route_wpc": 0}}
+          "route_wpc4": {"route_wpc": 4}, "route_wpc5": {"route_wpc": 5}, "route_wpc0": {"route_wpc": 0},
+          "route_ww3": {"route_ww": 3}, "route_ww3_wpc5": {"route_ww": 3, "route_wpc": 5},
+          "route_ww4": {"route_ww": 4}}
 
 
 def main():
