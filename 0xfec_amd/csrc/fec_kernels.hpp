@@ -154,8 +154,8 @@ struct XorArgs {
 struct Tuning {
     // resident workgroups per CU (dynamic-LDS caps, occupancy_lds; 0 = as many as fit)
     std::atomic<int> enc_wpc{3};    // RS(8,12) fixed-shape encode (2 / 4 / uncapped slower)
-    std::atomic<int> gen_wpc{0};    // generic RS encode and XOR encode
-    std::atomic<int> dec_wpc{0};    // plan-path rebuilds and XOR reconstruct
+    std::atomic<int> gen_wpc{0};    // generic RS encode
+    std::atomic<int> dec_wpc{0};    // plan-path rebuilds
     std::atomic<int> dir_wpc{-1};   // direct single-erasure decode; -1: by shape (k >= 8: 3, else 0)
     std::atomic<int> enc_bwpc{0};   // bit-sliced encode (RS(16,24), RS(20,30))
     // routing among shipped kernels (tests)
@@ -184,8 +184,9 @@ struct Tuning {
     // workgroup exits at once, so the direct route runs 12 of the 16 resident waves per CU, the
     // direct body's best residency, while the plan route keeps 16; 4: all)
     std::atomic<int> route_ww{3};
+    std::atomic<int> xor_wpc{6};    // XOR encode and reconstruct (fec_xor.hip)
 };
-constexpr int kTuningKeys = 16;   // fec__set_tuning keys 0..15, in the order above
+constexpr int kTuningKeys = 17;   // fec__set_tuning keys 0..16, in the order above
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):
 // halfway between 160K/(wpc+1) and 160K/wpc, never below what the kernel itself needs.

@@ -8,20 +8,35 @@ namespace fk {
 // KG = inputs loaded back to back per group (2, 4 or 8, the smallest that covers k, or 8 for
 // k > 8): a group issues exactly the loads it uses except for clamped repeats in the last
 // group, so XOR(2,1) issues 2 loads per item, not 8.
-template <int KG>
+// BF: branch-free, an input past `valid` (a clamped repeat) is masked out, not skipped. With a
+// branch around its fold (BF false) the compiler sinks the load into the branch, so the group's
+// loads go out one round trip after another (load, wait, fold, load, wait, fold). The reconstruct
+// folds branch-free (at 6 workgroups/CU 0.625 against 0.652 ms, 2^20 XOR(2,1) blocks); the encode
+// keeps the branching fold, whose one load at a time runs 1.2 % faster at 6 workgroups/CU (0.601
+// against 0.608 ms) though 6 % slower at 4 (profiles/r06/xor_ab_fold_r06u.log, _r06v).
+template <int KG, bool BF>
 __device__ __forceinline__ void xor_fold(uint4& acc, const uint4 (&x)[KG], uint32_t valid) {
 #pragma unroll
-    for (int jj = 0; jj < KG; ++jj)
-        if ((uint32_t)jj < valid) {
-            acc.x ^= x[jj].x;
-            acc.y ^= x[jj].y;
-            acc.z ^= x[jj].z;
-            acc.w ^= x[jj].w;
+    for (int jj = 0; jj < KG; ++jj) {
+        if constexpr (!BF) {
+            if ((uint32_t)jj < valid) {
+                acc.x ^= x[jj].x;
+                acc.y ^= x[jj].y;
+                acc.z ^= x[jj].z;
+                acc.w ^= x[jj].w;
+            }
+            continue;
         }
+        const uint32_t keep = (uint32_t)jj < valid ? ~0u : 0u;
+        acc.x ^= x[jj].x & keep;
+        acc.y ^= x[jj].y & keep;
+        acc.z ^= x[jj].z & keep;
+        acc.w ^= x[jj].w & keep;
+    }
 }
 
 // Flat grids (one item per lane), non-temporal loads and stores.
-template <int KG>
+template <int KG, bool BF>
 __global__ __launch_bounds__(kThreads) void xor_encode_kernel(XorArgs a) {
     constexpr bool NTL = true, NTS = true;
     const uint32_t k = a.k;
@@ -35,13 +50,13 @@ __global__ __launch_bounds__(kThreads) void xor_encode_kernel(XorArgs a) {
             uint4 x[KG];
 #pragma unroll
             for (int jj = 0; jj < KG; ++jj) x[jj] = ld16<NTL>(src + (uint64_t)min(j0 + jj, k - 1) * a.ss);
-            xor_fold<KG>(acc, x, k - j0);
+            xor_fold<KG, BF>(acc, x, k - j0);
         }
         store_chunk<NTS>(a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk, acc, a.len - c * kChunk);
     }
 }
 
-template <int KG>
+template <int KG, bool BF>
 __global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
     constexpr bool NTL = true, NTS = true;
     const uint32_t k = a.k, n = k + 1;
@@ -69,7 +84,11 @@ __global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
     uint32_t mk;
     if (a.cps >= 32) {   // the wave's <= 3 masks by scalar loads, off the vector memory path
         const uint32_t bfirst = fdiv(i0, a.div_cps);
-        mk = wave_masks(a.masks, bfirst, a.nblocks).of(b - bfirst);
+        const WaveMasks wm = wave_masks(a.masks, bfirst, a.nblocks);
+        // all three in flight together: left alone, the compiler sank the second and third load
+        // into the lanes' select branches, one wait each
+        asm volatile("" ::"s"(wm.m0), "s"(wm.m1), "s"(wm.m2));
+        mk = wm.of(b - bfirst);
     } else {
         mk = a.masks[b];
     }
@@ -89,15 +108,15 @@ __global__ __launch_bounds__(kThreads) void xor_reconstruct_kernel(XorArgs a) {
             const uint32_t s = j + (j >= mi);     // the k shards other than the missing one
             x[jj] = ld16<NTL>(s < k ? blk + (uint64_t)s * a.ss : par);
         }
-        xor_fold<KG>(acc, x, k - j0);
+        xor_fold<KG, BF>(acc, x, k - j0);
     }
     store_chunk<NTS>(blk + (uint64_t)mi * a.ss, acc, a.len - c * kChunk);
 }
 
 template <int KG>
 static void xor_launch(const XorArgs& a, int grid, size_t lds, bool encode, hipStream_t s) {
-    if (encode) hipLaunchKernelGGL((xor_encode_kernel<KG>), dim3(grid), dim3(kThreads), lds, s, a);
-    else hipLaunchKernelGGL((xor_reconstruct_kernel<KG>), dim3(grid), dim3(kThreads), lds, s, a);
+    if (encode) hipLaunchKernelGGL((xor_encode_kernel<KG, false>), dim3(grid), dim3(kThreads), lds, s, a);
+    else hipLaunchKernelGGL((xor_reconstruct_kernel<KG, true>), dim3(grid), dim3(kThreads), lds, s, a);
 }
 
 static hipError_t xor_dispatch(const XorArgs& a, int grid, size_t lds, bool encode, hipStream_t s) {
@@ -107,14 +126,17 @@ static hipError_t xor_dispatch(const XorArgs& a, int grid, size_t lds, bool enco
     return hipGetLastError();
 }
 
+// residency (knob xor_wpc): 6 workgroups/CU for both kernels. XOR(2,1), 2^20 blocks, against as
+// many as fit (8): encode 0.601 against 0.618 ms, reconstruct 0.625 against 0.630, its in-place
+// traffic twin 0.618 at 6 (profiles/r06/xor_ab_*_r06*.log)
 hipError_t launch_xor_encode(const XorArgs& a, int grid, hipStream_t s) {
-    return xor_dispatch(a, grid, occupancy_lds(g_tune.gen_wpc, 0), true, s);
+    return xor_dispatch(a, grid, occupancy_lds(g_tune.xor_wpc, 0), true, s);
 }
 
 // (XOR(2,1) by a one-item-per-lane kernel of its own measured 0.7 % slower, r04m: the gap to the
 // XOR twin is the in-place write, not the loop)
 hipError_t launch_xor_reconstruct(const XorArgs& a, int grid, hipStream_t s) {
-    return xor_dispatch(a, grid, occupancy_lds(g_tune.dec_wpc, 0), false, s);
+    return xor_dispatch(a, grid, occupancy_lds(g_tune.xor_wpc, 0), false, s);
 }
 
 }  // namespace fk

@@ -160,11 +160,14 @@ def test_rs_host_path_matches_oracle(codec, oracle, k, m):
     assert np.array_equal(dmg[:, :k], sh[:, :k])
 
 
+@pytest.mark.parametrize("wpc", [6, 0])
 @pytest.mark.parametrize("k", [1, 2, 3, 5, 9, 31])
 @pytest.mark.parametrize("L", [1, 6, 18, 513, 1202, 1436])
-def test_xor_device_matches_oracle(codec, oracle, torch, fec, k, L):
+def test_xor_device_matches_oracle(codec, oracle, torch, fec, tune, wpc, k, L):
     # L = 513: 33 chunks per shard, so a wave's 64 items span three blocks (the reconstruct's
-    # scalar mask loads take up to three); L < 497: the per-lane mask load
+    # scalar mask loads take up to three); L < 497: the per-lane mask load. wpc: the shipped
+    # residency of both XOR kernels (6 workgroups/CU) and as many as fit
+    tune(xor_wpc=wpc)
     rng = np.random.default_rng(k + L)
     n = k + 1
     S = (L + 15) // 16 * 16
