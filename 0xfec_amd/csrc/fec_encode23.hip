@@ -61,8 +61,9 @@ hipError_t launch_rs_encode23(const EncodeArgs& a, hipStream_t s) {
     const uint32_t chunks = (a.total + kThreads - 1) / kThreads;
     if (chunks == 0) return hipSuccess;
     // stores by the call's policy (a.sp: fec_kernels.hpp encode_store_policy)
-    if (a.sp == 1) hipLaunchKernelGGL(rs_encode23_kernel<1>, dim3(chunks), dim3(kThreads), 0, s, a);
-    else hipLaunchKernelGGL(rs_encode23_kernel<0>, dim3(chunks), dim3(kThreads), 0, s, a);
+    const size_t lds = occupancy_lds(g_tune.gen_wpc, 0);
+    if (a.sp == 1) hipLaunchKernelGGL(rs_encode23_kernel<1>, dim3(chunks), dim3(kThreads), lds, s, a);
+    else hipLaunchKernelGGL(rs_encode23_kernel<0>, dim3(chunks), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 

@@ -154,7 +154,7 @@ struct XorArgs {
 struct Tuning {
     // resident workgroups per CU (dynamic-LDS caps, occupancy_lds; 0 = as many as fit)
     std::atomic<int> enc_wpc{3};    // RS(8,12) fixed-shape encode (2 / 4 / uncapped slower)
-    std::atomic<int> gen_wpc{0};    // generic RS encode
+    std::atomic<int> gen_wpc{0};    // generic RS encode and the RS(2,3) encode
     std::atomic<int> dec_wpc{0};    // plan-path rebuilds
     std::atomic<int> dir_wpc{-1};   // direct single-erasure decode; -1: by shape (k >= 8: 3, else 0)
     std::atomic<int> enc_bwpc{0};   // bit-sliced encode (RS(16,24), RS(20,30))
