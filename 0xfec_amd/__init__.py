@@ -201,7 +201,7 @@ class Codec:
     TUNING_KEYS = {"enc_wpc": 0, "gen_wpc": 1, "dec_wpc": 2, "dir_wpc": 3, "enc_bwpc": 4, "enc_fixed": 5,
                    "dec_wave": 6, "dec_direct": 7, "host_chunk": 8, "host_threads": 9, "bat_zc": 10,
                    "dec_route": 11, "st_pol": 12, "dst_pol": 13,
-                   "route_wpc": 14, "route_ww": 15, "xor_wpc": 16}
+                   "route_wpc": 14, "route_ww": 15, "xor_wpc": 16, "enc_ww": 17}
 
     def set_tuning(self, **knobs):
         """Set kernel-selection knobs; returns the previous values (pass them back to restore)."""

@@ -1219,7 +1219,8 @@ int fec__set_tuning(fec_ctx* ctx, int key, int value) {
                                                 &t.enc_bwpc,  &t.enc_fixed,  &t.dec_wave,     &t.dec_direct,
                                                 &t.host_chunk, &t.host_threads, &t.bat_zc,     &t.dec_route,
                                                 &t.st_pol,     &t.dst_pol,    &t.route_wpc,
-                                                &t.route_ww,   &t.xor_wpc};
+                                                &t.route_ww,   &t.xor_wpc,
+                                                &t.enc_ww};
     if (key < 0 || key >= fk::kTuningKeys) return FEC_ERR_INVALID_ARG;
     return slots[key]->exchange(value);
 }

@@ -177,22 +177,52 @@ __device__ __forceinline__ void dy_encode_chunk(const uint4 (&x)[K], const uint8
 // twin; the kernel is in commit f1dd58a. A body with half the VALU ran no faster at 2 workgroups/CU
 // and slower at 3; leaf tables by scalar loads, with no LDS staging and no barrier, ran 5 % faster
 // at 2 and level at 3, where this kernel runs: DESIGN.md 3, r6 rows.)
-template <int K, int M, int SP = 0>
+// WW < 4 (knob enc_ww, default 3): WW waves of each workgroup take items (the workgroup covers
+// WW * 64), the others stage their table words and exit after the barrier; the working lanes issue
+// their shard loads before the table staging and the barrier, so the prologue runs under them.
+template <int K, int M, int SP = 0, int WW = 4>
 __global__ __launch_bounds__(kThreads) void rs_encode_fixed_kernel(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    {
-        uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
-        for (uint32_t i = threadIdx.x; i < (uint32_t)(M * K * 8); i += kThreads) dst[i] = a.dytabs[i];
-        __syncthreads();
-    }
-    const uint32_t it = xcd_order() * kThreads + threadIdx.x;
-    if (it >= a.total) return;
-    const uint32_t b = fdiv(it, a.div_cps);
-    const uint32_t c = it - b * a.cps;
-    const uint8_t* src = a.in + (uint64_t)b * a.in_bs + (uint64_t)c * kChunk;
     uint4 x[K];
+    uint32_t b, c;
+    if constexpr (WW < kThreads / 64) {
+        static_assert(M * K * 8 == kThreads, "one leaf-table word per thread");
+        const uint32_t wave = threadIdx.x >> 6;
+        // every kernel argument in one scalar round trip
+        const uint32_t order = xcd_order();
+        asm volatile("" ::"s"(a.in), "s"(a.in_bs), "s"(a.ss), "s"(a.total), "s"(a.cps), "s"(a.div_cps.magic),
+                     "s"(a.div_cps.shift), "s"(a.dytabs), "s"(order));
+        const uint32_t tw = a.dytabs[threadIdx.x];
+        const uint32_t it = order * (WW * 64u) + threadIdx.x;
+        const bool live = wave < (uint32_t)WW && it < a.total;
+        const uint32_t itc = min(it, a.total - 1u);
+        b = fdiv(itc, a.div_cps);
+        c = itc - b * a.cps;
+        // unconditional loads (a lane past the end re-reads the last item, an idle wave one table
+        // line): the table word's wait then counts only itself (vmcnt K), not the shard loads
+        const bool work = wave < (uint32_t)WW;
+        const uint8_t* src = work ? a.in + (uint64_t)b * a.in_bs + (uint64_t)c * kChunk
+                                  : reinterpret_cast<const uint8_t*>(a.dytabs);
+        const uint64_t ss = work ? a.ss : 0;
 #pragma unroll
-    for (int j = 0; j < K; ++j) x[j] = ld16<true>(src + (uint64_t)j * a.ss);
+        for (int j = 0; j < K; ++j) x[j] = ld16<true>(src + (uint64_t)j * ss);
+        reinterpret_cast<uint32_t*>(smem)[threadIdx.x] = tw;
+        __syncthreads();
+        if (!live) return;
+    } else {
+        {
+            uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
+            for (uint32_t i = threadIdx.x; i < (uint32_t)(M * K * 8); i += kThreads) dst[i] = a.dytabs[i];
+            __syncthreads();
+        }
+        const uint32_t it = xcd_order() * kThreads + threadIdx.x;
+        if (it >= a.total) return;
+        b = fdiv(it, a.div_cps);
+        c = it - b * a.cps;
+        const uint8_t* src = a.in + (uint64_t)b * a.in_bs + (uint64_t)c * kChunk;
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[j] = ld16<true>(src + (uint64_t)j * a.ss);
+    }
     uint32_t acc[M][4];
     dy_encode_chunk<K, M>(x, smem, acc);
     uint8_t* dst = a.out + (uint64_t)b * a.out_bs + (uint64_t)c * kChunk;
@@ -350,7 +380,11 @@ hipError_t launch_rs_encode_fixed(const EncodeArgs& a, hipStream_t s) {
     if (a.k == 16 && a.m == 8) return enc_bits_dispatch<16, 8>(a, s);
     if (a.k == 20 && a.m == 10) return enc_bits_dispatch<20, 10>(a, s);
     if (a.k == 8 && a.m == 4 && a.dytabs) {
-        // 3 workgroups per CU (knob enc_wpc; DESIGN.md 3: the flat grid at 3 beats 2, 4 and uncapped)
+        // 3 workgroups per CU (knob enc_wpc; DESIGN.md 3: the flat grid at 3 beats 2, 4 and uncapped),
+        // three of each workgroup's waves taking items (knob enc_ww): 9 working waves per CU with
+        // the shard loads issued before the table staging and barrier, -1.1 / -1.3 % time against
+        // four waves on two boxes (profiles/r06/enc_ww_ab_r06ww.log, _r06ww2); 2 working waves at 3 / 4
+        // workgroups per CU +11 / +4 %
         const int grid = (int)((a.total + kThreads - 1) / kThreads);
         const size_t lds = occupancy_lds(g_tune.enc_wpc, (size_t)a.m * a.k * sizeof(gf::PermTab));
         // parity stored with sc1 (a.sp 1, encode_store_policy: the line leaves the XCD's L2; -1.4 to
@@ -358,7 +392,16 @@ hipError_t launch_rs_encode_fixed(const EncodeArgs& a, hipStream_t s) {
         // (workgroups of 2 or 1 waves, residency in steps of 8 / 4 waves per CU: 2.49-2.67 ms against
         // 2.43 at 3 workgroups of 4 waves, profiles/r06/enc_nt_ab_r06h.log)
         if (a.sp == 1) {
-            hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4, 1>), dim3(grid), dim3(kThreads), lds, s, a);
+            const int ww = g_tune.enc_ww;
+            if (ww == 2 || ww == 3) {
+                const int g2 = (int)((a.total + 64u * ww - 1) / (64u * ww));
+                if (ww == 2)
+                    hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4, 1, 2>), dim3(g2), dim3(kThreads), lds, s, a);
+                else
+                    hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4, 1, 3>), dim3(g2), dim3(kThreads), lds, s, a);
+            } else {
+                hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4, 1>), dim3(grid), dim3(kThreads), lds, s, a);
+            }
         } else {
             hipLaunchKernelGGL((rs_encode_fixed_kernel<8, 4>), dim3(grid), dim3(kThreads), lds, s, a);
         }

@@ -185,8 +185,11 @@ struct Tuning {
     // direct body's best residency, while the plan route keeps 16; 4: all)
     std::atomic<int> route_ww{3};
     std::atomic<int> xor_wpc{6};    // XOR encode and reconstruct (fec_xor.hip)
+    // waves per workgroup that take items in the RS(8,12) encode (3: the fourth stages its table
+    // words and exits, 9 working waves per CU at 3 workgroups/CU, shard loads before the barrier; 4: all)
+    std::atomic<int> enc_ww{3};
 };
-constexpr int kTuningKeys = 17;   // fec__set_tuning keys 0..16, in the order above
+constexpr int kTuningKeys = 18;   // fec__set_tuning keys 0..17, in the order above
 
 // Dynamic LDS that caps residency at `wpc` workgroups per CU (160 KiB of LDS per CU on gfx950):
 // halfway between 160K/(wpc+1) and 160K/wpc, never below what the kernel itself needs.

@@ -379,6 +379,8 @@ ENC_VARIANTS = {
     "generic": dict(enc_fixed=0),
     "generic_wpc2": dict(enc_fixed=0, gen_wpc=2),
     "stpol_nt": dict(enc_fixed=1, st_pol=0),
+    "ww2_wpc4": dict(enc_fixed=1, enc_ww=2, enc_wpc=4),
+    "ww4": dict(enc_fixed=1, enc_ww=4),
 }
 
 
