@@ -382,8 +382,9 @@ hipError_t launch_rs_encode_fixed(const EncodeArgs& a, hipStream_t s) {
     if (a.k == 8 && a.m == 4 && a.dytabs) {
         // 3 workgroups per CU (knob enc_wpc; DESIGN.md 3: the flat grid at 3 beats 2, 4 and uncapped),
         // three of each workgroup's waves taking items (knob enc_ww): 9 working waves per CU with
-        // the shard loads issued before the table staging and barrier, -1.1 / -1.3 % time against
-        // four waves on two boxes (profiles/r06/enc_ww_ab_r06ww.log, _r06ww2); 2 working waves at 3 / 4
+        // the shard loads issued before the table staging and barrier, -1.1 / -1.3 / -1.1 % time
+        // against four waves on three boxes (profiles/r06/enc_ww_ab_r06ww.log, _r06ww2,
+        // enc_ww_stpol_ab_r06st.log); 2 working waves at 3 / 4
         // workgroups per CU +11 / +4 %
         const int grid = (int)((a.total + kThreads - 1) / kThreads);
         const size_t lds = occupancy_lds(g_tune.enc_wpc, (size_t)a.m * a.k * sizeof(gf::PermTab));
